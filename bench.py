@@ -1,0 +1,134 @@
+#!/usr/bin/env python3
+"""Headline benchmark: 2D domain-decomposed stencil, Gcells/s over N MI355X GPUs.
+
+BASELINE.json metric: "2D stencil Gcells/sec at 1/2/4/8 GPUs; GPU-GPU pingpong
+GB/s + µs latency". Config: the BASELINE 8-GPU problem — a 32768 x 32768 fp32
+periodic grid, 5-point Jacobi, decomposed over a Cartesian process grid (2x4 on
+8 GPUs; 1x1, 1x2, 2x2 below), halo exchange by native RCCL point-to-point over
+xGMI overlapped with the interior update. The global grid is fixed as N grows
+(strong scaling). Random-init synthetic data (deterministic per global cell).
+
+One step = one full Jacobi iteration of the global grid: halo exchange (pack ->
+RCCL send/recv per peer -> unpack) + stencil update of every core cell + buffer
+swap. W untimed warm-up steps, then K timed steps bracketed by barrier +
+device synchronisation on both sides; the time is the max over ranks.
+
+    python bench.py                       # N=1
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+
+Extras (not the headline number): on N=1 the BASELINE single-GPU config
+(8192^2 fp32); on N>=2 an RCCL ping-pong between ranks 0 and 1 (latency at 8 B,
+bandwidth at 256 MiB).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def _ms(x):
+    return round(x * 1e3, 4)
+
+
+def timed_run(st, ctx, steps: int, warmup: int) -> float:
+    st.run(warmup)
+    st.synchronize()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st.run(steps)
+    st.synchronize()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t1 = time.perf_counter()
+    return ctx.allreduce_max(t1 - t0)
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--global", dest="global_", default="32768x32768")
+    p.add_argument("--dims", default=None, help="process grid RxC (default: 1x1, 1x2, 2x2, 2x4)")
+    p.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    p.add_argument("--variant", default="auto", choices=["auto", "roll", "lds"])
+    p.add_argument("--no-overlap", action="store_true")
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-extras", action="store_true")
+    args = p.parse_args(argv)
+
+    from cuda_mpi_scratch_amd.models.pingpong import PingPong
+    from cuda_mpi_scratch_amd.models.stencil2d import Stencil2D, StencilConfig
+    from cuda_mpi_scratch_amd.parallel import choose_dims, init as dist_init
+
+    ctx = dist_init(backend="nccl" if torch.cuda.is_available() else "gloo")
+    n = ctx.world_size
+    if n != args.gpus and ctx.is_root:
+        print(f"warning: --gpus {args.gpus} but world size {n}", file=sys.stderr)
+    rows, cols = choose_dims(n, args.dims, prefer="wide")
+    gw, gh = (int(v) for v in args.global_.lower().split("x"))
+    cfg = StencilConfig(global_width=gw, global_height=gh, dims=f"{rows}x{cols}", dtype=args.dtype,
+                        kind="jacobi5", backend="auto", overlap=not args.no_overlap, graph=not args.no_graph,
+                        variant=args.variant)
+    st = Stencil2D(cfg, ctx)
+    dt = timed_run(st, ctx, args.steps, args.warmup)
+    value = st.cells_per_step * args.steps / dt / 1e9
+    extras: dict = {"backend": st.backend, "graph": st.graph_status(),
+                    "tile": f"{st.decomp.width}x{st.decomp.height}"}
+    del st
+    torch.cuda.empty_cache()
+
+    if not args.no_extras:
+        if n == 1:
+            cfg1 = StencilConfig(global_width=8192, global_height=8192, dims="1x1", dtype="f32")
+            st1 = Stencil2D(cfg1, ctx)
+            dt1 = timed_run(st1, ctx, 500, 50)
+            extras["stencil_8192sq_f32_1gpu_gcells_per_s"] = round(st1.cells_per_step * 500 / dt1 / 1e9, 2)
+            del st1
+        else:
+            pp = PingPong(ctx, "rccl", 256 << 20)
+            small = pp.run(8, "async", 20, 200)
+            big = pp.run(256 << 20, "async", 3, 20)
+            if ctx.is_root:
+                extras["pingpong_8B_latency_us"] = round(small.get("latency_us", 0.0), 2)
+                extras["pingpong_256MiB_gbps"] = round(big.get("gbps", 0.0), 2)
+                extras["pingpong_verified"] = bool(small.get("passed")) and bool(big.get("passed"))
+            del pp
+        ctx.barrier()
+
+    if ctx.is_root:
+        line = {
+            "metric": "2D stencil Gcells/sec",
+            "value": round(value, 3),
+            "unit": "Gcells/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": _ms(dt / args.steps),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp32" if args.dtype == "f32" else "fp64",
+            "data": "synthetic (deterministic random init per global cell)",
+            "config": {
+                "model": f"2D stencil {gw}x{gh} {args.dtype} 5-point Jacobi, periodic, RCCL halo exchange",
+                "global_batch": gw * gh,
+                "seq_len": None,
+                "parallelism": f"cart{rows}x{cols}",
+            },
+            "extras": extras,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,75 @@
+// RCCL communicator: the device data plane over xGMI.
+//
+// The reference pushed device pointers through a CUDA-aware MVAPICH2
+// (stencil2d/stencil2D.h:369,373; test-benchmark/mpi-pingpong-gpu.cpp:52-53).
+// Here every device-to-device byte goes through RCCL point-to-point or
+// collectives on a HIP stream; the control plane (rank discovery, unique-id
+// broadcast, host scalars) is MPI for the C++ apps and torch.distributed for the
+// Python launcher. Bootstrap is therefore a plain byte string.
+#pragma once
+
+#define MXS_WITH_RCCL 1
+#include <rccl/rccl.h>
+
+#include <string>
+#include <type_traits>
+
+#include "mxs/core/error.hpp"
+
+namespace mxs {
+
+template <typename T>
+constexpr ncclDataType_t rccl_type() {
+  if constexpr (std::is_same_v<T, float>) return ncclFloat32;
+  else if constexpr (std::is_same_v<T, double>) return ncclFloat64;
+  else if constexpr (std::is_same_v<T, int>) return ncclInt32;
+  else if constexpr (std::is_same_v<T, unsigned char> || std::is_same_v<T, char>) return ncclUint8;
+  else if constexpr (std::is_same_v<T, long long> || std::is_same_v<T, long>) return ncclInt64;
+  else static_assert(sizeof(T) == 0, "unsupported RCCL element type");
+}
+
+class RcclComm {
+ public:
+  // NCCL_UNIQUE_ID_BYTES raw bytes; call on one rank and broadcast.
+  static std::string make_unique_id();
+
+  // Collective over all `nranks` processes; the calling process must have
+  // selected its HIP device already.
+  RcclComm(const std::string& unique_id, int nranks, int rank);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  ncclComm_t get() const { return comm_; }
+  int rank() const { return rank_; }
+  int size() const { return nranks_; }
+
+  // Non-blocking health probe (ncclCommGetAsyncError): returns false and fills
+  // `msg` when the communicator is in an error state (e.g. a peer died).
+  bool healthy(std::string* msg = nullptr) const;
+  // Tear the communicator down without waiting for peers (after a failure).
+  void abort();
+
+  // Sum-allreduce `count` elements in place or out of place on `stream`.
+  template <typename T>
+  void allreduce_sum(const T* send, T* recv, size_t count, hipStream_t stream) const {
+    MXS_RCCL_CHECK(ncclAllReduce(send, recv, count, rccl_type<T>(), ncclSum, comm_, stream));
+  }
+  template <typename T>
+  void send(const T* buf, size_t count, int peer, hipStream_t stream) const {
+    MXS_RCCL_CHECK(ncclSend(buf, count, rccl_type<T>(), peer, comm_, stream));
+  }
+  template <typename T>
+  void recv(T* buf, size_t count, int peer, hipStream_t stream) const {
+    MXS_RCCL_CHECK(ncclRecv(buf, count, rccl_type<T>(), peer, comm_, stream));
+  }
+  void group_start() const { MXS_RCCL_CHECK(ncclGroupStart()); }
+  void group_end() const { MXS_RCCL_CHECK(ncclGroupEnd()); }
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int rank_ = 0;
+  int nranks_ = 1;
+};
+
+}  // namespace mxs

@@ -1,0 +1,115 @@
+// Host API of the hand-written CDNA4 (gfx950) kernels. Every launcher is
+// stream-ordered, allocation-free and synchronisation-free, so any sequence of
+// them can be captured into a hipGraph (cdna_hip_programming.md Guideline 9).
+//
+// Kernel inventory:
+//   K1/K3  fill, fill_region, fill_random       kernels/fill.hip
+//   K10    stencil5_rows / stencil5_rect         kernels/stencil.hip
+//          stencil_box (LDS-tiled (2R+1)^2)      kernels/stencil.hip
+//   K11/12 copy2d_batch (halo pack/unpack/self)  kernels/halo.hip
+//   K2/4/5/8 dot_atomic, dot_partials, reduce_partials, dot_single_pass, dot_racy
+//                                                kernels/dot.hip
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include "mxs/grid/layout.hpp"
+
+namespace mxs {
+namespace kernels {
+
+// ---------------------------------------------------------------- fill (K1/K3)
+template <typename T>
+void fill(T* p, index_t n, T value, hipStream_t s);
+// Fill a window of a buffer (reference InitKernel, stencil2d/mpi-2d-stencil-subarray-cuda.cu:17-28,
+// which launched one thread per block).
+template <typename T>
+void fill_region(T* base, const Array2D& region, T value, hipStream_t s);
+// Deterministic pseudo-random init of the core of a tile in [lo, hi): the value of
+// a cell depends only on its *global* coordinates and the seed, so any domain
+// decomposition of the same global grid starts from bit-identical data.
+template <typename T>
+void fill_random(T* tile, const TileGeom& g, index_t global_x0, index_t global_y0,
+                 index_t global_width, std::uint64_t seed, T lo, T hi, hipStream_t s);
+
+// ------------------------------------------------------------- stencil (K10)
+// out = c_center * u[y][x] + c_neighbor * ((u[y-1][x] + u[y+1][x]) + (u[y][x-1] + u[y][x+1]))
+// evaluated as fma(c_neighbor, (n + s) + (w + e), c_center * c) in the element type, so
+// every kernel variant and the host reference agree bit for bit.
+struct Stencil5Coeffs {
+  double center = 0.2;
+  double neighbor = 0.2;
+};
+
+enum class StencilVariant : int {
+  Auto = 0,        // tuned default
+  RegisterRoll = 1,  // rolling 3-row register window, x-neighbours by wave shuffles
+  LdsTile = 2,       // LDS-staged 2D tile with a 1-cell ring
+};
+
+// Update core rows [row_begin, row_end) over the full core width. Columns 0 and
+// width-1 read the ghost columns, so the result is only final once the halo for
+// the current iteration has landed (see StencilSolver for the overlap schedule).
+template <typename T>
+void stencil5_rows(const T* in, T* out, const TileGeom& g, index_t row_begin, index_t row_end,
+                   Stencil5Coeffs c, hipStream_t s, StencilVariant v = StencilVariant::Auto);
+
+// Update an arbitrary core rectangle [x0, x1) x [y0, y1) (scalar path; used for the
+// boundary columns of the overlapped schedule and for tiny tiles).
+template <typename T>
+void stencil5_rect(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0,
+                   index_t y1, Stencil5Coeffs c, hipStream_t s);
+
+// (2R+1)^2 box stencil with arbitrary weights (row-major, (2R+1)^2 entries), R in {1, 2}.
+// Needs a ghost ring of at least R cells. LDS-tiled: each workgroup stages a
+// (64+2R) x (16+2R) input tile once and reads the (2R+1)^2 taps from LDS.
+constexpr int kMaxBoxRadius = 2;
+struct BoxWeights {
+  int radius = 1;
+  float w[(2 * kMaxBoxRadius + 1) * (2 * kMaxBoxRadius + 1)] = {};
+};
+template <typename T>
+void stencil_box(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0,
+                 index_t y1, const BoxWeights& w, hipStream_t s);
+
+// ------------------------------------------------------ halo pack/unpack (K11/K12)
+// A batch of strided 2D copies between up to three base pointers
+// (slot 0 = tile, 1 = send buffer, 2 = recv buffer). One launch moves every
+// segment of a halo exchange: gridDim.y indexes the copy.
+constexpr int kMaxCopies = 24;
+struct Copy2D {
+  index_t src_off = 0, src_stride = 0;
+  index_t dst_off = 0, dst_stride = 0;
+  index_t width = 0, height = 0;
+  int src_slot = 0, dst_slot = 0;
+};
+struct Copy2DBatch {
+  int n = 0;
+  Copy2D op[kMaxCopies];
+};
+template <typename T>
+void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s);
+
+// ---------------------------------------------------------------- dot (K2-K8)
+enum class DotReduce : int {
+  Atomic = 0,      // per-block partial, one device atomic per block (mpicuda2.cu:65-81)
+  TwoPass = 1,     // per-block partials + 1-block finisher kernel (mpicuda4.cu:71-88 + device finish)
+  SinglePass = 2,  // last-block-done reduction with agent-scope release/acquire (mpicuda4.cu:157-185)
+  HostPartials = 3,  // per-block partials, summed on the host in f64 (REDUCE_CPU)
+  Racy = 4,        // NO_SYNC demonstrator: non-atomic `*out += partial` (ref_parallel-dot-product-atomics.cu:26-32)
+};
+
+// Scratch needed by the dot kernels: `partials` holds >= dot_max_blocks() Acc
+// values, `counter` one unsigned int (zeroed by the launcher every call).
+int dot_grid_size(index_t n, int block);
+constexpr int kDotBlock = 256;
+
+// result = sum(x[i] * y[i]) accumulated in Acc (double or float). Writes the
+// scalar into *out (device pointer). For HostPartials the partials are left in
+// `partials[0..grid)` and *out is not written.
+template <typename T, typename Acc>
+void dot(const T* x, const T* y, index_t n, Acc* out, Acc* partials, unsigned* counter,
+         DotReduce mode, int grid, hipStream_t s);
+
+}  // namespace kernels
+}  // namespace mxs

@@ -1,0 +1,69 @@
+// Halo pack / unpack / self-copy (K11, K12). Replaces the packing
+// that a CUDA-aware MPI did internally for MPI_Type_create_subarray halos
+// (stencil2d/stencil2D.h:203-228, 361-377).
+//
+// One launch moves every segment of one side of an exchange: gridDim.y indexes
+// the copy descriptor (passed by value in the kernarg segment, so the launch is
+// graph-capturable and needs no device-side descriptor table), gridDim.x
+// workgroups stride over the segment's elements. Row segments are contiguous on
+// both sides; column segments are strided on the tile side (one element per
+// pitch) and contiguous on the buffer side, so lanes map to consecutive buffer
+// elements and the strided side is the only uncoalesced one.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "mxs/core/error.hpp"
+#include "mxs/kernels/kernels.hpp"
+
+namespace mxs {
+namespace kernels {
+namespace {
+
+constexpr int kBlock = 256;
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void copy2d_batch_kernel(T* __restrict__ s0, T* __restrict__ s1,
+                                                              T* __restrict__ s2, Copy2DBatch b) {
+  const Copy2D& op = b.op[blockIdx.y];
+  // Wave-uniform selects (a runtime-indexed pointer array would go to scratch).
+  const T* __restrict__ src = (op.src_slot == 0 ? s0 : (op.src_slot == 1 ? s1 : s2)) + op.src_off;
+  T* __restrict__ dst = (op.dst_slot == 0 ? s0 : (op.dst_slot == 1 ? s1 : s2)) + op.dst_off;
+  const index_t n = op.width * op.height;
+  const index_t stride = index_t(gridDim.x) * blockDim.x;
+  if (op.width == 1) {  // column segment: no division in the loop
+    for (index_t i = index_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+      dst[i * op.dst_stride] = src[i * op.src_stride];
+    return;
+  }
+  for (index_t i = index_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const index_t y = i / op.width, x = i - y * op.width;
+    dst[y * op.dst_stride + x] = src[y * op.src_stride + x];
+  }
+}
+
+}  // namespace
+
+template <typename T>
+void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s) {
+  if (b.n <= 0) return;
+  MXS_CHECK(b.n <= kMaxCopies, "copy2d_batch: too many copies " << b.n);
+  index_t biggest = 0;
+  for (int i = 0; i < b.n; ++i) biggest = std::max(biggest, b.op[i].width * b.op[i].height);
+  if (biggest == 0) return;
+  // Enough workgroups for the largest segment, at most 64 per segment: halo
+  // segments are O(perimeter) and latency-bound, more workgroups only add launch cost.
+  const index_t want = (biggest + kBlock - 1) / kBlock;
+  const int gx = int(std::min<index_t>(want, 64));
+  copy2d_batch_kernel<T><<<dim3(gx, b.n), kBlock, 0, s>>>(slot0, slot1, slot2, b);
+  MXS_HIP_CHECK_LAUNCH();
+}
+
+template void copy2d_batch<float>(float*, float*, float*, const Copy2DBatch&, hipStream_t);
+template void copy2d_batch<double>(double*, double*, double*, const Copy2DBatch&, hipStream_t);
+template void copy2d_batch<int>(int*, int*, int*, const Copy2DBatch&, hipStream_t);
+template void copy2d_batch<unsigned char>(unsigned char*, unsigned char*, unsigned char*, const Copy2DBatch&,
+                                          hipStream_t);
+
+}  // namespace kernels
+}  // namespace mxs

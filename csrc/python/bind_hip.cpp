@@ -1,0 +1,340 @@
+// _mxs_hip: bindings of the HIP kernels and the native runtime (RCCL
+// communicator, halo exchanger, stencil solver, ping-pong).
+//
+// Buffers cross the boundary as raw device addresses (Python ints, e.g.
+// torch.Tensor.data_ptr()) and streams as hipStream_t handles
+// (torch.cuda.current_stream().cuda_stream), so the Python side keeps using the
+// PyTorch caching allocator while all device work is launched from C++.
+// Import torch BEFORE this module: then libamdhip64.so.7 / librccl.so.1 resolve
+// to the copies torch already loaded (one HIP runtime per process).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <memory>
+#include <stdexcept>
+#include <string>
+
+#include "mxs/comm/rccl_comm.hpp"
+#include "mxs/halo/exchange.hpp"
+#include "mxs/kernels/kernels.hpp"
+#include "mxs/runtime/pingpong.hpp"
+#include "mxs/runtime/stencil_solver.hpp"
+
+namespace py = pybind11;
+using namespace mxs;
+
+namespace {
+
+template <typename T>
+T* ptr(std::uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+hipStream_t strm(std::uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+enum class DType { F32, F64 };
+DType parse_dtype(const std::string& d) {
+  if (d == "f32" || d == "float32" || d == "float") return DType::F32;
+  if (d == "f64" || d == "float64" || d == "double") return DType::F64;
+  throw std::invalid_argument("unsupported dtype '" + d + "' (use f32 or f64)");
+}
+
+kernels::StencilVariant parse_variant(const std::string& v) {
+  if (v == "auto") return kernels::StencilVariant::Auto;
+  if (v == "roll") return kernels::StencilVariant::RegisterRoll;
+  if (v == "lds") return kernels::StencilVariant::LdsTile;
+  throw std::invalid_argument("unknown stencil variant '" + v + "' (auto|roll|lds)");
+}
+
+kernels::DotReduce parse_reduce(const std::string& r) {
+  if (r == "atomic") return kernels::DotReduce::Atomic;
+  if (r == "two-pass" || r == "two_pass") return kernels::DotReduce::TwoPass;
+  if (r == "single-pass" || r == "single_pass" || r == "gpu") return kernels::DotReduce::SinglePass;
+  if (r == "host" || r == "cpu") return kernels::DotReduce::HostPartials;
+  if (r == "racy" || r == "no-sync") return kernels::DotReduce::Racy;
+  throw std::invalid_argument("unknown reduction '" + r + "'");
+}
+
+kernels::BoxWeights make_box(int radius, const std::vector<float>& w) {
+  kernels::BoxWeights b;
+  b.radius = radius;
+  const size_t k = size_t(2 * radius + 1) * size_t(2 * radius + 1);
+  if (radius < 1 || radius > kernels::kMaxBoxRadius) throw std::invalid_argument("box radius must be 1 or 2");
+  if (w.size() != k) throw std::invalid_argument("box weights must have (2r+1)^2 entries");
+  for (size_t i = 0; i < k; ++i) b.w[i] = w[i];
+  return b;
+}
+
+// Type-erased solver handle so Python sees one class.
+struct SolverHandle {
+  DType dt;
+  std::unique_ptr<StencilSolver<float>> f;
+  std::unique_ptr<StencilSolver<double>> d;
+  template <typename F>
+  auto visit(F&& fn) {
+    return dt == DType::F32 ? fn(*f) : fn(*d);
+  }
+};
+
+struct ExchangerHandle {
+  DType dt;
+  std::unique_ptr<HaloExchanger<float>> f;
+  std::unique_ptr<HaloExchanger<double>> d;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_mxs_hip, m) {
+  m.doc() = "mxs HIP kernels (gfx950) and native runtime";
+
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    return n;
+  });
+  m.def("set_device", [](int d) { MXS_HIP_CHECK(hipSetDevice(d)); });
+  m.def("device_sync", []() { MXS_HIP_CHECK(hipDeviceSynchronize()); });
+  m.def("stream_sync", [](std::uintptr_t s) { MXS_HIP_CHECK(hipStreamSynchronize(strm(s))); });
+  m.def("device_arch", [](int d) {
+    hipDeviceProp_t p;
+    MXS_HIP_CHECK(hipGetDeviceProperties(&p, d));
+    return std::string(p.gcnArchName);
+  });
+
+  // ------------------------------------------------------------------ kernels
+  m.def(
+      "fill",
+      [](std::uintptr_t p, index_t n, double v, const std::string& dt, std::uintptr_t s) {
+        if (parse_dtype(dt) == DType::F32) kernels::fill<float>(ptr<float>(p), n, float(v), strm(s));
+        else kernels::fill<double>(ptr<double>(p), n, v, strm(s));
+      },
+      py::arg("ptr"), py::arg("n"), py::arg("value"), py::arg("dtype"), py::arg("stream") = 0);
+  m.def(
+      "fill_region",
+      [](std::uintptr_t p, const Array2D& r, double v, const std::string& dt, std::uintptr_t s) {
+        if (parse_dtype(dt) == DType::F32) kernels::fill_region<float>(ptr<float>(p), r, float(v), strm(s));
+        else kernels::fill_region<double>(ptr<double>(p), r, v, strm(s));
+      },
+      py::arg("ptr"), py::arg("region"), py::arg("value"), py::arg("dtype"), py::arg("stream") = 0);
+  m.def(
+      "fill_random",
+      [](std::uintptr_t p, const TileGeom& g, index_t gx0, index_t gy0, index_t gw, std::uint64_t seed, double lo,
+         double hi, const std::string& dt, std::uintptr_t s) {
+        if (parse_dtype(dt) == DType::F32)
+          kernels::fill_random<float>(ptr<float>(p), g, gx0, gy0, gw, seed, float(lo), float(hi), strm(s));
+        else
+          kernels::fill_random<double>(ptr<double>(p), g, gx0, gy0, gw, seed, lo, hi, strm(s));
+      },
+      py::arg("ptr"), py::arg("geom"), py::arg("global_x0"), py::arg("global_y0"), py::arg("global_width"),
+      py::arg("seed"), py::arg("lo") = 0.0, py::arg("hi") = 1.0, py::arg("dtype") = "f32", py::arg("stream") = 0);
+  m.def(
+      "stencil5_rows",
+      [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, index_t r0, index_t r1, double c0, double c1,
+         const std::string& dt, std::uintptr_t s, const std::string& variant) {
+        kernels::Stencil5Coeffs c{c0, c1};
+        const auto v = parse_variant(variant);
+        if (parse_dtype(dt) == DType::F32)
+          kernels::stencil5_rows<float>(ptr<float>(in), ptr<float>(out), g, r0, r1, c, strm(s), v);
+        else
+          kernels::stencil5_rows<double>(ptr<double>(in), ptr<double>(out), g, r0, r1, c, strm(s), v);
+      },
+      py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("row_begin"), py::arg("row_end"),
+      py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2, py::arg("dtype") = "f32", py::arg("stream") = 0,
+      py::arg("variant") = "auto");
+  m.def(
+      "stencil5_rect",
+      [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
+         double c0, double c1, const std::string& dt, std::uintptr_t s) {
+        kernels::Stencil5Coeffs c{c0, c1};
+        if (parse_dtype(dt) == DType::F32)
+          kernels::stencil5_rect<float>(ptr<float>(in), ptr<float>(out), g, x0, x1, y0, y1, c, strm(s));
+        else
+          kernels::stencil5_rect<double>(ptr<double>(in), ptr<double>(out), g, x0, x1, y0, y1, c, strm(s));
+      },
+      py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("x0"), py::arg("x1"), py::arg("y0"), py::arg("y1"),
+      py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2, py::arg("dtype") = "f32", py::arg("stream") = 0);
+  m.def(
+      "stencil_box",
+      [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
+         int radius, const std::vector<float>& w, const std::string& dt, std::uintptr_t s) {
+        const auto b = make_box(radius, w);
+        if (parse_dtype(dt) == DType::F32)
+          kernels::stencil_box<float>(ptr<float>(in), ptr<float>(out), g, x0, x1, y0, y1, b, strm(s));
+        else
+          kernels::stencil_box<double>(ptr<double>(in), ptr<double>(out), g, x0, x1, y0, y1, b, strm(s));
+      },
+      py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("x0"), py::arg("x1"), py::arg("y0"), py::arg("y1"),
+      py::arg("radius"), py::arg("weights"), py::arg("dtype") = "f32", py::arg("stream") = 0);
+  m.def("dot_grid_size", [](index_t n) { return kernels::dot_grid_size(n, kernels::kDotBlock); });
+  m.def(
+      "dot",
+      [](std::uintptr_t x, std::uintptr_t y, index_t n, std::uintptr_t out, std::uintptr_t partials,
+         std::uintptr_t counter, const std::string& reduce, const std::string& dt, const std::string& acc, int grid,
+         std::uintptr_t s) {
+        const auto mode = parse_reduce(reduce);
+        const DType d = parse_dtype(dt), a = parse_dtype(acc);
+        if (d == DType::F32 && a == DType::F32)
+          kernels::dot<float, float>(ptr<float>(x), ptr<float>(y), n, ptr<float>(out), ptr<float>(partials),
+                                     ptr<unsigned>(counter), mode, grid, strm(s));
+        else if (d == DType::F32)
+          kernels::dot<float, double>(ptr<float>(x), ptr<float>(y), n, ptr<double>(out), ptr<double>(partials),
+                                      ptr<unsigned>(counter), mode, grid, strm(s));
+        else if (a == DType::F64)
+          kernels::dot<double, double>(ptr<double>(x), ptr<double>(y), n, ptr<double>(out), ptr<double>(partials),
+                                       ptr<unsigned>(counter), mode, grid, strm(s));
+        else
+          throw std::invalid_argument("f64 inputs need an f64 accumulator");
+      },
+      py::arg("x"), py::arg("y"), py::arg("n"), py::arg("out"), py::arg("partials"), py::arg("counter"),
+      py::arg("reduce") = "single-pass", py::arg("dtype") = "f64", py::arg("acc") = "f64", py::arg("grid") = 0,
+      py::arg("stream") = 0);
+
+  // ------------------------------------------------------------------ RCCL
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init([](py::bytes uid, int nranks, int rank) {
+             return std::make_unique<RcclComm>(std::string(uid), nranks, rank);
+           }),
+           py::arg("unique_id"), py::arg("nranks"), py::arg("rank"), py::call_guard<py::gil_scoped_release>())
+      .def_static("make_unique_id", []() { return py::bytes(RcclComm::make_unique_id()); })
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("size", &RcclComm::size)
+      .def("healthy",
+           [](const RcclComm& c) {
+             std::string msg;
+             const bool ok = c.healthy(&msg);
+             return py::make_tuple(ok, msg);
+           })
+      .def("abort", &RcclComm::abort)
+      .def(
+          "allreduce_sum",
+          [](const RcclComm& c, std::uintptr_t send, std::uintptr_t recv, size_t count, const std::string& dt,
+             std::uintptr_t s) {
+            if (parse_dtype(dt) == DType::F32) c.allreduce_sum<float>(ptr<float>(send), ptr<float>(recv), count, strm(s));
+            else c.allreduce_sum<double>(ptr<double>(send), ptr<double>(recv), count, strm(s));
+          },
+          py::arg("send"), py::arg("recv"), py::arg("count"), py::arg("dtype"), py::arg("stream") = 0)
+      .def(
+          "send_bytes",
+          [](const RcclComm& c, std::uintptr_t buf, size_t n, int peer, std::uintptr_t s) {
+            c.send<unsigned char>(ptr<unsigned char>(buf), n, peer, strm(s));
+          },
+          py::arg("buf"), py::arg("nbytes"), py::arg("peer"), py::arg("stream") = 0)
+      .def(
+          "recv_bytes",
+          [](const RcclComm& c, std::uintptr_t buf, size_t n, int peer, std::uintptr_t s) {
+            c.recv<unsigned char>(ptr<unsigned char>(buf), n, peer, strm(s));
+          },
+          py::arg("buf"), py::arg("nbytes"), py::arg("peer"), py::arg("stream") = 0)
+      .def("group_start", &RcclComm::group_start)
+      .def("group_end", &RcclComm::group_end);
+
+  // ------------------------------------------------------------------ halo
+  py::enum_<HaloBackend>(m, "HaloBackend").value("LOCAL", HaloBackend::Local).value("RCCL", HaloBackend::Rccl);
+  py::class_<ExchangerHandle>(m, "HaloExchanger")
+      .def(py::init([](const HaloPlan& plan, HaloBackend b, const RcclComm* comm, const std::string& dt) {
+             auto h = std::make_unique<ExchangerHandle>();
+             h->dt = parse_dtype(dt);
+             if (h->dt == DType::F32) h->f = std::make_unique<HaloExchanger<float>>(plan, b, comm);
+             else h->d = std::make_unique<HaloExchanger<double>>(plan, b, comm);
+             return h;
+           }),
+           py::arg("plan"), py::arg("backend"), py::arg("comm") = nullptr, py::arg("dtype") = "f32",
+           py::keep_alive<1, 4>())
+      .def(
+          "exchange",
+          [](ExchangerHandle& h, std::uintptr_t tile, std::uintptr_t s) {
+            if (h.dt == DType::F32) h.f->exchange(ptr<float>(tile), strm(s));
+            else h.d->exchange(ptr<double>(tile), strm(s));
+          },
+          py::arg("tile"), py::arg("stream") = 0)
+      .def("wire_bytes", [](const ExchangerHandle& h) { return h.dt == DType::F32 ? h.f->wire_bytes() : h.d->wire_bytes(); });
+
+  // ------------------------------------------------------------------ solver
+  py::enum_<StencilKind>(m, "StencilKind").value("JACOBI5", StencilKind::Jacobi5).value("BOX", StencilKind::Box);
+  py::class_<SolverHandle>(m, "StencilSolver")
+      .def(py::init([](const CartTopology& topo, int rank, const TileGeom& tile, std::uintptr_t a, std::uintptr_t b,
+                       const RcclComm* comm, const std::string& dt, HaloBackend backend, bool overlap,
+                       bool use_graph, bool loopback_self, StencilKind kind, double c0, double c1, int box_radius,
+                       const std::vector<float>& box_w, const std::string& variant) {
+             SolverConfig cfg;
+             cfg.backend = backend;
+             cfg.overlap = overlap;
+             cfg.use_graph = use_graph;
+             cfg.loopback_self = loopback_self;
+             cfg.kind = kind;
+             cfg.coeffs = {c0, c1};
+             cfg.variant = parse_variant(variant);
+             if (kind == StencilKind::Box) cfg.box = make_box(box_radius, box_w);
+             auto h = std::make_unique<SolverHandle>();
+             h->dt = parse_dtype(dt);
+             if (h->dt == DType::F32)
+               h->f = std::make_unique<StencilSolver<float>>(topo, rank, tile, ptr<float>(a), ptr<float>(b), comm, cfg);
+             else
+               h->d = std::make_unique<StencilSolver<double>>(topo, rank, tile, ptr<double>(a), ptr<double>(b), comm,
+                                                              cfg);
+             return h;
+           }),
+           py::arg("topo"), py::arg("rank"), py::arg("tile"), py::arg("buf_a"), py::arg("buf_b"),
+           py::arg("comm") = nullptr, py::arg("dtype") = "f32", py::arg("backend") = HaloBackend::Local,
+           py::arg("overlap") = true, py::arg("use_graph") = true, py::arg("loopback_self") = false,
+           py::arg("kind") = StencilKind::Jacobi5, py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2,
+           py::arg("box_radius") = 1, py::arg("box_weights") = std::vector<float>{}, py::arg("variant") = "auto",
+           py::keep_alive<1, 7>())
+      .def("step", [](SolverHandle& h) { h.visit([](auto& s) { s.step(); }); })
+      .def(
+          "run", [](SolverHandle& h, int n) { h.visit([n](auto& s) { s.run(n); }); }, py::arg("iters"),
+          py::call_guard<py::gil_scoped_release>())
+      .def("exchange_only", [](SolverHandle& h) { h.visit([](auto& s) { s.exchange_only(); }); })
+      .def("synchronize", [](SolverHandle& h) { h.visit([](auto& s) { s.synchronize(); }); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("current",
+           [](SolverHandle& h) {
+             return h.visit([](auto& s) { return reinterpret_cast<std::uintptr_t>(s.current()); });
+           })
+      .def("compute_stream",
+           [](SolverHandle& h) {
+             return h.visit([](auto& s) { return reinterpret_cast<std::uintptr_t>(s.compute_stream()); });
+           })
+      .def("graph_active", [](SolverHandle& h) { return h.visit([](auto& s) { return s.graph_active(); }); })
+      .def("graph_status", [](SolverHandle& h) { return h.visit([](auto& s) { return s.graph_status(); }); });
+
+  // ------------------------------------------------------------------ ping-pong
+  py::enum_<PingPongMode>(m, "PingPongMode")
+      .value("BLOCKING", PingPongMode::Blocking)
+      .value("ASYNC", PingPongMode::Async)
+      .value("OVERLAP", PingPongMode::Overlap);
+  py::enum_<LocalPath>(m, "LocalPath")
+      .value("DEVICE_COPY", LocalPath::DeviceCopy)
+      .value("PINNED_STAGING", LocalPath::PinnedStaging)
+      .value("PAGEABLE_STAGING", LocalPath::PageableStaging);
+  py::class_<PingPongStats>(m, "PingPongStats")
+      .def_readonly("bytes", &PingPongStats::bytes)
+      .def_readonly("reps", &PingPongStats::reps)
+      .def_readonly("min_rtt_us", &PingPongStats::min_rtt_us)
+      .def_readonly("median_rtt_us", &PingPongStats::median_rtt_us)
+      .def_readonly("max_rtt_us", &PingPongStats::max_rtt_us)
+      .def_readonly("compute_alone_us", &PingPongStats::compute_alone_us)
+      .def_readonly("comm_alone_us", &PingPongStats::comm_alone_us)
+      .def_readonly("overlapped_us", &PingPongStats::overlapped_us)
+      .def_readonly("verified", &PingPongStats::verified)
+      .def("latency_us", &PingPongStats::latency_us)
+      .def("bandwidth_gbps", &PingPongStats::bandwidth_gbps);
+  m.def(
+      "pingpong_rccl",
+      [](const RcclComm& c, int peer, std::uintptr_t sb, std::uintptr_t rb, size_t bytes, int warmup, int reps,
+         PingPongMode mode, std::uintptr_t s) {
+        return pingpong_rccl(c, peer, ptr<void>(sb), ptr<void>(rb), bytes, warmup, reps, mode, strm(s));
+      },
+      py::arg("comm"), py::arg("peer"), py::arg("sendbuf"), py::arg("recvbuf"), py::arg("nbytes"),
+      py::arg("warmup") = 5, py::arg("reps") = 20, py::arg("mode") = PingPongMode::Blocking, py::arg("stream") = 0,
+      py::call_guard<py::gil_scoped_release>());
+  m.def(
+      "pingpong_local",
+      [](LocalPath p, std::uintptr_t a, std::uintptr_t b, size_t bytes, int warmup, int reps, std::uintptr_t s) {
+        return pingpong_local(p, ptr<void>(a), ptr<void>(b), bytes, warmup, reps, strm(s));
+      },
+      py::arg("path"), py::arg("buf_a"), py::arg("buf_b"), py::arg("nbytes"), py::arg("warmup") = 5,
+      py::arg("reps") = 20, py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>());
+}

@@ -1,0 +1,98 @@
+#include "mxs/halo/exchange.hpp"
+
+namespace mxs {
+
+namespace {
+kernels::Copy2D tile_to_buf(const Array2D& r, index_t buf_off, int buf_slot) {
+  kernels::Copy2D c;
+  c.src_off = r.index(0, 0);
+  c.src_stride = r.row_stride;
+  c.dst_off = buf_off;
+  c.dst_stride = r.width;
+  c.width = r.width;
+  c.height = r.height;
+  c.src_slot = 0;
+  c.dst_slot = buf_slot;
+  return c;
+}
+kernels::Copy2D buf_to_tile(const Array2D& r, index_t buf_off, int buf_slot) {
+  kernels::Copy2D c;
+  c.src_off = buf_off;
+  c.src_stride = r.width;
+  c.dst_off = r.index(0, 0);
+  c.dst_stride = r.row_stride;
+  c.width = r.width;
+  c.height = r.height;
+  c.src_slot = buf_slot;
+  c.dst_slot = 0;
+  return c;
+}
+void push(kernels::Copy2DBatch& b, const kernels::Copy2D& c) {
+  MXS_CHECK(b.n < kernels::kMaxCopies, "halo program exceeds " << kernels::kMaxCopies << " copies");
+  if (c.width > 0 && c.height > 0) b.op[b.n++] = c;
+}
+}  // namespace
+
+HaloCopyPrograms build_halo_copy_programs(const HaloPlan& plan) {
+  HaloCopyPrograms p;
+  for (const auto& m : plan.sends)
+    for (const auto& s : m.segments) push(p.pack, tile_to_buf(s.region, s.offset, 1));
+  for (const auto& c : plan.self_copies) {
+    kernels::Copy2D k;
+    k.src_off = c.src.index(0, 0);
+    k.src_stride = c.src.row_stride;
+    k.dst_off = c.dst.index(0, 0);
+    k.dst_stride = c.dst.row_stride;
+    k.width = c.src.width;
+    k.height = c.src.height;
+    k.src_slot = 0;
+    k.dst_slot = 0;
+    push(p.pack, k);
+  }
+  for (const auto& m : plan.recvs)
+    for (const auto& s : m.segments) push(p.unpack, buf_to_tile(s.region, s.offset, 2));
+  return p;
+}
+
+template <typename T>
+HaloExchanger<T>::HaloExchanger(const HaloPlan& plan, HaloBackend backend, const RcclComm* comm)
+    : plan_(plan), backend_(backend), comm_(comm), progs_(build_halo_copy_programs(plan)) {
+  if (!plan_.sends.empty()) {
+    MXS_CHECK(backend_ == HaloBackend::Rccl, "plan has remote peers: the Local backend cannot serve it");
+    MXS_CHECK(comm_ != nullptr, "Rccl halo backend needs a communicator");
+  }
+  send_.reset(plan_.send_elems);
+  recv_.reset(plan_.recv_elems);
+}
+
+template <typename T>
+void HaloExchanger<T>::pack(T* tile, hipStream_t stream) {
+  kernels::copy2d_batch<T>(tile, send_.get(), recv_.get(), progs_.pack, stream);
+}
+
+template <typename T>
+void HaloExchanger<T>::transfer(hipStream_t stream) {
+  if (plan_.sends.empty()) return;
+  comm_->group_start();
+  for (const auto& m : plan_.recvs) comm_->recv<T>(recv_.get() + m.offset, size_t(m.count), m.peer, stream);
+  for (const auto& m : plan_.sends) comm_->send<T>(send_.get() + m.offset, size_t(m.count), m.peer, stream);
+  comm_->group_end();
+}
+
+template <typename T>
+void HaloExchanger<T>::unpack(T* tile, hipStream_t stream) {
+  kernels::copy2d_batch<T>(tile, send_.get(), recv_.get(), progs_.unpack, stream);
+}
+
+template <typename T>
+void HaloExchanger<T>::exchange(T* tile, hipStream_t stream) {
+  pack(tile, stream);
+  transfer(stream);
+  unpack(tile, stream);
+}
+
+template class HaloExchanger<float>;
+template class HaloExchanger<double>;
+template class HaloExchanger<int>;
+
+}  // namespace mxs

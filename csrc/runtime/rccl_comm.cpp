@@ -1,0 +1,41 @@
+#include "mxs/comm/rccl_comm.hpp"
+
+#include <cstring>
+
+namespace mxs {
+
+std::string RcclComm::make_unique_id() {
+  ncclUniqueId id;
+  MXS_RCCL_CHECK(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+RcclComm::RcclComm(const std::string& unique_id, int nranks, int rank) : rank_(rank), nranks_(nranks) {
+  MXS_CHECK(unique_id.size() == sizeof(ncclUniqueId),
+            "RcclComm: unique id must be " << sizeof(ncclUniqueId) << " bytes, got " << unique_id.size());
+  MXS_CHECK(rank >= 0 && rank < nranks, "RcclComm: bad rank " << rank << " of " << nranks);
+  ncclUniqueId id;
+  std::memcpy(&id, unique_id.data(), sizeof(id));
+  MXS_RCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+}
+
+RcclComm::~RcclComm() {
+  if (comm_) (void)ncclCommDestroy(comm_);
+}
+
+bool RcclComm::healthy(std::string* msg) const {
+  if (!comm_) return false;
+  ncclResult_t async = ncclSuccess;
+  if (ncclCommGetAsyncError(comm_, &async) != ncclSuccess || async != ncclSuccess) {
+    if (msg) *msg = ncclGetErrorString(async);
+    return false;
+  }
+  return true;
+}
+
+void RcclComm::abort() {
+  if (comm_) (void)ncclCommAbort(comm_);
+  comm_ = nullptr;
+}
+
+}  // namespace mxs
