@@ -1,0 +1,102 @@
+// Stencil kernel tuning harness (one process, interleaved rounds: rule 24 of
+// cdna_hip_programming.md §5.4). Times every RegisterRoll instantiation, the
+// LDS-tile variant and a float4 copy of the same bytes (the achievable
+// read+write roofline) on a W x H fp32 tile; prints one JSON line per variant.
+//
+//   stencil_tune [W] [H] [rounds]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "mxs/core/error.hpp"
+#include "mxs/runtime/hip_utils.hpp"
+#include "../csrc/kernels/stencil_device.hpp"
+
+using namespace mxs;
+using namespace mxs::kernels::detail;
+
+__global__ __launch_bounds__(256) void copy4(const float4* __restrict__ a, float4* __restrict__ b, index_t n) {
+  const index_t stride = index_t(gridDim.x) * blockDim.x;
+  for (index_t i = index_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) b[i] = a[i];
+}
+
+struct Variant {
+  std::string name;
+  std::function<void(hipStream_t)> launch;
+  std::vector<float> ms;
+};
+
+template <int ROWS, int CH, bool NT, int WX, bool NTL, int NW = 4>
+Variant roll(const float* in, float* out, const TileGeom& g) {
+  char buf[128];
+  std::snprintf(buf, sizeof(buf), "roll_r%d_c%d_nt%d_wx%d_ntl%d_nw%d", ROWS, CH, int(NT), WX, int(NTL), NW);
+  return {buf, [=](hipStream_t s) {
+            constexpr int WY = NW / WX;
+            const index_t gx = (g.width + 256 * WX - 1) / (256 * WX);
+            const index_t gy = (g.height + ROWS * WY - 1) / (ROWS * WY);
+            stencil5_roll_kernel<float, ROWS, CH, NT, WX, NTL, NW><<<dim3(gx, gy), NW * 64, 0, s>>>(
+                in, out, g.pitch, g.core_offset(), g.width, 0, g.height, 0.2f, 0.2f);
+          }};
+}
+
+int main(int argc, char** argv) {
+  const index_t W = argc > 1 ? atol(argv[1]) : 32768;
+  const index_t H = argc > 2 ? atol(argv[2]) : 32768;
+  const int rounds = argc > 3 ? atoi(argv[3]) : 5;
+  const TileGeom g = TileGeom::aligned(W, H, 1, 1, 4);
+  DeviceBuffer<float> a(g.alloc_elems()), b(g.alloc_elems());
+  MXS_HIP_CHECK(hipMemset(a.get(), 0, a.bytes()));
+  MXS_HIP_CHECK(hipMemset(b.get(), 0, b.bytes()));
+  const float* in = a.get();
+  float* out = b.get();
+  std::vector<Variant> vs;
+  const index_t n4 = g.alloc_elems() / 4;
+  vs.push_back({"copy_float4", [=](hipStream_t s) {
+                  copy4<<<kNumCUs * 8, 256, 0, s>>>(reinterpret_cast<const float4*>(in), reinterpret_cast<float4*>(out), n4);
+                }});
+  vs.push_back({"lds_th16", [=](hipStream_t s) {
+                  const index_t gx = (W + 255) / 256, gy = (H + 15) / 16;
+                  stencil5_lds_kernel<float, 16><<<dim3(gx, gy), 256, (16 + 2) * (256 + 8) * 4, s>>>(
+                      in, out, g.pitch, g.core_offset(), W, 0, H, 0.2f, 0.2f);
+                }});
+  vs.push_back(roll<8, 8, true, 4, false>(in, out, g));
+  vs.push_back(roll<4, 4, true, 4, false>(in, out, g));
+  vs.push_back(roll<2, 2, true, 4, false>(in, out, g));
+  vs.push_back(roll<3, 3, true, 4, false>(in, out, g));
+  vs.push_back(roll<4, 4, true, 4, false, 8>(in, out, g));
+  vs.push_back(roll<4, 4, true, 8, false, 8>(in, out, g));
+  vs.push_back(roll<4, 4, true, 2, false, 4>(in, out, g));
+  vs.push_back(roll<4, 4, true, 2, false, 2>(in, out, g));
+  vs.push_back(roll<4, 4, true, 1, false, 1>(in, out, g));
+  vs.push_back(roll<2, 2, true, 8, false, 8>(in, out, g));
+  vs.push_back(roll<4, 4, true, 16, false, 16>(in, out, g));
+  vs.push_back(roll<4, 4, false, 4, false>(in, out, g));
+  vs.push_back(roll<4, 2, true, 4, false>(in, out, g));
+
+  Stream st;
+  Event e0(true), e1(true);
+  for (auto& v : vs) v.launch(st.get());  // warm-up / first-touch
+  st.sync();
+  for (int r = 0; r < rounds; ++r)
+    for (auto& v : vs) {
+      e0.record(st.get());
+      for (int k = 0; k < 3; ++k) v.launch(st.get());
+      e1.record(st.get());
+      e1.sync();
+      v.ms.push_back(e1.since(e0) / 3);
+    }
+  const double bytes = 2.0 * double(W) * double(H) * 4.0;
+  for (auto& v : vs) {
+    std::sort(v.ms.begin(), v.ms.end());
+    const double med = v.ms[v.ms.size() / 2], best = v.ms[0];
+    const double cbytes = v.name == "copy_float4" ? 2.0 * double(g.alloc_elems()) * 4.0 : bytes;
+    std::printf("{\"variant\": \"%s\", \"median_ms\": %.4f, \"best_ms\": %.4f, \"tb_s\": %.3f, \"gcells_s\": %.1f}\n",
+                v.name.c_str(), med, best, cbytes / (med * 1e-3) / 1e12, double(W) * double(H) / (med * 1e-3) / 1e9);
+  }
+  return 0;
+}

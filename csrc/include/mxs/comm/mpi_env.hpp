@@ -1,0 +1,72 @@
+// MPI control plane for the C++ apps (reference: mpierr.h — the MPI_ macro that
+// formats "Error <code>: error message / error class message" and either throws
+// (-DMPI_ERR_USE_EXCEPTIONS) or prints and MPI_Aborts).
+//
+// MpiEnv is the RAII owner of MPI_Init/MPI_Finalize. It installs
+// MPI_ERRORS_RETURN on MPI_COMM_WORLD with MPI_Comm_set_errhandler (the
+// reference used MPI_Errhandler_set, removed in MPI-3, and called it before
+// MPI_Init in mpicuda2.cpp — SURVEY Q6) and routes every mxs failure (HIP, RCCL,
+// checks) to MPI_Abort so one failing rank never leaves its peers blocked.
+#pragma once
+
+#include <mpi.h>
+
+#include <sstream>
+#include <string>
+
+#include "mxs/core/error.hpp"
+
+namespace mxs {
+
+// "Error <code>:\n  error message: <string>\n  error class message: <class string>"
+inline std::string format_mpi_error(int code) {
+  char buf[MPI_MAX_ERROR_STRING];
+  int len = 0;
+  std::ostringstream os;
+  MPI_Error_string(code, buf, &len);
+  os << "Error " << code << ":\n  error message: " << std::string(buf, size_t(len));
+  int cls = 0;
+  MPI_Error_class(code, &cls);
+  MPI_Error_string(cls, buf, &len);
+  os << "\n  error class message: " << std::string(buf, size_t(len));
+  return os.str();
+}
+
+inline void mpi_check(int code, const char* expr, const char* file, int line) {
+  if (code == MPI_SUCCESS) return;
+  std::ostringstream os;
+  os << where(file, line) << " - " << expr << " failed\n" << format_mpi_error(code);
+  raise_error(os.str(), code);
+}
+
+#define MXS_MPI_CHECK(expr) ::mxs::mpi_check((expr), #expr, __FILE__, __LINE__)
+
+enum class MpiErrors { Abort, Throw };
+
+class MpiEnv {
+ public:
+  MpiEnv(int* argc, char*** argv, MpiErrors mode = MpiErrors::Abort);
+  ~MpiEnv();
+  MpiEnv(const MpiEnv&) = delete;
+  MpiEnv& operator=(const MpiEnv&) = delete;
+
+  int rank() const { return rank_; }
+  int size() const { return size_; }
+  const std::string& processor_name() const { return name_; }
+  // Ranks sharing this node (MPI_Comm_split_type(MPI_COMM_TYPE_SHARED)).
+  int local_rank() const { return local_rank_; }
+  int local_size() const { return local_size_; }
+  int node_count() const { return node_count_; }
+  int node_index() const { return node_index_; }
+
+  void barrier() const { MXS_MPI_CHECK(MPI_Barrier(MPI_COMM_WORLD)); }
+  double max_over_ranks(double v) const;
+  double sum_over_ranks(double v) const;
+
+ private:
+  int rank_ = 0, size_ = 1, local_rank_ = 0, local_size_ = 1, node_count_ = 1, node_index_ = 0;
+  std::string name_;
+  bool finalize_ = false;
+};
+
+}  // namespace mxs

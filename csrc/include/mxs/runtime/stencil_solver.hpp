@@ -4,17 +4,19 @@
 //
 // Per iteration (cur -> nxt), with `overlap` on:
 //
-//   comm stream    : wait(ready) -> pack(cur) -> RCCL send/recv -> unpack(cur) -> record(halo)
-//   compute stream : interior rows [1, H-1) of nxt  (reads only cur's core ... and
-//                    ghost columns, see below)       -> wait(halo)
-//                    boundary rows 0 and H-1, boundary columns 0 and W-1 -> record(ready)
+//   main stream : record(fork) -> pack(cur) -> RCCL send/recv -> unpack(cur) -> wait(interior)
+//                 -> boundary rows 0 and H-1, boundary columns 0 and W-1
+//   side stream : wait(fork) -> interior rows [1, H-1) of nxt -> record(interior)
+//
+// (RCCL must run on the capture-origin stream, so the exchange chain stays on
+// the main stream and the long interior sweep is the forked branch.)
 //
 // The interior launch covers full rows, so its columns 0 and W-1 read ghost
 // columns that the unpack may be writing concurrently; those two output columns
 // are recomputed by the boundary launch after the halo has landed, so the race
 // is benign by construction (it only ever produces values that are overwritten).
 // Without `overlap` (or for Local/1x1 grids) the iteration is exchange + one
-// full sweep on the compute stream.
+// full sweep on the main stream.
 //
 // `use_graph`: two iterations (cur->nxt, nxt->cur) are captured once into a
 // hipGraph and replayed, so an iteration costs one graph launch of host work
@@ -61,8 +63,8 @@ class StencilSolver {
 
   T* current() const { return cur_; }
   T* other() const { return nxt_; }
-  hipStream_t compute_stream() const { return compute_.get(); }
-  hipStream_t comm_stream() const { return comm_.get(); }
+  hipStream_t main_stream() const { return main_.get(); }
+  hipStream_t side_stream() const { return side_.get(); }
   bool graph_active() const { return graphs_[0].valid(); }
   const std::string& graph_status() const { return graph_status_; }
   const HaloPlan& plan() const { return ex_->plan(); }
@@ -70,8 +72,8 @@ class StencilSolver {
 
  private:
   void enqueue_step(T* cur, T* nxt);
-  void update(const T* in, T* out, index_t r0, index_t r1, bool full_rows);
-  void update_cols(const T* in, T* out, index_t r0, index_t r1);
+  void update(const T* in, T* out, index_t r0, index_t r1, hipStream_t s);
+  void update_cols(const T* in, T* out, index_t r0, index_t r1, hipStream_t s);
   bool try_capture();
 
   TileGeom tile_;
@@ -79,8 +81,8 @@ class StencilSolver {
   T* cur_;
   T* nxt_;
   std::unique_ptr<HaloExchanger<T>> ex_;
-  Stream compute_, comm_;
-  Event ready_, halo_;
+  Stream main_, side_;
+  Event fork_, interior_;
   GraphExec graphs_[2];  // [0]: buf_a -> buf_b, [1]: buf_b -> buf_a (as captured)
   int parity_ = 0;
   bool graph_tried_ = false;

@@ -8,19 +8,24 @@
 //
 // Variant RegisterRoll (default):
 //   * a wave owns a 64 x VEC column segment (VEC = 16 B / sizeof(T): 256 fp32
-//     or 128 fp64 columns) and walks a strip of ROWS rows top to bottom;
+//     or 128 fp64 columns) and a strip of ROWS rows;
 //   * each lane issues one 16-byte load per row (global_load_dwordx4, a whole
 //     1 KiB wave-instruction on aligned rows: TileGeom::aligned) and keeps a
 //     rolling 3-row window (up / mid / down) in registers, so vertical reuse
-//     costs nothing and every input element is fetched from HBM once per strip;
+//     inside a strip costs nothing;
 //   * horizontal neighbours come from the adjacent lane by a wave shuffle
 //     (x-1 of the first element, x+1 of the last); only lanes 0 and 63 load the
 //     single column just outside the segment;
 //   * rows are processed in chunks of CH: the CH row loads of a chunk are issued
-//     back to back before any arithmetic, so each wave keeps CH KiB in flight
-//     (Little's law: ~50 KiB per CU covers HBM latency at 6+ TB/s);
-//   * 4 waves per workgroup take 4 vertically adjacent strips of the same
-//     columns, so the two rows a strip re-reads at its ends are L2 hits.
+//     back to back before any arithmetic. Measured (bench/stencil_tune.hip,
+//     profiles/stencil_tuning): the winner is a SHORT strip (3-4 rows) loaded in
+//     one chunk — ROWS+2 independent 1 KiB loads in flight per wave from its
+//     first instruction — with 4 waves side by side covering 4 KiB of a row. The
+//     two rows a strip re-reads at its ends come from L2 / Infinity Cache
+//     (vertically adjacent strips run concurrently on one XCD), while long
+//     rolling strips (32 rows) lose ~30 % to exposed HBM latency;
+//   * non-temporal (streaming) stores: the output is not re-read before the
+//     next sweep, so it should not displace the input rows in L2.
 // Variant LdsTile: the textbook LDS-staged tile (a (TH+2) x (TW+2) input tile
 //   staged once per workgroup with 16-byte loads, five LDS reads per output).
 //   Kept as the measured alternative (see profiles/ and docs/PERF.md).
@@ -31,239 +36,32 @@
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
 
+#include "stencil_device.hpp"
+
 namespace mxs {
 namespace kernels {
 namespace {
-
-template <typename T>
-struct Vec16 {
-  static constexpr int N = 16 / sizeof(T);
-  using type = T __attribute__((ext_vector_type(N)));
-};
-
-template <typename T>
-__device__ __forceinline__ T fma_t(T a, T b, T c);
-template <>
-__device__ __forceinline__ float fma_t<float>(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-template <>
-__device__ __forceinline__ double fma_t<double>(double a, double b, double c) { return __builtin_fma(a, b, c); }
-
-// One output cell, fixed evaluation order (see kernels.hpp).
-template <typename T>
-__device__ __forceinline__ T jac(T c, T n, T s, T w, T e, T c0, T c1) {
-  return fma_t<T>(c1, (n + s) + (w + e), c0 * c);
-}
-
-constexpr int kWavesPerBlock = 4;
-constexpr int kBlock = kWavesPerBlock * kWaveSize;
-
-// ------------------------------------------------------------- RegisterRoll
-template <typename T, int ROWS, int CH, bool NT>
-__global__ __launch_bounds__(kBlock) void stencil5_roll_kernel(const T* __restrict__ in, T* __restrict__ out,
-                                                               index_t pitch, index_t core_off, index_t W,
-                                                               index_t row_begin, index_t row_end, T c0, T c1) {
-  static_assert(ROWS % CH == 0, "ROWS must be a multiple of CH");
-  constexpr int N = Vec16<T>::N;
-  constexpr int SEG = kWaveSize * N;
-  using V = typename Vec16<T>::type;
-
-  const int lane = threadIdx.x & (kWaveSize - 1);
-  const int wave = threadIdx.x / kWaveSize;
-  const index_t seg_base = index_t(blockIdx.x) * SEG;
-  const index_t x = seg_base + index_t(lane) * N;
-  const index_t y0 = row_begin + (index_t(blockIdx.y) * kWavesPerBlock + wave) * ROWS;
-  if (y0 >= row_end) return;  // wave-uniform exit
-  const index_t y1 = y0 + ROWS < row_end ? y0 + ROWS : row_end;
-
-  const bool load_ok = x < W + N;  // covers the lane right after the last core vector
-  const bool active = x < W;
-  const bool right_edge = (lane == kWaveSize - 1) && (seg_base + SEG <= W);
-  const T* __restrict__ pin = in + core_off + x;
-  T* __restrict__ pout = out + core_off + x;
-
-  auto ldv = [&](index_t y) -> V {
-    V v = V(T(0));
-    if (load_ok) v = *reinterpret_cast<const V*>(pin + y * pitch);
-    return v;
-  };
-  auto lde = [&](index_t y) -> T {
-    T e = T(0);
-    if (lane == 0) e = pin[y * pitch - 1];
-    else if (right_edge) e = pin[y * pitch + N];
-    return e;
-  };
-  auto emit = [&](index_t y, const V& up, const V& mid, const V& dn, T emid) {
-    T left = __shfl_up(mid[N - 1], 1);
-    T right = __shfl_down(mid[0], 1);
-    if (lane == 0) left = emid;
-    if (lane == kWaveSize - 1) right = emid;
-    V o;
-    o[0] = jac<T>(mid[0], up[0], dn[0], left, mid[1 % N], c0, c1);
-    if constexpr (N == 2) {
-      o[1] = jac<T>(mid[1], up[1], dn[1], mid[0], right, c0, c1);
-    } else {
-#pragma unroll
-      for (int i = 1; i < N - 1; ++i) o[i] = jac<T>(mid[i], up[i], dn[i], mid[i - 1], mid[i + 1], c0, c1);
-      o[N - 1] = jac<T>(mid[N - 1], up[N - 1], dn[N - 1], mid[N - 2], right, c0, c1);
-    }
-    if (active) {
-      T* p = pout + y * pitch;
-      if (x + N <= W) {
-        if constexpr (NT) __builtin_nontemporal_store(o, reinterpret_cast<V*>(p));
-        else *reinterpret_cast<V*>(p) = o;
-      } else {
-#pragma unroll
-        for (int i = 0; i < N; ++i)
-          if (x + i < W) p[i] = o[i];
-      }
-    }
-  };
-
-  V up = ldv(y0 - 1);
-  V mid = ldv(y0);
-  T emid = lde(y0);
-
-  if (y1 - y0 == ROWS) {
-    // Full strip: chunks of CH rows, loads of a chunk issued before its math.
-#pragma unroll 1
-    for (int c = 0; c < ROWS; c += CH) {
-      V dn[CH];
-      T edn[CH];
-#pragma unroll
-      for (int k = 0; k < CH; ++k) {
-        dn[k] = ldv(y0 + c + k + 1);
-        edn[k] = lde(y0 + c + k + 1);
-      }
-#pragma unroll
-      for (int k = 0; k < CH; ++k) {
-        emit(y0 + c + k, up, mid, dn[k], emid);
-        up = mid;
-        mid = dn[k];
-        emid = edn[k];
-      }
-    }
-  } else {
-#pragma unroll 1
-    for (index_t y = y0; y < y1; ++y) {
-      const V dn = ldv(y + 1);
-      const T edn = lde(y + 1);
-      emit(y, up, mid, dn, emid);
-      up = mid;
-      mid = dn;
-      emid = edn;
-    }
-  }
-}
-
-// ----------------------------------------------------------------- LdsTile
-// Workgroup tile: TW = 64*N columns x TH rows of outputs, 256 threads.
-template <typename T, int TH>
-__global__ __launch_bounds__(kBlock) void stencil5_lds_kernel(const T* __restrict__ in, T* __restrict__ out,
-                                                              index_t pitch, index_t core_off, index_t W,
-                                                              index_t row_begin, index_t row_end, T c0, T c1) {
-  constexpr int N = Vec16<T>::N;
-  constexpr int TW = kWaveSize * N;
-  constexpr int LW = TW + 2 * N;  // staged row: one extra vector on each side (keeps 16 B alignment)
-  using V = typename Vec16<T>::type;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  T* tile = reinterpret_cast<T*>(smem_raw);  // (TH + 2) x LW
-
-  const index_t x0 = index_t(blockIdx.x) * TW;
-  const index_t y0 = row_begin + index_t(blockIdx.y) * TH;
-  const index_t rows = (y0 + TH <= row_end) ? TH : (row_end - y0);
-  const int nvec = LW / N;  // vectors per staged row
-  // Stage rows y0-1 .. y0+rows (inclusive), columns x0-N .. x0+TW+N-1.
-  for (int i = threadIdx.x; i < (rows + 2) * nvec; i += kBlock) {
-    const int r = i / nvec, v = i - r * nvec;
-    const index_t gx = x0 - N + index_t(v) * N;
-    V val = V(T(0));
-    if (gx < W + N) val = *reinterpret_cast<const V*>(in + core_off + (y0 - 1 + r) * pitch + gx);
-    *reinterpret_cast<V*>(tile + r * LW + v * N) = val;
-  }
-  __syncthreads();
-  // Each thread: one column group of N, rows strided by 4 (one wave per row).
-  const int lane = threadIdx.x & (kWaveSize - 1);
-  const int wave = threadIdx.x / kWaveSize;
-  const index_t x = x0 + index_t(lane) * N;
-  if (x >= W) return;
-  for (int r = wave; r < rows; r += kWavesPerBlock) {
-    const T* up = tile + r * LW + N + lane * N;
-    const T* mid = up + LW;
-    const T* dn = mid + LW;
-    V o;
-#pragma unroll
-    for (int i = 0; i < N; ++i) o[i] = jac<T>(mid[i], up[i], dn[i], mid[i - 1], mid[i + 1], c0, c1);
-    T* p = out + core_off + (y0 + r) * pitch + x;
-    if (x + N <= W) {
-      *reinterpret_cast<V*>(p) = o;
-    } else {
-#pragma unroll
-      for (int i = 0; i < N; ++i)
-        if (x + i < W) p[i] = o[i];
-    }
-  }
-}
-
-// ------------------------------------------------------------------ rect
-template <typename T>
-__global__ __launch_bounds__(kBlock) void stencil5_rect_kernel(const T* __restrict__ in, T* __restrict__ out,
-                                                               index_t pitch, index_t core_off, index_t x0,
-                                                               index_t w, index_t y0, index_t h, T c0, T c1) {
-  const index_t n = w * h;
-  const index_t stride = index_t(gridDim.x) * blockDim.x;
-  for (index_t i = index_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const index_t yy = i / w, xx = i - yy * w;
-    const index_t o = core_off + (y0 + yy) * pitch + (x0 + xx);
-    out[o] = jac<T>(in[o], in[o - pitch], in[o + pitch], in[o - 1], in[o + 1], c0, c1);
-  }
-}
-
-// -------------------------------------------------------------- box (LDS)
-// Output tile 64 x 16 per 256-thread workgroup: thread (tx, ty) computes column
-// tx, rows 4*ty .. 4*ty+3. The (16+2R) x (64+2R) input tile is staged in LDS once;
-// every output then reads its (2R+1)^2 taps from LDS, rolling down the 4 rows.
-template <typename T, int R>
-__global__ __launch_bounds__(kBlock) void stencil_box_kernel(const T* __restrict__ in, T* __restrict__ out,
-                                                             index_t pitch, index_t core_off, index_t x0,
-                                                             index_t w, index_t y0, index_t h, BoxWeights bw) {
-  constexpr int TW = 64, TH = 16, LW = TW + 2 * R + 1;  // +1 breaks the power-of-two row stride
-  constexpr int LH = TH + 2 * R, K = 2 * R + 1;
-  __shared__ T tile[LH * LW];
-  const index_t bx = x0 + index_t(blockIdx.x) * TW;
-  const index_t by = y0 + index_t(blockIdx.y) * TH;
-  for (int i = threadIdx.x; i < LH * (TW + 2 * R); i += kBlock) {
-    const int r = i / (TW + 2 * R), c = i - r * (TW + 2 * R);
-    const index_t gx = bx - R + c, gy = by - R + r;
-    // Cells past the rectangle are never written; clamp reads to the tile + ghost ring.
-    T v = T(0);
-    if (gx < x0 + w + R && gy < y0 + h + R) v = in[core_off + gy * pitch + gx];
-    tile[r * LW + c] = v;
-  }
-  __syncthreads();
-  float wk[K * K];
-#pragma unroll
-  for (int i = 0; i < K * K; ++i) wk[i] = bw.w[i];
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const index_t gx = bx + tx;
-  if (gx >= x0 + w) return;
-#pragma unroll
-  for (int rr = 0; rr < 4; ++rr) {
-    const int r = ty * 4 + rr;
-    const index_t gy = by + r;
-    if (gy >= y0 + h) break;
-    T acc = T(0);
-#pragma unroll
-    for (int ky = 0; ky < K; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < K; ++kx) acc = fma_t<T>(T(wk[ky * K + kx]), tile[(r + ky) * LW + tx + kx], acc);
-    out[core_off + gy * pitch + gx] = acc;
-  }
-}
-
-// Tuned defaults (see docs/PERF.md for the sweep behind them).
-constexpr int kRollRows = 32;
-constexpr int kRollChunk = 8;
+using namespace detail;
 constexpr int kLdsRows = 16;
+
+// Tuned on MI355X with bench/stencil_tune.hip (profiles/stencil_tuning/*.log):
+// short strips whose ROWS+2 row loads are all issued up front beat long rolling
+// strips — the extra rows a short strip re-reads are L2/Infinity-Cache hits
+// (vertically adjacent strips run concurrently on the same XCD), while
+// per-wave bytes in flight are what the HBM stream needs. 4 waves side by side
+// cover 4 KiB of a row per workgroup. 3-row strips are best up to ~16K-wide
+// tiles, 4-row strips on wider ones (32768^2: 738 vs 731 Gcells/s).
+template <typename T, int ROWS>
+void launch_roll(const T* in, T* out, const TileGeom& g, index_t row_begin, index_t row_end, T c0, T c1,
+                 hipStream_t s) {
+  constexpr int N = Vec16<T>::N;
+  constexpr int WX = 4, NW = 4;
+  const index_t rows = row_end - row_begin;
+  const index_t gx = (g.width + index_t(kWaveSize) * N * WX - 1) / (index_t(kWaveSize) * N * WX);
+  const index_t gy = (rows + ROWS - 1) / ROWS;
+  stencil5_roll_kernel<T, ROWS, ROWS, true, WX, false, NW><<<dim3(unsigned(gx), unsigned(gy)), NW * kWaveSize, 0, s>>>(
+      in, out, g.pitch, g.core_offset(), g.width, row_begin, row_end, c0, c1);
+}
 
 }  // namespace
 
@@ -287,9 +85,8 @@ void stencil5_rows(const T* in, T* out, const TileGeom& g, index_t row_begin, in
     stencil5_lds_kernel<T, kLdsRows><<<dim3(unsigned(gx), unsigned(gy)), kBlock, lds, s>>>(
         in, out, g.pitch, g.core_offset(), g.width, row_begin, row_end, c0, c1);
   } else {
-    const index_t gy = (rows + index_t(kWavesPerBlock) * kRollRows - 1) / (index_t(kWavesPerBlock) * kRollRows);
-    stencil5_roll_kernel<T, kRollRows, kRollChunk, true><<<dim3(unsigned(gx), unsigned(gy)), kBlock, 0, s>>>(
-        in, out, g.pitch, g.core_offset(), g.width, row_begin, row_end, c0, c1);
+    if (g.width * int(sizeof(T)) >= 32768 * 4) launch_roll<T, 4>(in, out, g, row_begin, row_end, c0, c1, s);
+    else launch_roll<T, 3>(in, out, g, row_begin, row_end, c0, c1, s);
   }
   MXS_HIP_CHECK_LAUNCH();
 }

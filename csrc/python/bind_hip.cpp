@@ -293,9 +293,9 @@ PYBIND11_MODULE(_mxs_hip, m) {
            [](SolverHandle& h) {
              return h.visit([](auto& s) { return reinterpret_cast<std::uintptr_t>(s.current()); });
            })
-      .def("compute_stream",
+      .def("main_stream",
            [](SolverHandle& h) {
-             return h.visit([](auto& s) { return reinterpret_cast<std::uintptr_t>(s.compute_stream()); });
+             return h.visit([](auto& s) { return reinterpret_cast<std::uintptr_t>(s.main_stream()); });
            })
       .def("graph_active", [](SolverHandle& h) { return h.visit([](auto& s) { return s.graph_active(); }); })
       .def("graph_status", [](SolverHandle& h) { return h.visit([](auto& s) { return s.graph_status(); }); });

@@ -7,9 +7,9 @@ namespace mxs {
 template <typename T>
 StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGeom& tile, T* buf_a, T* buf_b,
                                 const RcclComm* comm, const SolverConfig& cfg)
-    : tile_(tile), cfg_(cfg), cur_(buf_a), nxt_(buf_b), compute_(true, 0), comm_(true, -1) {
-  // The comm stream gets the higher priority (lower number): its short pack /
-  // unpack launches should not queue behind a long interior sweep.
+    : tile_(tile), cfg_(cfg), cur_(buf_a), nxt_(buf_b), main_(true, -1), side_(true, 0) {
+  // The main stream gets the higher priority (lower number): its short pack /
+  // unpack / boundary launches should not queue behind the long interior sweep.
   const int radius = cfg_.kind == StencilKind::Box ? cfg_.box.radius : 1;
   MXS_CHECK(tile_.halo_x >= radius && tile_.halo_y >= radius, "ghost ring narrower than the stencil radius");
   const bool corners = cfg_.corners || cfg_.kind == StencilKind::Box;
@@ -21,51 +21,56 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
 
 template <typename T>
 StencilSolver<T>::~StencilSolver() {
-  (void)hipStreamSynchronize(compute_.get());
-  (void)hipStreamSynchronize(comm_.get());
+  (void)hipStreamSynchronize(main_.get());
+  (void)hipStreamSynchronize(side_.get());
 }
 
 template <typename T>
-void StencilSolver<T>::update(const T* in, T* out, index_t r0, index_t r1, bool /*full_rows*/) {
+void StencilSolver<T>::update(const T* in, T* out, index_t r0, index_t r1, hipStream_t s) {
   if (r1 <= r0) return;
   if (cfg_.kind == StencilKind::Jacobi5)
-    kernels::stencil5_rows<T>(in, out, tile_, r0, r1, cfg_.coeffs, compute_.get(), cfg_.variant);
+    kernels::stencil5_rows<T>(in, out, tile_, r0, r1, cfg_.coeffs, s, cfg_.variant);
   else
-    kernels::stencil_box<T>(in, out, tile_, 0, tile_.width, r0, r1, cfg_.box, compute_.get());
+    kernels::stencil_box<T>(in, out, tile_, 0, tile_.width, r0, r1, cfg_.box, s);
 }
 
 template <typename T>
-void StencilSolver<T>::update_cols(const T* in, T* out, index_t r0, index_t r1) {
+void StencilSolver<T>::update_cols(const T* in, T* out, index_t r0, index_t r1, hipStream_t s) {
   if (r1 <= r0) return;
   const index_t w = tile_.width;
   const index_t r = cfg_.kind == StencilKind::Box ? cfg_.box.radius : 1;
   if (cfg_.kind == StencilKind::Jacobi5) {
-    kernels::stencil5_rect<T>(in, out, tile_, 0, r, r0, r1, cfg_.coeffs, compute_.get());
-    kernels::stencil5_rect<T>(in, out, tile_, w - r, w, r0, r1, cfg_.coeffs, compute_.get());
+    kernels::stencil5_rect<T>(in, out, tile_, 0, r, r0, r1, cfg_.coeffs, s);
+    kernels::stencil5_rect<T>(in, out, tile_, w - r, w, r0, r1, cfg_.coeffs, s);
   } else {
-    kernels::stencil_box<T>(in, out, tile_, 0, r, r0, r1, cfg_.box, compute_.get());
-    kernels::stencil_box<T>(in, out, tile_, w - r, w, r0, r1, cfg_.box, compute_.get());
+    kernels::stencil_box<T>(in, out, tile_, 0, r, r0, r1, cfg_.box, s);
+    kernels::stencil_box<T>(in, out, tile_, w - r, w, r0, r1, cfg_.box, s);
   }
 }
 
+// Stream roles: the MAIN stream (the capture origin, high priority) carries the
+// exchange chain pack -> RCCL -> unpack and the boundary update; the interior
+// sweep forks onto the SIDE stream. RCCL calls must sit on the capture-origin
+// stream: captured from a forked stream, RCCL (ROCm 7.x) crashes at capture.
 template <typename T>
 void StencilSolver<T>::enqueue_step(T* cur, T* nxt) {
   const index_t h = tile_.height;
+  hipStream_t m = main_.get(), side = side_.get();
   if (!cfg_.overlap) {
-    ex_->exchange(cur, compute_.get());
-    update(cur, nxt, 0, h, true);
+    ex_->exchange(cur, m);
+    update(cur, nxt, 0, h, m);
     return;
   }
   const index_t r = cfg_.kind == StencilKind::Box ? cfg_.box.radius : 1;
-  ready_.record(compute_.get());
-  ready_.wait_on(comm_.get());
-  ex_->exchange(cur, comm_.get());
-  halo_.record(comm_.get());
-  update(cur, nxt, r, h - r, true);  // interior (its edge columns are redone below)
-  halo_.wait_on(compute_.get());
-  update(cur, nxt, 0, r, true);
-  update(cur, nxt, h - r, h, true);
-  update_cols(cur, nxt, r, h - r);
+  fork_.record(m);
+  fork_.wait_on(side);
+  update(cur, nxt, r, h - r, side);  // interior (its edge columns are redone below)
+  interior_.record(side);
+  ex_->exchange(cur, m);
+  interior_.wait_on(m);
+  update(cur, nxt, 0, r, m);
+  update(cur, nxt, h - r, h, m);
+  update_cols(cur, nxt, r, h - r, m);
 }
 
 template <typename T>
@@ -76,7 +81,7 @@ bool StencilSolver<T>::try_capture() {
     T* a = k == 0 ? cur_ : nxt_;
     T* b = k == 0 ? nxt_ : cur_;
     hipGraph_t g = nullptr;
-    if (hipStreamBeginCapture(compute_.get(), hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    if (hipStreamBeginCapture(main_.get(), hipStreamCaptureModeThreadLocal) != hipSuccess) {
       (void)hipGetLastError();
       graph_status_ = "hipStreamBeginCapture failed";
       return false;
@@ -88,7 +93,7 @@ bool StencilSolver<T>::try_capture() {
       graph_status_ = std::string("capture failed: ") + e.what();
       ok = false;
     }
-    const hipError_t end = hipStreamEndCapture(compute_.get(), &g);
+    const hipError_t end = hipStreamEndCapture(main_.get(), &g);
     if (!ok || end != hipSuccess || g == nullptr) {
       (void)hipGetLastError();
       if (ok) graph_status_ = "hipStreamEndCapture failed";
@@ -111,7 +116,7 @@ template <typename T>
 void StencilSolver<T>::step() {
   if (cfg_.use_graph && !graph_tried_) try_capture();
   if (graphs_[0].valid()) {
-    graphs_[parity_].launch(compute_.get());
+    graphs_[parity_].launch(main_.get());
     parity_ ^= 1;
   } else {
     enqueue_step(cur_, nxt_);
@@ -126,13 +131,13 @@ void StencilSolver<T>::run(int iters) {
 
 template <typename T>
 void StencilSolver<T>::exchange_only() {
-  ex_->exchange(cur_, compute_.get());
+  ex_->exchange(cur_, main_.get());
 }
 
 template <typename T>
 void StencilSolver<T>::synchronize() {
-  compute_.sync();
-  comm_.sync();
+  main_.sync();
+  side_.sync();
 }
 
 template class StencilSolver<float>;
