@@ -1,0 +1,252 @@
+// stencil2d — 2D domain-decomposed stencil on MI355X GPUs.
+// Reference: stencil2d/mpi-2d-stencil-subarray-cuda.cu (+ stencil2d/stencil2D.h).
+//
+// MPI is the control plane (ranks, Cartesian grid, RCCL bootstrap, timing);
+// device data moves by one of:
+//   --backend rccl        per-peer ncclSend/ncclRecv over xGMI (default when every
+//                         rank has its own GPU), compute/comm overlap + hipGraph;
+//   --backend mpi-staged  HIP pack -> pinned host staging -> MPI -> HIP unpack
+//                         (default when ranks share a GPU; --pageable for the
+//                         non-PAGE_LOCKED variant);
+//   --backend local       1x1 periodic grid: a single HIP self-copy launch.
+//
+//   mpiexec -n 9 stencil2d            # reference run: 16x16 tiles, 5x5 stencil, fp64,
+//                                     # one exchange, per-rank dump files "row_col"
+//   mpiexec -n 8 stencil2d --global 32768x32768 --dims 2x4 --dtype f32 --iters 200
+//
+// Positional arguments keep the reference contract: [local width (= height) [stencil width]].
+// More options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
+// --iters N, --warmup N, --no-overlap, --no-graph, --loopback, --bind bunch|rrobin,
+// --dump / --no-dump, --checksum, --non-periodic, --seed S, --json FILE.
+#include <mpi.h>
+
+#include <cmath>
+#include <fstream>
+#include <iostream>
+#include <memory>
+#include <sstream>
+#include <vector>
+
+#include "app_common.hpp"
+#include "mxs/comm/mpi_env.hpp"
+#include "mxs/comm/mpi_halo.hpp"
+#include "mxs/comm/rccl_comm.hpp"
+#include "mxs/core/cli.hpp"
+#include "mxs/core/device.hpp"
+#include "mxs/kernels/kernels.hpp"
+#include "mxs/runtime/stencil_solver.hpp"
+
+using namespace mxs;
+
+namespace {
+
+std::unique_ptr<RcclComm> make_comm(const MpiEnv& env) {
+  std::string uid = env.rank() == 0 ? RcclComm::make_unique_id() : std::string(sizeof(ncclUniqueId), '\0');
+  MXS_MPI_CHECK(MPI_Bcast(&uid[0], int(uid.size()), MPI_BYTE, 0, MPI_COMM_WORLD));
+  return std::make_unique<RcclComm>(uid, env.size(), env.rank());
+}
+
+template <typename T>
+void copy_tile_to_host(std::vector<T>& h, const T* d, const TileGeom& g) {
+  h.resize(size_t(g.alloc_elems()));
+  MXS_HIP_CHECK(hipMemcpy(h.data(), d, h.size() * sizeof(T), hipMemcpyDeviceToHost));
+}
+
+template <typename T>
+int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBinding& dev, index_t lw, index_t lh,
+        index_t gx0, index_t gy0, index_t gw, index_t gh, int sw, int sh) {
+  const int rank = env.rank();
+  const TileGeom g = TileGeom::aligned(lw, lh, sw / 2, sh / 2, int(sizeof(T)));
+  const long long iters = cli.get_int("iters", 0);
+  const bool dump = cli.has("dump") ? cli.flag("dump") : (iters == 0 && lw <= 64 && lh <= 64 && !cli.flag("no-dump"));
+
+  // Backend selection.
+  std::string backend = cli.get("backend", "auto");
+  const bool loopback = cli.flag("loopback");
+  if (backend == "auto") {
+    if (env.size() == 1) backend = loopback ? "rccl" : "local";
+    else if (env.local_size() > dev.devices_used) backend = "mpi-staged";  // GPUs shared: RCCL refuses
+    else backend = "rccl";
+  }
+  std::unique_ptr<RcclComm> comm;
+  if (backend == "rccl") comm = make_comm(env);
+
+  DeviceBuffer<T> a(g.alloc_elems()), b(g.alloc_elems());
+  Stream init_stream;
+  MPI_Comm cart = make_cart_comm(topo);
+
+  SolverConfig cfg;
+  cfg.backend = backend == "rccl" ? HaloBackend::Rccl : HaloBackend::Local;
+  cfg.overlap = !cli.flag("no-overlap");
+  cfg.use_graph = !cli.flag("no-graph");
+  cfg.loopback_self = loopback;
+  cfg.coeffs = {cli.get_double("c-center", 0.2), cli.get_double("c-neighbor", 0.2)};
+  std::unique_ptr<StencilSolver<T>> solver;
+  std::unique_ptr<MpiStagedHalo<T>> staged;
+  const HaloPlan plan = make_halo_plan(topo, rank, g, true, loopback);
+  if (backend == "mpi-staged") {
+    staged = std::make_unique<MpiStagedHalo<T>>(plan, cart, !cli.flag("pageable"));
+  } else {
+    MXS_CHECK(backend == "rccl" || backend == "local", "unknown backend " << backend);
+    solver = std::make_unique<StencilSolver<T>>(topo, rank, g, a.get(), b.get(), comm.get(), cfg);
+  }
+
+  if (iters == 0) {
+    // Reference run: ghosts -1, core = rank id, one exchange, dump before/after.
+    kernels::fill<T>(a.get(), g.alloc_elems(), T(-1), init_stream.get());
+    kernels::fill_region<T>(a.get(), g.core(), T(rank), init_stream.get());
+    init_stream.sync();
+    std::ostringstream os;
+    std::vector<T> h;
+    if (dump) {
+      copy_tile_to_host(h, a.get(), g);
+      write_dump_header(os, topo, rank, dev.device, lw, lh, sw, sh, "HIP");
+      os << "Array" << '\n';
+      app::dump_tile(os, h.data(), g);
+      os << '\n';
+    }
+    if (staged) {
+      staged->exchange(a.get(), init_stream.get());
+      init_stream.sync();
+    } else {
+      solver->exchange_only();
+      solver->synchronize();
+    }
+    if (dump) {
+      copy_tile_to_host(h, a.get(), g);
+      os << "Array after exchange" << '\n';
+      app::dump_tile(os, h.data(), g);
+      std::ofstream f(dump_file_name(topo, rank));
+      f << os.str();
+    }
+  } else {
+    kernels::fill<T>(a.get(), g.alloc_elems(), T(0), init_stream.get());
+    kernels::fill<T>(b.get(), g.alloc_elems(), T(0), init_stream.get());
+    kernels::fill_random<T>(a.get(), g, gx0, gy0, gw, std::uint64_t(cli.get_int("seed", 1234)), T(0), T(1),
+                            init_stream.get());
+    init_stream.sync();
+    T* cur = a.get();
+    T* nxt = b.get();
+    auto steps = [&](long long n) {
+      if (solver) {
+        solver->run(int(n));
+        return;
+      }
+      for (long long i = 0; i < n; ++i) {
+        staged->exchange(cur, init_stream.get());
+        kernels::stencil5_rows<T>(cur, nxt, g, 0, lh, cfg.coeffs, init_stream.get());
+        std::swap(cur, nxt);
+      }
+    };
+    auto sync = [&]() {
+      if (solver) solver->synchronize();
+      init_stream.sync();
+    };
+    const long long warmup = cli.get_int("warmup", 10);
+    steps(warmup);
+    sync();
+    env.barrier();
+    const double t0 = MPI_Wtime();
+    steps(iters);
+    sync();
+    env.barrier();
+    const double dt = env.max_over_ranks(MPI_Wtime() - t0);
+    if (solver) cur = solver->current();
+    const double gcells = double(gw) * double(gh) * double(iters) / dt / 1e9;
+    double checksum = std::nan("");
+    const bool want_sum = cli.has("checksum") ? cli.flag("checksum") : (lw * lh <= (index_t(1) << 24));
+    if (want_sum) {
+      std::vector<T> h;
+      copy_tile_to_host(h, cur, g);
+      double local = 0;
+      for (index_t y = 0; y < lh; ++y)
+        for (index_t x = 0; x < lw; ++x) local += double(h[size_t(g.core_offset() + y * g.pitch + x)]);
+      checksum = env.sum_over_ranks(local);
+    }
+    if (rank == 0) {
+      std::ostringstream js;
+      js << "{\"app\": \"stencil2d\", \"metric\": \"gcells_per_s\", \"value\": " << app::fmt(gcells)
+         << ", \"ms_per_iter\": " << app::fmt(dt / double(iters) * 1e3) << ", \"ranks\": " << env.size()
+         << ", \"dims\": \"" << topo.rows << "x" << topo.cols << "\", \"global\": \"" << gw << "x" << gh
+         << "\", \"dtype\": \"" << (sizeof(T) == 4 ? "f32" : "f64") << "\", \"backend\": \"" << backend
+         << "\", \"graph\": \"" << (solver ? solver->graph_status() : std::string("n/a")) << "\", \"iters\": " << iters;
+      if (want_sum) js << ", \"checksum\": " << app::fmt(checksum);
+      js << "}";
+      std::cout << "Gcells/s: " << app::fmt(gcells) << '\n';
+      if (want_sum) std::cout << "checksum: " << app::fmt(checksum) << '\n';
+      std::cout << js.str() << std::endl;
+      app::append_json(cli.get("json"), js.str());
+    }
+  }
+  solver.reset();
+  staged.reset();
+  MPI_Comm_free(&cart);
+  return 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  MpiEnv env(&argc, &argv);
+  Cli cli(argc, argv, {"dump", "no-dump", "non-periodic", "strict-square", "no-overlap", "no-graph", "loopback",
+                       "pageable", "checksum"});
+  const DeviceBinding dev = bind_device(env, cli.get("bind", "bunch"));
+  const int n = env.size();
+  int rows, cols;
+  const int dim = int(std::lround(std::sqrt(double(n))));
+  if (cli.has("dims")) {
+    auto d = parse_dims(cli.get("dims"));
+    rows = d[0];
+    cols = d[1];
+  } else if (dim * dim == n) {
+    rows = cols = dim;
+  } else {
+    if (cli.flag("strict-square")) {
+      if (env.rank() == 0) std::cerr << "Numer of MPI tasks must be a perfect square" << std::endl;
+      return 1;
+    }
+    auto d = dims_create(n);
+    rows = d[0];
+    cols = d[1];
+  }
+  if (rows * cols != n) {
+    if (env.rank() == 0) std::cerr << "process grid " << rows << "x" << cols << " != " << n << " ranks" << std::endl;
+    return 1;
+  }
+  const bool periodic = !cli.flag("non-periodic");
+  const CartTopology topo(rows, cols, periodic, periodic);
+  const auto c = topo.coords(env.rank());
+  const auto& pos = cli.positional();
+  index_t gw = 0, gh = 0, lw = 16, lh = 16, gx0 = 0, gy0 = 0;
+  int sw = 5;
+  if (!pos.empty()) lw = lh = std::atoll(pos[0].c_str());
+  if (pos.size() >= 2) sw = std::atoi(pos[1].c_str());
+  if (cli.has("stencil")) sw = int(cli.get_int("stencil", sw));
+  const int sh = int(cli.get_int("stencil-height", sw));
+  if (cli.has("global")) {
+    auto wh = parse_wxh(cli.get("global"));
+    gw = wh.first;
+    gh = wh.second;
+    const Block1D bx = block_split(gw, cols, c[1]), by = block_split(gh, rows, c[0]);
+    lw = bx.len;
+    lh = by.len;
+    gx0 = bx.start;
+    gy0 = by.start;
+  } else {
+    if (cli.has("local")) {
+      auto wh = parse_wxh(cli.get("local"));
+      lw = wh.first;
+      lh = wh.second;
+    }
+    gw = lw * cols;
+    gh = lh * rows;
+    gx0 = lw * c[1];
+    gy0 = lh * c[0];
+  }
+  if (lw < sw || lh < sh) {
+    if (env.rank() == 0) std::cerr << "Error: grid size < stencil size" << std::endl;
+    return 1;
+  }
+  if (cli.get("dtype", "f64") == "f32") return run<float>(env, cli, topo, dev, lw, lh, gx0, gy0, gw, gh, sw, sh);
+  return run<double>(env, cli, topo, dev, lw, lh, gx0, gy0, gw, gh, sw, sh);
+}

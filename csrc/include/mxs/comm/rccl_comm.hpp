@@ -8,15 +8,25 @@
 // Python launcher. Bootstrap is therefore a plain byte string.
 #pragma once
 
-#define MXS_WITH_RCCL 1
 #include <rccl/rccl.h>
 
+#include <sstream>
 #include <string>
 #include <type_traits>
 
 #include "mxs/core/error.hpp"
 
 namespace mxs {
+
+inline void rccl_check(ncclResult_t res, const char* expr, const char* file, int line) {
+  if (res != ncclSuccess) {
+    std::ostringstream os;
+    os << where(file, line) << " - RCCL error " << int(res) << ": " << ncclGetErrorString(res) << " in `" << expr
+       << "`";
+    raise_error(os.str(), int(res));
+  }
+}
+#define MXS_RCCL_CHECK(expr) ::mxs::rccl_check((expr), #expr, __FILE__, __LINE__)
 
 template <typename T>
 constexpr ncclDataType_t rccl_type() {

@@ -81,19 +81,4 @@ inline void hip_check(hipError_t err, const char* expr, const char* file, int li
 #define MXS_HIP_CHECK_LAUNCH() ::mxs::hip_check(hipGetLastError(), "kernel launch", __FILE__, __LINE__)
 #endif
 
-#if defined(MXS_WITH_RCCL)
-#include <rccl/rccl.h>
-
-namespace mxs {
-inline void rccl_check(ncclResult_t res, const char* expr, const char* file, int line) {
-  if (res != ncclSuccess) {
-    std::ostringstream os;
-    os << where(file, line) << " - RCCL error " << int(res) << ": " << ncclGetErrorString(res)
-       << " in `" << expr << "`";
-    raise_error(os.str(), int(res));
-  }
-}
-}  // namespace mxs
-
-#define MXS_RCCL_CHECK(expr) ::mxs::rccl_check((expr), #expr, __FILE__, __LINE__)
-#endif
+// RCCL checks (MXS_RCCL_CHECK) live in comm/rccl_comm.hpp.

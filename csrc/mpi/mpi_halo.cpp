@@ -2,39 +2,6 @@
 
 namespace mxs {
 
-MPI_Comm make_cart_comm(const CartTopology& topo) {
-  int dims[2] = {topo.rows, topo.cols};
-  int periods[2] = {topo.periodic_rows ? 1 : 0, topo.periodic_cols ? 1 : 0};
-  MPI_Comm cart;
-  MXS_MPI_CHECK(MPI_Cart_create(MPI_COMM_WORLD, 2, dims, periods, /*reorder=*/0, &cart));
-  MPI_Comm_set_errhandler(cart, MPI_ERRORS_RETURN);
-  return cart;
-}
-
-template <typename T>
-MpiHostHalo<T>::MpiHostHalo(const CartTopology& topo, int rank, const TileGeom& tile, MPI_Comm comm, bool corners)
-    : comm_(comm) {
-  const index_t rows = tile.total_height();
-  for (int d = 0; d < kNumDirs; ++d) {
-    if (!corners && dir_is_corner(d)) continue;
-    const int tag = reference_tag(d);
-    const int from = topo.neighbor(rank, dir_opposite(d));
-    const int to = topo.neighbor(rank, d);
-    recvs_.push_back({from == kProcNull ? MPI_PROC_NULL : from, tag,
-                      make_subarray_type<T>(rows, recv_region(tile, dir_opposite(d)))});
-    sends_.push_back({to == kProcNull ? MPI_PROC_NULL : to, tag, make_subarray_type<T>(rows, send_region(tile, d))});
-  }
-}
-
-template <typename T>
-void MpiHostHalo<T>::exchange(T* tile) {
-  std::vector<MPI_Request> req(recvs_.size() + sends_.size());
-  size_t k = 0;
-  for (auto& r : recvs_) MXS_MPI_CHECK(MPI_Irecv(tile, 1, r.type.get(), r.peer, r.tag, comm_, &req[k++]));
-  for (auto& s : sends_) MXS_MPI_CHECK(MPI_Isend(tile, 1, s.type.get(), s.peer, s.tag, comm_, &req[k++]));
-  MXS_MPI_CHECK(MPI_Waitall(int(req.size()), req.data(), MPI_STATUSES_IGNORE));
-}
-
 template <typename T>
 MpiStagedHalo<T>::MpiStagedHalo(const HaloPlan& plan, MPI_Comm comm, bool page_locked)
     : plan_(plan), comm_(comm), progs_(build_halo_copy_programs(plan)) {
@@ -72,8 +39,6 @@ void MpiStagedHalo<T>::exchange(T* tile, hipStream_t stream) {
   kernels::copy2d_batch<T>(tile, dsend_.get(), drecv_.get(), progs_.unpack, stream);
 }
 
-template class MpiHostHalo<float>;
-template class MpiHostHalo<double>;
 template class MpiStagedHalo<float>;
 template class MpiStagedHalo<double>;
 

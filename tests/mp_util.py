@@ -1,0 +1,41 @@
+"""Launch N gloo ranks of tests/mp_worker.py (127.0.0.1 rendezvous) and collect
+their RESULT lines."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(task: str, nprocs: int, args: dict, timeout: int = 240) -> list[dict]:
+    port = free_port()
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ)
+        env.update(RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+                   OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "mp_worker.py"), task, json.dumps(args)],
+                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    results = []
+    try:
+        for p in procs:
+            out, err = p.communicate(timeout=timeout)
+            if p.returncode != 0:
+                raise RuntimeError(f"rank failed rc={p.returncode}\n{err[-3000:]}")
+            line = [ln for ln in out.splitlines() if ln.startswith("RESULT ")]
+            assert line, f"no result\nstdout={out[-2000:]}\nstderr={err[-2000:]}"
+            results.append(json.loads(line[-1][len("RESULT "):]))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return sorted(results, key=lambda r: r["rank"])

@@ -1,0 +1,85 @@
+"""Worker for multi-process (gloo) tests: one process per rank, launched by
+tests/mp_util.py with RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set.
+Prints one JSON line prefixed with ``RESULT `` on stdout."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from cuda_mpi_scratch_amd.models.stencil2d import Stencil2D, StencilConfig  # noqa: E402
+from cuda_mpi_scratch_amd.parallel import init  # noqa: E402
+
+
+def task_golden(args):
+    """Reference run: 16x16 tiles, 5x5 stencil, fp64, core = rank, one exchange."""
+    ctx = init(backend="gloo", device="cpu")
+    cfg = StencilConfig(global_width=16 * args["cols"], global_height=16 * args["rows"],
+                        dims=f"{args['rows']}x{args['cols']}", dtype="f64", stencil_width=5, init="rank")
+    st = Stencil2D(cfg, ctx, device="cpu")
+    before = st.full_view().clone()
+    st.exchange()
+    text = st.dump_text([("Array", before), ("Array after exchange", st.full_view())])
+    ctx.destroy()
+    return {"rank": ctx.rank, "coords": [st.decomp.row, st.decomp.col], "text": text}
+
+
+def task_jacobi(args):
+    """Random init + N iterations; returns the global grid (rank 0)."""
+    ctx = init(backend="gloo", device="cpu")
+    cfg = StencilConfig(global_width=args["w"], global_height=args["h"], dims=args["dims"],
+                        dtype=args.get("dtype", "f32"), seed=args.get("seed", 5), kind=args.get("kind", "jacobi5"),
+                        box_weights=args.get("box_weights", []), stencil_width=args.get("stencil_width", 3))
+    st = Stencil2D(cfg, ctx, device="cpu")
+    st.run(args["iters"])
+    g = st.gather_global()
+    ctx.destroy()
+    out = {"rank": ctx.rank}
+    if ctx.rank == 0:
+        out["grid"] = g.double().tolist()
+    return out
+
+
+def task_halo_property(args):
+    """Non-square tiles and grids: after one exchange every ghost cell holds the
+    owning neighbour's core value (cell value = global linear index)."""
+    from cuda_mpi_scratch_amd.ops import fill_region  # noqa: F401
+
+    ctx = init(backend="gloo", device="cpu")
+    rows, cols = args["rows"], args["cols"]
+    w, h, halo = args["w"], args["h"], args["halo"]
+    gw, gh = w * cols, h * rows
+    cfg = StencilConfig(global_width=gw, global_height=gh, dims=f"{rows}x{cols}", dtype="f64",
+                        stencil_width=2 * halo + 1, init="rank", periodic=args.get("periodic", True))
+    st = Stencil2D(cfg, ctx, device="cpu")
+    d = st.decomp
+    core = st.core_view()
+    ys = torch.arange(d.y0, d.y0 + d.height, dtype=torch.float64)[:, None]
+    xs = torch.arange(d.x0, d.x0 + d.width, dtype=torch.float64)[None, :]
+    core.copy_(ys * gw + xs)
+    full = st.full_view()
+    st.exchange()
+    bad = 0
+    for ly in range(full.shape[0]):
+        for lx in range(full.shape[1]):
+            gy, gx = d.y0 + ly - halo, d.x0 + lx - halo
+            inside = 0 <= gy < gh and 0 <= gx < gw
+            if not inside and not cfg.periodic:
+                continue
+            gy %= gh
+            gx %= gw
+            if float(full[ly, lx]) != float(gy * gw + gx):
+                bad += 1
+    ctx.destroy()
+    return {"rank": ctx.rank, "bad": bad}
+
+
+if __name__ == "__main__":
+    task = sys.argv[1]
+    args = json.loads(sys.argv[2])
+    res = globals()[f"task_{task}"](args)
+    sys.stdout.write("RESULT " + json.dumps(res) + "\n")
+    sys.stdout.flush()
