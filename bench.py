@@ -80,7 +80,7 @@ def main(argv=None) -> int:
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup)
     value = st.cells_per_step * args.steps / dt / 1e9
-    extras: dict = {"backend": st.backend, "graph": st.graph_status(),
+    extras: dict = {"backend": st.backend, "halo": st.halo_mode(), "graph": st.graph_status(),
                     "tile": f"{st.decomp.width}x{st.decomp.height}"}
     del st
     torch.cuda.empty_cache()

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "mxs/core/error.hpp"
+#include "mxs/kernels/kernels.hpp"
 #include "mxs/runtime/hip_utils.hpp"
 #include "../csrc/kernels/stencil_device.hpp"
 
@@ -29,6 +30,7 @@ struct Variant {
   std::string name;
   std::function<void(hipStream_t)> launch;
   std::vector<float> ms;
+  int steps = 1;  // Jacobi iterations per launch
 };
 
 template <int ROWS, int CH, bool NT, int WX, bool NTL, int NW = 4>
@@ -44,14 +46,47 @@ Variant roll(const float* in, float* out, const TileGeom& g) {
           }};
 }
 
+template <int S, int TW, int TH>
+Variant tb(const float* in, float* out, const TileGeom& g) {
+  char buf[128];
+  std::snprintf(buf, sizeof(buf), "tb_s%d_tw%d_th%d", S, TW, TH);
+  Variant v{buf, [=](hipStream_t s) {
+              const size_t lds = tb_lds_bytes<float, S, TW, TH>();
+              const dim3 grid(unsigned((g.width + TW - 1) / TW), unsigned((g.height + TH - 1) / TH));
+              stencil5_tb_kernel<float, S, TW, TH, true><<<grid, 256, lds, s>>>(
+                  in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, 0.2f, 0.2f);
+            }};
+  v.steps = S;
+  return v;
+}
+
+template <int S, int TW, int TH, bool WRAP = true>
+Variant tb1(const float* in, float* out, const TileGeom& g) {
+  char buf[128];
+  std::snprintf(buf, sizeof(buf), "tb1_s%d_tw%d_th%d%s", S, TW, TH, WRAP ? "_wrap" : "");
+  Variant v{buf, [=](hipStream_t s) {
+              const size_t lds = tb1_lds_bytes<float, S, TW, TH>();
+              const dim3 grid(unsigned((g.width + TW - 1) / TW), unsigned((g.height + TH - 1) / TH));
+              stencil5_tb1_kernel<float, S, TW, TH, WRAP><<<grid, 256, lds, s>>>(
+                  in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, 0.2f, 0.2f);
+            }};
+  v.steps = S;
+  return v;
+}
+
 int main(int argc, char** argv) {
   const index_t W = argc > 1 ? atol(argv[1]) : 32768;
   const index_t H = argc > 2 ? atol(argv[2]) : 32768;
   const int rounds = argc > 3 ? atoi(argv[3]) : 5;
-  const TileGeom g = TileGeom::aligned(W, H, 1, 1, 4);
+  const TileGeom g = TileGeom::aligned(W, H, 8, 8, 4);  // 8-deep ghost ring: non-wrap tb variants up to S = 8
   DeviceBuffer<float> a(g.alloc_elems()), b(g.alloc_elems());
-  MXS_HIP_CHECK(hipMemset(a.get(), 0, a.bytes()));
-  MXS_HIP_CHECK(hipMemset(b.get(), 0, b.bytes()));
+  // Random data: zero-filled operands raise the clock under load and inflate
+  // the numbers (cdna_hip_programming.md §5.4 rule 25).
+  kernels::fill<float>(a.get(), g.alloc_elems(), 0.f, nullptr);
+  kernels::fill<float>(b.get(), g.alloc_elems(), 0.f, nullptr);
+  kernels::fill_random<float>(a.get(), g, 0, 0, W, 7, 0.f, 1.f, nullptr);
+  kernels::fill_random<float>(b.get(), g, 0, 0, W, 8, 0.f, 1.f, nullptr);
+  MXS_HIP_CHECK(hipDeviceSynchronize());
   const float* in = a.get();
   float* out = b.get();
   std::vector<Variant> vs;
@@ -64,24 +99,39 @@ int main(int argc, char** argv) {
                   stencil5_lds_kernel<float, 16><<<dim3(gx, gy), 256, (16 + 2) * (256 + 8) * 4, s>>>(
                       in, out, g.pitch, g.core_offset(), W, 0, H, 0.2f, 0.2f);
                 }});
-  vs.push_back(roll<8, 8, true, 4, false>(in, out, g));
-  vs.push_back(roll<4, 4, true, 4, false>(in, out, g));
-  vs.push_back(roll<2, 2, true, 4, false>(in, out, g));
   vs.push_back(roll<3, 3, true, 4, false>(in, out, g));
-  vs.push_back(roll<4, 4, true, 4, false, 8>(in, out, g));
-  vs.push_back(roll<4, 4, true, 8, false, 8>(in, out, g));
-  vs.push_back(roll<4, 4, true, 2, false, 4>(in, out, g));
-  vs.push_back(roll<4, 4, true, 2, false, 2>(in, out, g));
-  vs.push_back(roll<4, 4, true, 1, false, 1>(in, out, g));
-  vs.push_back(roll<2, 2, true, 8, false, 8>(in, out, g));
-  vs.push_back(roll<4, 4, true, 16, false, 16>(in, out, g));
-  vs.push_back(roll<4, 4, false, 4, false>(in, out, g));
-  vs.push_back(roll<4, 2, true, 4, false>(in, out, g));
+  vs.push_back(roll<4, 4, true, 4, false>(in, out, g));
+  vs.push_back(tb1<2, 128, 32, false>(in, out, g));
+  vs.push_back(tb1<3, 128, 32, false>(in, out, g));
+  vs.push_back(tb1<4, 128, 32, false>(in, out, g));
+  vs.push_back(tb1<4, 128, 32, true>(in, out, g));
+  vs.push_back(tb1<4, 128, 24, false>(in, out, g));
+  vs.push_back(tb1<4, 192, 24, false>(in, out, g));
+  vs.push_back(tb1<4, 128, 16, false>(in, out, g));
+  vs.push_back(tb1<5, 128, 32, false>(in, out, g));
+  vs.push_back(tb1<6, 128, 32, false>(in, out, g));
+  vs.push_back(tb1<6, 128, 24, false>(in, out, g));
+  vs.push_back(tb1<8, 128, 32, false>(in, out, g));
+  vs.push_back(tb1<8, 128, 48, false>(in, out, g));
+  vs.push_back(tb1<4, 64, 32, false>(in, out, g));
+  vs.push_back(tb1<4, 64, 64, false>(in, out, g));
 
   Stream st;
   Event e0(true), e1(true);
-  for (auto& v : vs) v.launch(st.get());  // warm-up / first-touch
-  st.sync();
+  // Warm-up / first-touch; drop variants whose launch is rejected (e.g. LDS over the limit).
+  std::vector<Variant> ok;
+  for (auto& v : vs) {
+    (void)hipGetLastError();
+    v.launch(st.get());
+    const hipError_t e = hipGetLastError();
+    st.sync();
+    if (e != hipSuccess) {
+      std::printf("{\"variant\": \"%s\", \"error\": \"%s\"}\n", v.name.c_str(), hipGetErrorString(e));
+      continue;
+    }
+    ok.push_back(std::move(v));
+  }
+  vs = std::move(ok);
   for (int r = 0; r < rounds; ++r)
     for (auto& v : vs) {
       e0.record(st.get());
@@ -96,7 +146,8 @@ int main(int argc, char** argv) {
     const double med = v.ms[v.ms.size() / 2], best = v.ms[0];
     const double cbytes = v.name == "copy_float4" ? 2.0 * double(g.alloc_elems()) * 4.0 : bytes;
     std::printf("{\"variant\": \"%s\", \"median_ms\": %.4f, \"best_ms\": %.4f, \"tb_s\": %.3f, \"gcells_s\": %.1f}\n",
-                v.name.c_str(), med, best, cbytes / (med * 1e-3) / 1e12, double(W) * double(H) / (med * 1e-3) / 1e9);
+                v.name.c_str(), med, best, cbytes / (med * 1e-3) / 1e12,
+                double(W) * double(H) * v.steps / (med * 1e-3) / 1e9);
   }
   return 0;
 }

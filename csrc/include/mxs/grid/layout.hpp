@@ -119,9 +119,10 @@ struct TileGeom {
     const index_t a = align_bytes / elem_bytes;                // elements per alignment unit
     const index_t lead = ((hx + a - 1) / a) * a;               // core starts here
     g.x_origin = lead - hx;                                    // first ghost column
-    // Room for the last (possibly partial) core vector plus one more vector, so a
-    // 16-byte load that starts at any core column < width + a stays inside the row.
-    const index_t min_pitch = lead + ((w + a - 1) / a) * a + (hx > a ? hx : a);
+    // Room for the last (possibly partial) core vector, the right ghost columns
+    // rounded up to whole vectors, plus one more vector: a 16-byte load that starts
+    // at any column < width + roundup(halo_x) stays inside the row.
+    const index_t min_pitch = lead + ((w + a - 1) / a) * a + ((hx + a - 1) / a) * a + a;
     const index_t pa = pitch_align_bytes / elem_bytes;
     g.pitch = ((min_pitch + pa - 1) / pa) * pa;
     return g;

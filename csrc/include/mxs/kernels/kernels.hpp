@@ -54,6 +54,26 @@ template <typename T>
 void stencil5_rows(const T* in, T* out, const TileGeom& g, index_t row_begin, index_t row_end,
                    Stencil5Coeffs c, hipStream_t s, StencilVariant v = StencilVariant::Auto);
 
+// Full-tile update of a 1x1 periodic grid with the self-exchange fused into the
+// addressing (row -1 reads row H-1, column W reads column 0, ...): one launch per
+// iteration, no ghost traffic. Needs width % (16 / sizeof(T)) == 0.
+template <typename T>
+void stencil5_periodic(const T* in, T* out, const TileGeom& g, Stencil5Coeffs c, hipStream_t s);
+template <typename T>
+bool stencil5_periodic_supported(const TileGeom& g);
+
+// Temporal blocking: `steps` (S) Jacobi iterations in one launch over the core
+// rectangle [x0, x1) x [y0, y1), LDS-tiled (each workgroup stages its tile plus an
+// S-deep apron once, iterates S times in LDS, writes once: ~S x less HBM traffic
+// per iteration). The source must hold valid data S cells around the rectangle:
+// a ghost ring >= S deep exchanged for this super-step, or `wrap` (1x1 periodic
+// grid: reads wrap around the tile). Supported S: 1..8. Bitwise identical to S
+// single steps (same per-cell fma sequence).
+constexpr int kMaxTimeBlock = 8;
+template <typename T>
+void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0, index_t y1,
+                 Stencil5Coeffs c, bool wrap, hipStream_t s);
+
 // Update an arbitrary core rectangle [x0, x1) x [y0, y1) (scalar path; used for the
 // boundary columns of the overlapped schedule and for tiny tiles).
 template <typename T>

@@ -2,26 +2,32 @@
 // reference's exchange-compute loop (stencil2d/mpi-2d-stencil-subarray-cuda.cu:169-172,
 // whose Compute() was empty and whose loop ran once).
 //
-// Per iteration (cur -> nxt), with `overlap` on:
+// Time blocking (`time_block` = S, Jacobi5): every super-step exchanges an
+// S-deep halo (same bytes per iteration as S 1-deep exchanges, S x fewer
+// latency-bound messages) and then advances S iterations in one LDS-tiled launch
+// (kernels::stencil5_tb: ~S x less HBM traffic per iteration). S = 1 is the
+// classic one-exchange-per-iteration loop. Results are bitwise identical for any S.
+//
+// Per super-step (cur -> nxt), with `overlap` on:
 //
 //   main stream : record(fork) -> pack(cur) -> RCCL send/recv -> unpack(cur) -> wait(interior)
-//                 -> boundary rows 0 and H-1, boundary columns 0 and W-1
-//   side stream : wait(fork) -> interior rows [1, H-1) of nxt -> record(interior)
+//                 -> boundary rows [0, S) and [H-S, H), boundary columns [0, S) and [W-S, W)
+//   side stream : wait(fork) -> interior rows [S, H-S) of nxt -> record(interior)
 //
 // (RCCL must run on the capture-origin stream, so the exchange chain stays on
 // the main stream and the long interior sweep is the forked branch.)
 //
-// The interior launch covers full rows, so its columns 0 and W-1 read ghost
-// columns that the unpack may be writing concurrently; those two output columns
-// are recomputed by the boundary launch after the halo has landed, so the race
-// is benign by construction (it only ever produces values that are overwritten).
-// Without `overlap` (or for Local/1x1 grids) the iteration is exchange + one
-// full sweep on the main stream.
+// The interior launch covers full rows, so its first/last S columns read ghost
+// columns that the unpack may be writing concurrently; those output columns are
+// recomputed by the boundary launch after the halo has landed, so the race is
+// benign by construction (it only ever produces values that are overwritten).
+// Without `overlap` (or with nothing to hide) the super-step is exchange + one
+// full launch on the main stream. A 1x1 periodic grid fuses the self-exchange
+// into the kernel's wrap-around addressing (`fuse_periodic_self`).
 //
-// `use_graph`: two iterations (cur->nxt, nxt->cur) are captured once into a
-// hipGraph and replayed, so an iteration costs one graph launch of host work
-// (launch-bound inner loops, Guideline 9). If capture fails (e.g. an RCCL build
-// without graph support) the solver falls back to eager launches.
+// `use_graph`: the super-step is captured once per buffer orientation into a
+// hipGraph and replayed (launch-bound inner loops, Guideline 9). If capture fails
+// (e.g. an RCCL build without graph support) the solver falls back to eager launches.
 #pragma once
 
 #include <memory>
@@ -39,8 +45,15 @@ struct SolverConfig {
   HaloBackend backend = HaloBackend::Local;
   bool overlap = true;
   bool use_graph = true;
-  bool corners = true;        // exchange diagonal neighbours too (needed by Box)
+  bool corners = true;        // exchange diagonal neighbours too (needed by Box and time blocking)
   bool loopback_self = false;  // route self-neighbours through RCCL (1-GPU wire test)
+  // 1x1 periodic grid + Jacobi5: fuse the self-exchange into the kernel's
+  // wrap-around addressing (ghost cells untouched; exchange_only() still performs
+  // an explicit exchange for dumps).
+  bool fuse_periodic_self = true;
+  // Jacobi iterations per halo exchange / per launch (1..kernels::kMaxTimeBlock);
+  // the tile's ghost ring must be at least this deep.
+  int time_block = 1;
   StencilKind kind = StencilKind::Jacobi5;
   kernels::Stencil5Coeffs coeffs;
   kernels::BoxWeights box;
@@ -57,7 +70,7 @@ class StencilSolver {
   ~StencilSolver();
 
   void step();            // enqueue one iteration
-  void run(int iters);    // enqueue `iters` iterations (graph replay when enabled)
+  void run(int iters);    // enqueue `iters` iterations (super-steps of time_block, graph replay)
   void exchange_only();   // enqueue a halo exchange of the current tile (no update)
   void synchronize();     // wait for everything enqueued so far
 
@@ -68,24 +81,31 @@ class StencilSolver {
   bool graph_active() const { return graphs_[0].valid(); }
   const std::string& graph_status() const { return graph_status_; }
   const HaloPlan& plan() const { return ex_->plan(); }
+  bool fused_periodic() const { return fused_; }
+  bool overlapped() const { return cfg_.overlap; }
+  int time_block() const { return block_; }
   index_t cells_per_iteration() const { return tile_.width * tile_.height; }
 
  private:
-  void enqueue_step(T* cur, T* nxt);
-  void update(const T* in, T* out, index_t r0, index_t r1, hipStream_t s);
-  void update_cols(const T* in, T* out, index_t r0, index_t r1, hipStream_t s);
+  void enqueue_block(T* cur, T* nxt);   // block_ iterations
+  void enqueue_single(T* cur, T* nxt);  // 1 iteration (remainders)
+  // `steps` iterations over core rows [r0, r1) x cols [c0, c1).
+  void update(const T* in, T* out, int steps, index_t c0, index_t c1, index_t r0, index_t r1, hipStream_t s);
   bool try_capture();
 
   TileGeom tile_;
   SolverConfig cfg_;
+  int block_ = 1;
+  int radius_ = 1;
   T* cur_;
   T* nxt_;
   std::unique_ptr<HaloExchanger<T>> ex_;
   Stream main_, side_;
   Event fork_, interior_;
-  GraphExec graphs_[2];  // [0]: buf_a -> buf_b, [1]: buf_b -> buf_a (as captured)
+  GraphExec graphs_[2];  // one super-step per buffer orientation (as captured)
   int parity_ = 0;
   bool graph_tried_ = false;
+  bool fused_ = false;
   std::string graph_status_ = "not captured";
 };
 

@@ -92,6 +92,86 @@ void stencil5_rows(const T* in, T* out, const TileGeom& g, index_t row_begin, in
 }
 
 template <typename T>
+bool stencil5_periodic_supported(const TileGeom& g) {
+  constexpr int N = Vec16<T>::N;
+  return g.width % N == 0 && g.width >= N && g.height >= 1 && (g.pitch % N) == 0 &&
+         ((g.x_origin + g.halo_x) % N) == 0;
+}
+
+template <typename T>
+void stencil5_periodic(const T* in, T* out, const TileGeom& g, Stencil5Coeffs c, hipStream_t s) {
+  MXS_CHECK(stencil5_periodic_supported<T>(g), "stencil5_periodic: width must be a multiple of the vector width");
+  constexpr int N = Vec16<T>::N;
+  constexpr int WX = 4, NW = 4;
+  const T c0 = T(c.center), c1 = T(c.neighbor);
+  const index_t gx = (g.width + index_t(kWaveSize) * N * WX - 1) / (index_t(kWaveSize) * N * WX);
+  auto go = [&](auto rows_tag) {
+    constexpr int R = decltype(rows_tag)::value;
+    const index_t gy = (g.height + R - 1) / R;
+    stencil5_roll_kernel<T, R, R, true, WX, false, NW, true><<<dim3(unsigned(gx), unsigned(gy)), NW * kWaveSize, 0, s>>>(
+        in, out, g.pitch, g.core_offset(), g.width, 0, g.height, c0, c1, g.height);
+  };
+  if (g.width * int(sizeof(T)) >= 32768 * 4) go(std::integral_constant<int, 4>{});
+  else go(std::integral_constant<int, 3>{});
+  MXS_HIP_CHECK_LAUNCH();
+}
+
+namespace {
+// Tuned tile (bench/stencil_tune.hip, profiles/stencil_tuning/tune7-8): 128 fp32
+// columns (64 fp64: same bytes) x 32 rows per 256-thread workgroup, single LDS
+// buffer (23 KB at S = 4 -> 6 workgroups per CU).
+template <typename T, int S, bool WRAP>
+void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
+               hipStream_t s) {
+  constexpr int TW = sizeof(T) == 4 ? 128 : 64;
+  constexpr int TH = 32;
+  const size_t lds = tb1_lds_bytes<T, S, TW, TH>();
+  const dim3 grid(unsigned((x1 - x0 + TW - 1) / TW), unsigned((y1 - y0 + TH - 1) / TH));
+  stencil5_tb1_kernel<T, S, TW, TH, WRAP><<<grid, 256, lds, s>>>(in, out, g.pitch, g.core_offset(), g.width,
+                                                                 g.height, x0, x1, y0, y1, c0, c1);
+}
+
+template <typename T, bool WRAP>
+void dispatch_tb(int steps, const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
+                 T c0, T c1, hipStream_t s) {
+  switch (steps) {
+    case 1: launch_tb<T, 1, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
+    case 2: launch_tb<T, 2, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
+    case 3: launch_tb<T, 3, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
+    case 4: launch_tb<T, 4, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
+    case 5: launch_tb<T, 5, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
+    case 6: launch_tb<T, 6, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
+    case 7: launch_tb<T, 7, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
+    case 8: launch_tb<T, 8, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
+    default: MXS_CHECK(false, "stencil5_tb: steps must be in [1, " << kMaxTimeBlock << "], got " << steps);
+  }
+}
+}  // namespace
+
+template <typename T>
+void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0, index_t y1,
+                 Stencil5Coeffs c, bool wrap, hipStream_t s) {
+  if (x1 <= x0 || y1 <= y0) return;
+  constexpr int N = Vec16<T>::N;
+  MXS_CHECK(x0 >= 0 && y0 >= 0 && x1 <= g.width && y1 <= g.height, "stencil5_tb: rect out of the core");
+  MXS_CHECK(x0 % N == 0, "stencil5_tb: x0 must be a multiple of the vector width");
+  MXS_CHECK((g.pitch % N) == 0 && ((g.x_origin + g.halo_x) % N) == 0, "stencil5_tb needs a TileGeom::aligned layout");
+  const int sa = ((steps + N - 1) / N) * N;
+  if (wrap) {
+    MXS_CHECK(g.width % N == 0, "stencil5_tb wrap: width must be a multiple of the vector width");
+  } else {
+    MXS_CHECK(g.halo_x >= steps && g.halo_y >= steps,
+              "stencil5_tb: ghost ring (" << g.halo_x << ") shallower than the time block (" << steps << ")");
+    MXS_CHECK(g.x_origin + g.halo_x >= sa && g.pitch >= g.x_origin + g.halo_x + ((g.width + N - 1) / N) * N + sa,
+              "stencil5_tb: row padding too small for the x apron");
+  }
+  const T c0 = T(c.center), c1 = T(c.neighbor);
+  if (wrap) dispatch_tb<T, true>(steps, in, out, g, x0, x1, y0, y1, c0, c1, s);
+  else dispatch_tb<T, false>(steps, in, out, g, x0, x1, y0, y1, c0, c1, s);
+  MXS_HIP_CHECK_LAUNCH();
+}
+
+template <typename T>
 void stencil5_rect(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
                    Stencil5Coeffs c, hipStream_t s) {
   if (x1 <= x0 || y1 <= y0) return;
@@ -123,6 +203,10 @@ void stencil_box(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1,
                                  StencilVariant);                                                              \
   template void stencil5_rect<T>(const T*, T*, const TileGeom&, index_t, index_t, index_t, index_t,             \
                                  Stencil5Coeffs, hipStream_t);                                                 \
+  template void stencil5_periodic<T>(const T*, T*, const TileGeom&, Stencil5Coeffs, hipStream_t);              \
+  template void stencil5_tb<T>(const T*, T*, const TileGeom&, int, index_t, index_t, index_t, index_t,          \
+                               Stencil5Coeffs, bool, hipStream_t);                                             \
+  template bool stencil5_periodic_supported<T>(const TileGeom&);                                               \
   template void stencil_box<T>(const T*, T*, const TileGeom&, index_t, index_t, index_t, index_t,               \
                                const BoxWeights&, hipStream_t);
 MXS_INST_STENCIL(float)

@@ -36,10 +36,15 @@ constexpr int kBlock = kWavesPerBlock * kWaveSize;
 // ------------------------------------------------------------- RegisterRoll
 // WX waves side by side along x (4/WX stacked along y) per 256-thread workgroup;
 // NT = non-temporal (streaming) stores, NTL = non-temporal loads.
-template <typename T, int ROWS, int CH, bool NT, int WX = 1, bool NTL = false, int NW = kWavesPerBlock>
+// WRAP: periodic wrap-around addressing inside the tile (rows -1 / H map to H-1 / 0,
+// columns -1 / W to W-1 / 0) — the fused self-exchange of a 1x1 periodic grid, so
+// no ghost cell is read or written. Requires W % VEC == 0.
+template <typename T, int ROWS, int CH, bool NT, int WX = 1, bool NTL = false, int NW = kWavesPerBlock,
+          bool WRAP = false>
 __global__ __launch_bounds__(NW * kWaveSize) void stencil5_roll_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                index_t pitch, index_t core_off, index_t W,
-                                                               index_t row_begin, index_t row_end, T c0, T c1) {
+                                                               index_t row_begin, index_t row_end, T c0, T c1,
+                                                               index_t H = 0) {
   static_assert(ROWS % CH == 0, "ROWS must be a multiple of CH");
   constexpr int N = Vec16<T>::N;
   constexpr int SEG = kWaveSize * N;
@@ -58,29 +63,44 @@ __global__ __launch_bounds__(NW * kWaveSize) void stencil5_roll_kernel(const T* 
 
   const bool load_ok = x < W + N;  // covers the lane right after the last core vector
   const bool active = x < W;
-  const bool right_edge = (lane == kWaveSize - 1) && (seg_base + SEG <= W);
+  // Lane whose x+1 neighbour of its last element is not in the next lane's vector:
+  // lane 63 (next segment), or under WRAP the lane holding column W-1.
+  const bool right_lane = (lane == kWaveSize - 1) || (WRAP && x + N == W);
+  const bool right_load = WRAP ? right_lane && active : (lane == kWaveSize - 1) && (seg_base + SEG <= W);
+  // Column offsets (relative to x) of the two edge values.
+  const index_t left_col = (WRAP && x == 0) ? W - 1 : -1;
+  const index_t right_col = (WRAP && x + N == W) ? -x : N;
   const T* __restrict__ pin = in + core_off + x;
   T* __restrict__ pout = out + core_off + x;
 
+  auto row = [&](index_t y) -> index_t {
+    if constexpr (WRAP) return y < 0 ? y + H : (y >= H ? y - H : y);
+    else return y;
+  };
   auto ldv = [&](index_t y) -> V {
     V v = V(T(0));
+    const index_t r = row(y);
     if (load_ok) {
-      if constexpr (NTL) v = __builtin_nontemporal_load(reinterpret_cast<const V*>(pin + y * pitch));
-      else v = *reinterpret_cast<const V*>(pin + y * pitch);
+      if constexpr (NTL) v = __builtin_nontemporal_load(reinterpret_cast<const V*>(pin + r * pitch));
+      else v = *reinterpret_cast<const V*>(pin + r * pitch);
     }
     return v;
   };
-  auto lde = [&](index_t y) -> T {
-    T e = T(0);
-    if (lane == 0) e = pin[y * pitch - 1];
-    else if (right_edge) e = pin[y * pitch + N];
+  struct Edge {
+    T l, r;
+  };
+  auto lde = [&](index_t y) -> Edge {
+    Edge e{T(0), T(0)};
+    const index_t r = row(y);
+    if (lane == 0) e.l = pin[r * pitch + left_col];
+    if (right_load) e.r = pin[r * pitch + right_col];
     return e;
   };
-  auto emit = [&](index_t y, const V& up, const V& mid, const V& dn, T emid) {
+  auto emit = [&](index_t y, const V& up, const V& mid, const V& dn, Edge emid) {
     T left = __shfl_up(mid[N - 1], 1);
     T right = __shfl_down(mid[0], 1);
-    if (lane == 0) left = emid;
-    if (lane == kWaveSize - 1) right = emid;
+    if (lane == 0) left = emid.l;
+    if (right_lane) right = emid.r;
     V o;
     o[0] = jac<T>(mid[0], up[0], dn[0], left, mid[1 % N], c0, c1);
     if constexpr (N == 2) {
@@ -105,14 +125,14 @@ __global__ __launch_bounds__(NW * kWaveSize) void stencil5_roll_kernel(const T* 
 
   V up = ldv(y0 - 1);
   V mid = ldv(y0);
-  T emid = lde(y0);
+  Edge emid = lde(y0);
 
   if (y1 - y0 == ROWS) {
     // Full strip: chunks of CH rows, loads of a chunk issued before its math.
 #pragma unroll 1
     for (int c = 0; c < ROWS; c += CH) {
       V dn[CH];
-      T edn[CH];
+      Edge edn[CH];
 #pragma unroll
       for (int k = 0; k < CH; ++k) {
         dn[k] = ldv(y0 + c + k + 1);
@@ -130,7 +150,7 @@ __global__ __launch_bounds__(NW * kWaveSize) void stencil5_roll_kernel(const T* 
 #pragma unroll 1
     for (index_t y = y0; y < y1; ++y) {
       const V dn = ldv(y + 1);
-      const T edn = lde(y + 1);
+      const Edge edn = lde(y + 1);
       emit(y, up, mid, dn, emid);
       up = mid;
       mid = dn;
@@ -245,6 +265,243 @@ __global__ __launch_bounds__(kBlock) void stencil_box_kernel(const T* __restrict
 }
 
 // Tuned defaults (see docs/PERF.md for the sweep behind them).
+
+}  // namespace detail
+}  // namespace kernels
+}  // namespace mxs
+
+namespace mxs {
+namespace kernels {
+namespace detail {
+
+// --------------------------------------------------------- temporal blocking
+// S Jacobi iterations per launch, LDS-tiled (the "LDS tiling" of the stencil):
+// a workgroup stages its TW x TH output tile plus an S-deep apron once from HBM
+// into LDS (16-byte vector loads, all issued up front), runs S 5-point steps
+// LDS -> LDS (ping-pong buffers; the valid region shrinks by one cell per step,
+// so no intermediate halo is ever exchanged), then writes the TW x TH result
+// once (non-temporal 16-byte stores). HBM traffic per iteration drops by ~S x
+// (plus the apron re-read, (TW+2SA)(TH+2S)/(TW*TH)). The tile's source region
+// needs a ghost ring of depth >= S (exchanged S-deep every S iterations), or
+// WRAP for the 1x1 periodic grid (global reads wrap around the tile).
+//
+// The x apron SA = S rounded up to the vector width keeps every staged row and
+// every LDS access 16-byte aligned; LDS rows are padded by one vector on each
+// side (the x-1 / x+N reads of the edge chunks land in the padding: those cells
+// are outside the valid region and never reach the output).
+template <typename T, int S, int TW, int TH, bool WRAP>
+__global__ __launch_bounds__(256) void stencil5_tb_kernel(const T* __restrict__ in, T* __restrict__ out, index_t pitch,
+                                                         index_t core_off, index_t W, index_t H, index_t x_begin,
+                                                         index_t x_end, index_t y_begin, index_t y_end, T c0, T c1) {
+  constexpr int N = Vec16<T>::N;
+  constexpr int SA = ((S + N - 1) / N) * N;  // x apron, vector aligned
+  constexpr int LW = TW + 2 * SA;            // staged columns
+  constexpr int LP = LW + 2 * N;             // LDS row pitch (elements)
+  constexpr int LH = TH + 2 * S;             // staged rows
+  constexpr int NV = LW / N;                 // vectors per staged row
+  static_assert(TW % N == 0, "tile width must be a multiple of the vector width");
+  using V = typename Vec16<T>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_tb[];
+  T* buf0 = reinterpret_cast<T*>(smem_tb);
+  T* buf1 = buf0 + LH * LP;
+
+  const index_t tx0 = x_begin + index_t(blockIdx.x) * TW;
+  const index_t ty0 = y_begin + index_t(blockIdx.y) * TH;
+  const int tid = threadIdx.x;
+
+  // ---- stage (rows ty0-S .. ty0+TH+S-1, cols tx0-SA .. tx0+TW+SA-1)
+  for (int i = tid; i < LH * NV; i += 256) {
+    const int r = i / NV, v = i - r * NV;
+    index_t gy = ty0 - S + r;
+    index_t gx = tx0 - SA + index_t(v) * N;
+    V val = V(T(0));
+    bool ok;
+    if constexpr (WRAP) {
+      gy = ((gy % H) + H) % H;
+      gx = ((gx % W) + W) % W;  // W % N == 0: a wrapped vector never straddles the seam
+      ok = true;
+    } else {
+      ok = gy < H + S && gx < W + SA;  // inside the tile's ghost ring + padding
+    }
+    if (ok) val = *reinterpret_cast<const V*>(in + core_off + gy * pitch + gx);
+    *reinterpret_cast<V*>(buf0 + r * LP + N + v * N) = val;
+  }
+  __syncthreads();
+
+  // ---- S steps in LDS
+  T* src = buf0;
+  T* dst = buf1;
+#pragma unroll 1
+  for (int s = 0; s < S; ++s) {
+    for (int i = tid; i < (LH - 2) * NV; i += 256) {
+      const int r = 1 + i / NV, v = i - (r - 1) * NV;
+      const int base = r * LP + N + v * N;
+      const V mid = *reinterpret_cast<const V*>(src + base);
+      const V up = *reinterpret_cast<const V*>(src + base - LP);
+      const V dn = *reinterpret_cast<const V*>(src + base + LP);
+      const T left = src[base - 1];
+      const T right = src[base + N];
+      V o;
+      o[0] = jac<T>(mid[0], up[0], dn[0], left, mid[1 % N], c0, c1);
+      if constexpr (N == 2) {
+        o[1] = jac<T>(mid[1], up[1], dn[1], mid[0], right, c0, c1);
+      } else {
+#pragma unroll
+        for (int k = 1; k < N - 1; ++k) o[k] = jac<T>(mid[k], up[k], dn[k], mid[k - 1], mid[k + 1], c0, c1);
+        o[N - 1] = jac<T>(mid[N - 1], up[N - 1], dn[N - 1], mid[N - 2], right, c0, c1);
+      }
+      *reinterpret_cast<V*>(dst + base) = o;
+    }
+    __syncthreads();
+    T* t = src;
+    src = dst;
+    dst = t;
+  }
+
+  // ---- write the TW x TH result
+  constexpr int OV = TW / N;
+  for (int i = tid; i < TH * OV; i += 256) {
+    const int r = i / OV, v = i - r * OV;
+    const index_t gy = ty0 + r, gx = tx0 + index_t(v) * N;
+    if (gy >= y_end || gx >= x_end) continue;
+    const V o = *reinterpret_cast<const V*>(src + (r + S) * LP + N + SA + v * N);
+    T* p = out + core_off + gy * pitch + gx;
+    if (gx + N <= x_end) {
+      __builtin_nontemporal_store(o, reinterpret_cast<V*>(p));
+    } else {
+#pragma unroll
+      for (int k = 0; k < N; ++k)
+        if (gx + k < x_end) p[k] = o[k];
+    }
+  }
+}
+
+template <typename T, int S, int TW, int TH>
+constexpr size_t tb_lds_bytes() {
+  constexpr int N = Vec16<T>::N;
+  constexpr int SA = ((S + N - 1) / N) * N;
+  return size_t(2) * (TH + 2 * S) * (TW + 2 * SA + 2 * N) * sizeof(T);
+}
+
+}  // namespace detail
+}  // namespace kernels
+}  // namespace mxs
+
+namespace mxs {
+namespace kernels {
+namespace detail {
+
+// Single-LDS-buffer variant of stencil5_tb_kernel: each step reads its cells into
+// registers (a compile-time number of vectors per thread, statically indexed so
+// they stay in VGPRs), barrier, writes them back in place, barrier. Half the LDS
+// of the ping-pong form, so more workgroups per CU keep HBM busy while others
+// compute.
+template <typename T, int S, int TW, int TH, bool WRAP>
+__global__ __launch_bounds__(256) void stencil5_tb1_kernel(const T* __restrict__ in, T* __restrict__ out, index_t pitch,
+                                                          index_t core_off, index_t W, index_t H, index_t x_begin,
+                                                          index_t x_end, index_t y_begin, index_t y_end, T c0, T c1) {
+  constexpr int N = Vec16<T>::N;
+  constexpr int SA = ((S + N - 1) / N) * N;
+  constexpr int LW = TW + 2 * SA;
+  constexpr int LP = LW + 2 * N;
+  constexpr int LH = TH + 2 * S;
+  constexpr int NV = LW / N;
+  constexpr int CELLS = (LH - 2) * NV;            // vectors updated per step
+  constexpr int PER = (CELLS + 255) / 256;        // per thread
+  static_assert(TW % N == 0, "tile width must be a multiple of the vector width");
+  using V = typename Vec16<T>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_tb1[];
+  T* buf = reinterpret_cast<T*>(smem_tb1);
+
+  const index_t tx0 = x_begin + index_t(blockIdx.x) * TW;
+  const index_t ty0 = y_begin + index_t(blockIdx.y) * TH;
+  const int tid = threadIdx.x;
+  // Staged coordinates stay within one period of the tile unless the tile is
+  // smaller than the workgroup's footprint: then fall back to a full modulo.
+  const bool one_period = W >= TW + 2 * SA && H >= TH + 2 * S;
+
+  for (int i = tid; i < LH * NV; i += 256) {
+    const int r = i / NV, v = i - r * NV;
+    index_t gy = ty0 - S + r;
+    index_t gx = tx0 - SA + index_t(v) * N;
+    V val = V(T(0));
+    bool ok;
+    if constexpr (WRAP) {
+      if (one_period) {
+        gy = gy < 0 ? gy + H : (gy >= H ? gy - H : gy);
+        gx = gx < 0 ? gx + W : (gx >= W ? gx - W : gx);
+      } else {
+        gy = ((gy % H) + H) % H;
+        gx = ((gx % W) + W) % W;
+      }
+      ok = true;
+    } else {
+      ok = gy < H + S && gx < W + SA;
+    }
+    if (ok) val = *reinterpret_cast<const V*>(in + core_off + gy * pitch + gx);
+    *reinterpret_cast<V*>(buf + r * LP + N + v * N) = val;
+  }
+  __syncthreads();
+
+#pragma unroll 1
+  for (int s = 0; s < S; ++s) {
+    V res[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + k * 256;
+      if (i < CELLS) {
+        const int r = 1 + i / NV, v = i - (r - 1) * NV;
+        const int base = r * LP + N + v * N;
+        const V mid = *reinterpret_cast<const V*>(buf + base);
+        const V up = *reinterpret_cast<const V*>(buf + base - LP);
+        const V dn = *reinterpret_cast<const V*>(buf + base + LP);
+        const T left = buf[base - 1];
+        const T right = buf[base + N];
+        V o;
+        o[0] = jac<T>(mid[0], up[0], dn[0], left, mid[1 % N], c0, c1);
+        if constexpr (N == 2) {
+          o[1] = jac<T>(mid[1], up[1], dn[1], mid[0], right, c0, c1);
+        } else {
+#pragma unroll
+          for (int q = 1; q < N - 1; ++q) o[q] = jac<T>(mid[q], up[q], dn[q], mid[q - 1], mid[q + 1], c0, c1);
+          o[N - 1] = jac<T>(mid[N - 1], up[N - 1], dn[N - 1], mid[N - 2], right, c0, c1);
+        }
+        res[k] = o;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + k * 256;
+      if (i < CELLS) {
+        const int r = 1 + i / NV, v = i - (r - 1) * NV;
+        *reinterpret_cast<V*>(buf + r * LP + N + v * N) = res[k];
+      }
+    }
+    __syncthreads();
+  }
+
+  constexpr int OV = TW / N;
+  for (int i = tid; i < TH * OV; i += 256) {
+    const int r = i / OV, v = i - r * OV;
+    const index_t gy = ty0 + r, gx = tx0 + index_t(v) * N;
+    if (gy >= y_end || gx >= x_end) continue;
+    const V o = *reinterpret_cast<const V*>(buf + (r + S) * LP + N + SA + v * N);
+    T* p = out + core_off + gy * pitch + gx;
+    if (gx + N <= x_end) {
+      __builtin_nontemporal_store(o, reinterpret_cast<V*>(p));
+    } else {
+#pragma unroll
+      for (int k = 0; k < N; ++k)
+        if (gx + k < x_end) p[k] = o[k];
+    }
+  }
+}
+
+template <typename T, int S, int TW, int TH>
+constexpr size_t tb1_lds_bytes() {
+  return tb_lds_bytes<T, S, TW, TH>() / 2;
+}
 
 }  // namespace detail
 }  // namespace kernels

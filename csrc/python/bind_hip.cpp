@@ -144,6 +144,19 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2, py::arg("dtype") = "f32", py::arg("stream") = 0,
       py::arg("variant") = "auto");
   m.def(
+      "stencil5_tb",
+      [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0,
+         index_t y1, double c0, double c1, bool wrap, const std::string& dt, std::uintptr_t s) {
+        kernels::Stencil5Coeffs c{c0, c1};
+        if (parse_dtype(dt) == DType::F32)
+          kernels::stencil5_tb<float>(ptr<float>(in), ptr<float>(out), g, steps, x0, x1, y0, y1, c, wrap, strm(s));
+        else
+          kernels::stencil5_tb<double>(ptr<double>(in), ptr<double>(out), g, steps, x0, x1, y0, y1, c, wrap, strm(s));
+      },
+      py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("steps"), py::arg("x0"), py::arg("x1"), py::arg("y0"),
+      py::arg("y1"), py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2, py::arg("wrap") = false,
+      py::arg("dtype") = "f32", py::arg("stream") = 0);
+  m.def(
       "stencil5_rect",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
          double c0, double c1, const std::string& dt, std::uintptr_t s) {
@@ -257,12 +270,14 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def(py::init([](const CartTopology& topo, int rank, const TileGeom& tile, std::uintptr_t a, std::uintptr_t b,
                        const RcclComm* comm, const std::string& dt, HaloBackend backend, bool overlap,
                        bool use_graph, bool loopback_self, StencilKind kind, double c0, double c1, int box_radius,
-                       const std::vector<float>& box_w, const std::string& variant) {
+                       const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block) {
              SolverConfig cfg;
              cfg.backend = backend;
              cfg.overlap = overlap;
              cfg.use_graph = use_graph;
              cfg.loopback_self = loopback_self;
+             cfg.fuse_periodic_self = fuse_periodic;
+             cfg.time_block = time_block;
              cfg.kind = kind;
              cfg.coeffs = {c0, c1};
              cfg.variant = parse_variant(variant);
@@ -281,6 +296,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("overlap") = true, py::arg("use_graph") = true, py::arg("loopback_self") = false,
            py::arg("kind") = StencilKind::Jacobi5, py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2,
            py::arg("box_radius") = 1, py::arg("box_weights") = std::vector<float>{}, py::arg("variant") = "auto",
+           py::arg("fuse_periodic") = true, py::arg("time_block") = 1,
            py::keep_alive<1, 7>())
       .def("step", [](SolverHandle& h) { h.visit([](auto& s) { s.step(); }); })
       .def(
@@ -298,7 +314,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
              return h.visit([](auto& s) { return reinterpret_cast<std::uintptr_t>(s.main_stream()); });
            })
       .def("graph_active", [](SolverHandle& h) { return h.visit([](auto& s) { return s.graph_active(); }); })
-      .def("graph_status", [](SolverHandle& h) { return h.visit([](auto& s) { return s.graph_status(); }); });
+      .def("graph_status", [](SolverHandle& h) { return h.visit([](auto& s) { return s.graph_status(); }); })
+      .def("fused_periodic", [](SolverHandle& h) { return h.visit([](auto& s) { return s.fused_periodic(); }); })
+      .def("overlapped", [](SolverHandle& h) { return h.visit([](auto& s) { return s.overlapped(); }); })
+      .def("time_block", [](SolverHandle& h) { return h.visit([](auto& s) { return s.time_block(); }); });
 
   // ------------------------------------------------------------------ ping-pong
   py::enum_<PingPongMode>(m, "PingPongMode")

@@ -1,5 +1,6 @@
 #include "mxs/runtime/stencil_solver.hpp"
 
+#include <algorithm>
 #include <utility>
 
 namespace mxs {
@@ -10,13 +11,21 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
     : tile_(tile), cfg_(cfg), cur_(buf_a), nxt_(buf_b), main_(true, -1), side_(true, 0) {
   // The main stream gets the higher priority (lower number): its short pack /
   // unpack / boundary launches should not queue behind the long interior sweep.
-  const int radius = cfg_.kind == StencilKind::Box ? cfg_.box.radius : 1;
-  MXS_CHECK(tile_.halo_x >= radius && tile_.halo_y >= radius, "ghost ring narrower than the stencil radius");
-  const bool corners = cfg_.corners || cfg_.kind == StencilKind::Box;
+  block_ = cfg_.kind == StencilKind::Jacobi5 ? std::max(1, cfg_.time_block) : 1;
+  MXS_CHECK(block_ <= kernels::kMaxTimeBlock, "time_block must be <= " << kernels::kMaxTimeBlock);
+  radius_ = cfg_.kind == StencilKind::Box ? cfg_.box.radius : 1;
+  const int depth = std::max(radius_, block_);  // cells a super-step reads beyond the core
+  MXS_CHECK(tile_.halo_x >= depth && tile_.halo_y >= depth,
+            "ghost ring (" << tile_.halo_x << ") shallower than the stencil radius x time block (" << depth << ")");
+  const bool corners = cfg_.corners || cfg_.kind == StencilKind::Box || block_ > 1;
   const HaloPlan plan = make_halo_plan(topo, rank, tile_, corners, cfg_.loopback_self);
   ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm);
   // Overlap only pays when there is a wire transfer to hide and an interior.
-  if (plan.sends.empty() || tile_.height <= 2 * radius || tile_.width <= 2 * radius) cfg_.overlap = false;
+  if (plan.sends.empty() || tile_.height <= 2 * depth || tile_.width <= 2 * depth) cfg_.overlap = false;
+  const bool all_self = plan.sends.empty() && int(plan.self_copies.size()) == (corners ? kNumDirs : 4);
+  constexpr int N = 16 / int(sizeof(T));
+  fused_ = cfg_.fuse_periodic_self && all_self && cfg_.kind == StencilKind::Jacobi5 && tile_.width % N == 0 &&
+           kernels::stencil5_periodic_supported<T>(tile_);
 }
 
 template <typename T>
@@ -26,26 +35,29 @@ StencilSolver<T>::~StencilSolver() {
 }
 
 template <typename T>
-void StencilSolver<T>::update(const T* in, T* out, index_t r0, index_t r1, hipStream_t s) {
-  if (r1 <= r0) return;
-  if (cfg_.kind == StencilKind::Jacobi5)
+void StencilSolver<T>::update(const T* in, T* out, int steps, index_t c0, index_t c1, index_t r0, index_t r1,
+                              hipStream_t s) {
+  if (r1 <= r0 || c1 <= c0) return;
+  if (cfg_.kind == StencilKind::Box) {
+    kernels::stencil_box<T>(in, out, tile_, c0, c1, r0, r1, cfg_.box, s);
+  } else if (steps > 1) {
+    kernels::stencil5_tb<T>(in, out, tile_, steps, c0, c1, r0, r1, cfg_.coeffs, false, s);
+  } else if (c0 == 0 && c1 == tile_.width) {
     kernels::stencil5_rows<T>(in, out, tile_, r0, r1, cfg_.coeffs, s, cfg_.variant);
-  else
-    kernels::stencil_box<T>(in, out, tile_, 0, tile_.width, r0, r1, cfg_.box, s);
+  } else {
+    kernels::stencil5_rect<T>(in, out, tile_, c0, c1, r0, r1, cfg_.coeffs, s);
+  }
 }
 
 template <typename T>
-void StencilSolver<T>::update_cols(const T* in, T* out, index_t r0, index_t r1, hipStream_t s) {
-  if (r1 <= r0) return;
-  const index_t w = tile_.width;
-  const index_t r = cfg_.kind == StencilKind::Box ? cfg_.box.radius : 1;
-  if (cfg_.kind == StencilKind::Jacobi5) {
-    kernels::stencil5_rect<T>(in, out, tile_, 0, r, r0, r1, cfg_.coeffs, s);
-    kernels::stencil5_rect<T>(in, out, tile_, w - r, w, r0, r1, cfg_.coeffs, s);
-  } else {
-    kernels::stencil_box<T>(in, out, tile_, 0, r, r0, r1, cfg_.box, s);
-    kernels::stencil_box<T>(in, out, tile_, w - r, w, r0, r1, cfg_.box, s);
+void StencilSolver<T>::enqueue_single(T* cur, T* nxt) {
+  hipStream_t m = main_.get();
+  if (fused_) {
+    kernels::stencil5_periodic<T>(cur, nxt, tile_, cfg_.coeffs, m);
+    return;
   }
+  ex_->exchange(cur, m);
+  update(cur, nxt, 1, 0, tile_.width, 0, tile_.height, m);
 }
 
 // Stream roles: the MAIN stream (the capture origin, high priority) carries the
@@ -53,24 +65,36 @@ void StencilSolver<T>::update_cols(const T* in, T* out, index_t r0, index_t r1, 
 // sweep forks onto the SIDE stream. RCCL calls must sit on the capture-origin
 // stream: captured from a forked stream, RCCL (ROCm 7.x) crashes at capture.
 template <typename T>
-void StencilSolver<T>::enqueue_step(T* cur, T* nxt) {
-  const index_t h = tile_.height;
+void StencilSolver<T>::enqueue_block(T* cur, T* nxt) {
+  const index_t h = tile_.height, w = tile_.width;
+  const int S = block_;
   hipStream_t m = main_.get(), side = side_.get();
-  if (!cfg_.overlap) {
-    ex_->exchange(cur, m);
-    update(cur, nxt, 0, h, m);
+  if (fused_) {
+    if (S == 1) kernels::stencil5_periodic<T>(cur, nxt, tile_, cfg_.coeffs, m);
+    else kernels::stencil5_tb<T>(cur, nxt, tile_, S, 0, w, 0, h, cfg_.coeffs, true, m);
     return;
   }
-  const index_t r = cfg_.kind == StencilKind::Box ? cfg_.box.radius : 1;
+  if (!cfg_.overlap) {
+    ex_->exchange(cur, m);
+    update(cur, nxt, S, 0, w, 0, h, m);
+    return;
+  }
+  const index_t d = std::max(radius_, S);  // dependency depth of the super-step
   fork_.record(m);
   fork_.wait_on(side);
-  update(cur, nxt, r, h - r, side);  // interior (its edge columns are redone below)
+  update(cur, nxt, S, 0, w, d, h - d, side);  // interior (its edge columns are redone below)
   interior_.record(side);
   ex_->exchange(cur, m);
   interior_.wait_on(m);
-  update(cur, nxt, 0, r, m);
-  update(cur, nxt, h - r, h, m);
-  update_cols(cur, nxt, r, h - r, m);
+  update(cur, nxt, S, 0, w, 0, d, m);
+  update(cur, nxt, S, 0, w, h - d, h, m);
+  // Column strips; the temporally blocked kernel needs a vector-aligned start, so
+  // the right strip may start a few (interior) columns early: recomputing those
+  // reproduces the same values.
+  constexpr index_t N = 16 / index_t(sizeof(T));
+  const index_t right0 = S > 1 ? ((w - d) / N) * N : w - d;
+  update(cur, nxt, S, 0, d, d, h - d, m);
+  update(cur, nxt, S, right0, w, d, h - d, m);
 }
 
 template <typename T>
@@ -88,7 +112,7 @@ bool StencilSolver<T>::try_capture() {
     }
     bool ok = true;
     try {
-      enqueue_step(a, b);
+      enqueue_block(a, b);
     } catch (const std::exception& e) {
       graph_status_ = std::string("capture failed: ") + e.what();
       ok = false;
@@ -113,20 +137,28 @@ bool StencilSolver<T>::try_capture() {
 }
 
 template <typename T>
-void StencilSolver<T>::step() {
-  if (cfg_.use_graph && !graph_tried_) try_capture();
-  if (graphs_[0].valid()) {
-    graphs_[parity_].launch(main_.get());
-    parity_ ^= 1;
-  } else {
-    enqueue_step(cur_, nxt_);
+void StencilSolver<T>::run(int iters) {
+  const int supers = iters / block_, rem = iters % block_;
+  for (int i = 0; i < supers; ++i) {
+    if (cfg_.use_graph && !graph_tried_) try_capture();
+    if (graphs_[0].valid()) {
+      graphs_[parity_].launch(main_.get());
+      parity_ ^= 1;
+    } else {
+      enqueue_block(cur_, nxt_);
+    }
+    std::swap(cur_, nxt_);
   }
-  std::swap(cur_, nxt_);
+  for (int i = 0; i < rem; ++i) {
+    enqueue_single(cur_, nxt_);
+    std::swap(cur_, nxt_);
+    parity_ ^= 1;  // keep the graph orientation in sync with the buffers
+  }
 }
 
 template <typename T>
-void StencilSolver<T>::run(int iters) {
-  for (int i = 0; i < iters; ++i) step();
+void StencilSolver<T>::step() {
+  run(1);
 }
 
 template <typename T>

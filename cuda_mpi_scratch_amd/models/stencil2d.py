@@ -54,6 +54,10 @@ class StencilConfig:
     graph: bool = True
     loopback: bool = False           # single GPU: send self-neighbour halos through RCCL
     variant: str = "auto"            # stencil kernel variant: auto | roll | lds
+    fuse_periodic: bool = True       # 1x1 periodic: fuse the self-exchange into the kernel addressing
+    # Jacobi iterations per halo exchange and per (LDS temporally blocked) launch on
+    # GPU; the ghost ring is made this deep. 1 = one exchange per iteration.
+    time_block: int = 4
     seed: int = 1234
     init: str = "random"             # random | rank
 
@@ -77,6 +81,11 @@ class Stencil2D:
         d = self.decomp
         self.dtype = _DTYPES[cfg.dtype]
         h = cfg.halo
+        # Temporal blocking only for the GPU Jacobi solver and not for the reference's
+        # exchange-only run (its dumps show a stencil_width/2 ghost ring).
+        self.time_block = (max(1, cfg.time_block) if (dev.type == "cuda" and cfg.kind == "jacobi5"
+                                                      and cfg.init != "rank") else 1)
+        h = max(h, self.time_block)
         C = core()
         if dev.type == "cuda":
             self.geom = C.TileGeom.aligned(d.width, d.height, h, h, self.dtype.itemsize)
@@ -107,7 +116,8 @@ class Stencil2D:
             radius = (int(round(math.sqrt(len(weights)))) - 1) // 2 if weights else 1
             self.solver = H.StencilSolver(d.topo, d.rank, self.geom, self.a.data_ptr(), self.b.data_ptr(), self.comm,
                                           cfg.dtype, be, cfg.overlap, cfg.graph, cfg.loopback, kind, cfg.c_center,
-                                          cfg.c_neighbor, radius, weights, cfg.variant)
+                                          cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
+                                          self.time_block)
         else:
             self.plan = make_plan(d, self.geom, corners=True)
             self.halo = TorchHalo(self.plan, self.ctx)
@@ -198,6 +208,16 @@ class Stencil2D:
 
     def graph_status(self) -> str:
         return self.solver.graph_status() if self.solver is not None else "python loop"
+
+    def halo_mode(self) -> str:
+        """How the halo is refreshed each iteration."""
+        if self.solver is None:
+            return "torch-p2p"
+        tb = self.solver.time_block()
+        blk = f", time-blocked x{tb} (one {tb}-deep exchange + one LDS launch per {tb} iterations)" if tb > 1 else ""
+        if self.solver.fused_periodic():
+            return "fused-periodic (1x1 self-exchange in the kernel addressing)" + blk
+        return f"{self.backend}" + (" + overlap" if self.solver.overlapped() else "") + blk
 
     # ----------------------------------------------------------------- dump
     def dump_text(self, stage_arrays: list[tuple[str, torch.Tensor]], device_id: int | None = None,

@@ -54,3 +54,76 @@ def test_reference_compat_run_single_rank(gpu):
     assert before.shape == (20, 20)
     assert (before[2:18, 2:18] == 0).all() and before[0, 0] == -1
     assert (after == 0).all()
+
+
+@pytest.mark.parametrize("w,fuse,expect_fused", [(300, True, True), (300, False, False), (301, True, False)])
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_fused_periodic_matches_explicit_exchange(gpu, w, fuse, expect_fused, dtype):
+    h, iters = 45, 5
+    cfg = StencilConfig(global_width=w, global_height=h, dims="1x1", dtype=dtype, seed=4, fuse_periodic=fuse)
+    st = Stencil2D(cfg)
+    assert st.solver.fused_periodic() == expect_fused
+    st.run(iters)
+    st.synchronize()
+    t = torch.float32 if dtype == "f32" else torch.float64
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, 4, dtype=t), iters)
+    tol = 1e-5 if dtype == "f32" else 1e-12
+    assert (st.core_view().cpu() - ref).abs().max().item() < tol
+
+
+def _multi_step_reference(full, steps, c0=0.2, c1=0.2):
+    """S Jacobi steps on a (core + ghost ring) array; edges stay frozen, so after S
+    steps everything at distance >= S from the border is exact."""
+    u = full.clone()
+    for _ in range(steps):
+        n, s, w, e, c = u[:-2, 1:-1], u[2:, 1:-1], u[1:-1, :-2], u[1:-1, 2:], u[1:-1, 1:-1]
+        sums = (n + s) + (w + e)
+        new = u.clone()
+        if u.dtype == torch.float32:
+            c1t = torch.tensor(c1, dtype=torch.float32).double()
+            prod = (torch.tensor(c0, dtype=torch.float32) * c).double()
+            new[1:-1, 1:-1] = (c1t * sums.double() + prod).float()
+        else:
+            new[1:-1, 1:-1] = c1 * sums + c0 * c
+        u = new
+    return u
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 8])
+@pytest.mark.parametrize("shape", [(300, 70), (129, 33), (1024, 96)])
+def test_stencil5_tb_kernel_matches_steps(gpu, dtype, steps, shape):
+    from cuda_mpi_scratch_amd import core, hip
+    from cuda_mpi_scratch_amd.ops.stencil import dtype_name
+
+    w, h = shape
+    g = core().TileGeom.aligned(w, h, steps, steps, torch.tensor([], dtype=dtype).element_size())
+    gen = torch.Generator().manual_seed(steps)
+    host = torch.zeros(g.alloc_elems(), dtype=dtype)
+    v = host.view(g.total_height(), g.pitch)
+    full = torch.rand(g.total_height(), g.total_width(), generator=gen, dtype=torch.float64).to(dtype)
+    v[:, g.x_origin:g.x_origin + g.total_width()] = full
+    src = host.to(gpu)
+    dst = torch.full_like(src, -3.0)
+    hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, 0, w, 0, h, 0.2, 0.2, False, dtype_name(src),
+                      torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = dst.cpu().view(g.total_height(), g.pitch)[g.halo_y:g.halo_y + h, g.x_origin + g.halo_x:g.x_origin + g.halo_x + w]
+    ref = _multi_step_reference(full, steps)[steps:steps + h, steps:steps + w]
+    tol = 2e-7 if dtype == torch.float32 else 1e-15
+    assert torch.allclose(got.double(), ref.double(), rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("backend,loopback", [("local", False), ("rccl", True)])
+@pytest.mark.parametrize("time_block", [2, 4, 6])
+@pytest.mark.parametrize("overlap,graph", [(False, False), (True, True), (True, False)])
+def test_solver_time_blocked(gpu, backend, loopback, time_block, overlap, graph):
+    w, h, iters = 264, 97, 15  # iters not a multiple of the block: remainder path too
+    cfg = StencilConfig(global_width=w, global_height=h, dims="1x1", dtype="f32", backend=backend,
+                        loopback=loopback, graph=graph, overlap=overlap, seed=21, time_block=time_block)
+    st = Stencil2D(cfg)
+    assert st.solver.time_block() == time_block
+    st.run(iters)
+    st.synchronize()
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, 21), iters)
+    assert (st.core_view().cpu() - ref).abs().max().item() < 1e-5
