@@ -16,10 +16,12 @@
 //
 // Positional arguments keep the reference contract: [local width (= height) [stencil width]].
 // More options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
-// --iters N, --warmup N, --no-overlap, --no-graph, --loopback, --bind bunch|rrobin,
+// --iters N, --warmup N, --time-block S (default 4 on timed runs), --no-overlap, --no-graph,
+// --loopback, --bind bunch|rrobin,
 // --dump / --no-dump, --checksum, --non-periodic, --seed S, --json FILE.
 #include <mpi.h>
 
+#include <algorithm>
 #include <cmath>
 #include <fstream>
 #include <iostream>
@@ -56,7 +58,6 @@ template <typename T>
 int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBinding& dev, index_t lw, index_t lh,
         index_t gx0, index_t gy0, index_t gw, index_t gh, int sw, int sh) {
   const int rank = env.rank();
-  const TileGeom g = TileGeom::aligned(lw, lh, sw / 2, sh / 2, int(sizeof(T)));
   const long long iters = cli.get_int("iters", 0);
   const bool dump = cli.has("dump") ? cli.flag("dump") : (iters == 0 && lw <= 64 && lh <= 64 && !cli.flag("no-dump"));
 
@@ -68,6 +69,12 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
     else if (env.local_size() > dev.devices_used) backend = "mpi-staged";  // GPUs shared: RCCL refuses
     else backend = "rccl";
   }
+  // Temporal blocking (timed runs on the solver backends): S Jacobi steps per
+  // launch on an S-deep ghost ring exchanged once per S steps.
+  const int time_block =
+      backend == "mpi-staged" ? 1 : int(cli.get_int("time-block", iters > 0 && lw >= 64 && lh >= 64 ? 4 : 1));
+  const TileGeom g = TileGeom::aligned(lw, lh, std::max(sw / 2, time_block), std::max(sh / 2, time_block),
+                                       int(sizeof(T)));
   std::unique_ptr<RcclComm> comm;
   if (backend == "rccl") comm = make_comm(env);
 
@@ -81,6 +88,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   cfg.use_graph = !cli.flag("no-graph");
   cfg.loopback_self = loopback;
   cfg.coeffs = {cli.get_double("c-center", 0.2), cli.get_double("c-neighbor", 0.2)};
+  cfg.time_block = time_block;
   std::unique_ptr<StencilSolver<T>> solver;
   std::unique_ptr<MpiStagedHalo<T>> staged;
   const HaloPlan plan = make_halo_plan(topo, rank, g, true, loopback);
@@ -169,7 +177,8 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
          << ", \"ms_per_iter\": " << app::fmt(dt / double(iters) * 1e3) << ", \"ranks\": " << env.size()
          << ", \"dims\": \"" << topo.rows << "x" << topo.cols << "\", \"global\": \"" << gw << "x" << gh
          << "\", \"dtype\": \"" << (sizeof(T) == 4 ? "f32" : "f64") << "\", \"backend\": \"" << backend
-         << "\", \"graph\": \"" << (solver ? solver->graph_status() : std::string("n/a")) << "\", \"iters\": " << iters;
+         << "\", \"graph\": \"" << (solver ? solver->graph_status() : std::string("n/a"))
+         << "\", \"time_block\": " << time_block << ", \"iters\": " << iters;
       if (want_sum) js << ", \"checksum\": " << app::fmt(checksum);
       js << "}";
       std::cout << "Gcells/s: " << app::fmt(gcells) << '\n';

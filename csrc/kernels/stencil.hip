@@ -117,18 +117,31 @@ void stencil5_periodic(const T* in, T* out, const TileGeom& g, Stencil5Coeffs c,
 }
 
 namespace {
-// Tuned tile (bench/stencil_tune.hip, profiles/stencil_tuning/tune7-8): 128 fp32
-// columns (64 fp64: same bytes) x 32 rows per 256-thread workgroup, single LDS
-// buffer (23 KB at S = 4 -> 6 workgroups per CU).
-template <typename T, int S, bool WRAP>
-void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
-               hipStream_t s) {
-  constexpr int TW = sizeof(T) == 4 ? 128 : 64;
-  constexpr int TH = 32;
+template <typename T, int S, int TW, int TH, bool WRAP>
+void launch_tb_tile(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
+                    hipStream_t s) {
   const size_t lds = tb1_lds_bytes<T, S, TW, TH>();
   const dim3 grid(unsigned((x1 - x0 + TW - 1) / TW), unsigned((y1 - y0 + TH - 1) / TH));
   stencil5_tb1_kernel<T, S, TW, TH, WRAP><<<grid, 256, lds, s>>>(in, out, g.pitch, g.core_offset(), g.width,
                                                                  g.height, x0, x1, y0, y1, c0, c1);
+}
+
+// Tile shapes: the bulk tile is tuned (bench/stencil_tune.hip, profiles/
+// stencil_tuning/tune7-9): 128 fp32 columns (64 fp64: same bytes) x 32 rows per
+// 256-thread workgroup, single LDS buffer (23 KB at S = 4 -> 6 workgroups per
+// CU). The overlap schedule's boundary strips are S rows or S columns thin; a
+// bulk tile would recompute 8-32x the strip, so thin strips get a matching
+// thin tile (32 x 128 for column strips, 128 x 8 for row strips).
+template <typename T, int S, bool WRAP>
+void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
+               hipStream_t s) {
+  constexpr int TW = sizeof(T) == 4 ? 128 : 64;
+  constexpr int NW = sizeof(T) == 4 ? 32 : 16;
+  if constexpr (!WRAP) {
+    if (x1 - x0 <= NW) return launch_tb_tile<T, S, NW, 128, false>(in, out, g, x0, x1, y0, y1, c0, c1, s);
+    if (y1 - y0 <= 8) return launch_tb_tile<T, S, TW, 8, false>(in, out, g, x0, x1, y0, y1, c0, c1, s);
+  }
+  launch_tb_tile<T, S, TW, 32, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
 }
 
 template <typename T, bool WRAP>

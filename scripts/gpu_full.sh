@@ -12,3 +12,5 @@ timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || { echo bench fa
 tail -1 gpurun_out/bench.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_bench" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 --warmup 5 --no-extras > gpurun_out/prof_bench.log 2>&1
 echo "rocprof rc=$?"
+[ -n "$WITH_TUNE" ] && { TUNE_TAG=$WITH_TUNE bash scripts/gpu_tune.sh || exit 1; }
+exit 0

@@ -61,6 +61,19 @@ def test_stencil_gpu_matches_cpu_app(gpu, tmp_path, n, dims):
     assert abs(a - b) <= 1e-9 * abs(b)
 
 
+@pytest.mark.parametrize("extra", [["--loopback", "--time-block", "3"], ["--loopback", "--time-block", "4", "--no-overlap"],
+                                   ["--time-block", "1"], ["--time-block", "5", "--no-graph"]])
+def test_stencil_gpu_time_block_matches_cpu_app(gpu, tmp_path, extra):
+    args = ["--global", "200x72", "--dims", "1x1", "--dtype", "f64", "--iters", "11", "--stencil", "3"]
+    g = mpirun(1, "stencil2d", *args, "--checksum", "--warmup", "0", *extra, cwd=tmp_path)
+    assert g.returncode == 0, g.stderr[-3000:]
+    assert f'"time_block": {extra[extra.index("--time-block") + 1]}' in g.stdout
+    c = mpirun(1, "stencil2d_cpu", *args, cwd=tmp_path)
+    assert c.returncode == 0, c.stderr[-3000:]
+    a, b = _checksum(g.stdout), _checksum(c.stdout)
+    assert abs(a - b) <= 1e-9 * abs(b)
+
+
 def test_stencil_gpu_timed_run_reports_rate(gpu, tmp_path):
     r = mpirun(1, "stencil2d", "--global", "4096x4096", "--dtype", "f32", "--iters", "50", "--stencil", "3",
                cwd=tmp_path)

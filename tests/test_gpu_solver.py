@@ -127,3 +127,33 @@ def test_solver_time_blocked(gpu, backend, loopback, time_block, overlap, graph)
     st.synchronize()
     ref = jacobi_reference_global(random_values(0, 0, w, h, w, 21), iters)
     assert (st.core_view().cpu() - ref).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("steps", [2, 4])
+@pytest.mark.parametrize("rect", [(0, 300, 0, 4), (0, 8, 4, 66), (288, 300, 4, 66), (0, 300, 66, 70), (16, 40, 3, 50)])
+def test_stencil5_tb_kernel_strips(gpu, dtype, steps, rect):
+    """Thin boundary strips (the overlap schedule's rows / columns) take their own
+    tile shapes; the result inside the rect is exact and nothing outside is written."""
+    from cuda_mpi_scratch_amd import core, hip
+    from cuda_mpi_scratch_amd.ops.stencil import dtype_name
+
+    w, h = 300, 70
+    x0, x1, y0, y1 = rect
+    g = core().TileGeom.aligned(w, h, steps, steps, torch.tensor([], dtype=dtype).element_size())
+    gen = torch.Generator().manual_seed(5)
+    host = torch.zeros(g.alloc_elems(), dtype=dtype)
+    full = torch.rand(g.total_height(), g.total_width(), generator=gen, dtype=torch.float64).to(dtype)
+    host.view(g.total_height(), g.pitch)[:, g.x_origin:g.x_origin + g.total_width()] = full
+    src = host.to(gpu)
+    dst = torch.full_like(src, -3.0)
+    hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, x0, x1, y0, y1, 0.2, 0.2, False, dtype_name(src),
+                      torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = dst.cpu().view(g.total_height(), g.pitch)[g.halo_y:g.halo_y + h, g.x_origin + g.halo_x:g.x_origin + g.halo_x + w]
+    ref = _multi_step_reference(full, steps)[steps:steps + h, steps:steps + w]
+    tol = 2e-7 if dtype == torch.float32 else 1e-15
+    assert torch.allclose(got[y0:y1, x0:x1].double(), ref[y0:y1, x0:x1].double(), rtol=tol, atol=tol)
+    mask = torch.ones(h, w, dtype=torch.bool)
+    mask[y0:y1, x0:x1] = False
+    assert (got[mask] == -3.0).all()
