@@ -16,7 +16,7 @@
 //
 // Positional arguments keep the reference contract: [local width (= height) [stencil width]].
 // More options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
-// --iters N, --warmup N, --time-block S (default 4 on timed runs), --no-overlap, --no-graph,
+// --iters N, --warmup N, --time-block S (default 12 on timed runs), --no-overlap, --no-graph,
 // --loopback, --bind bunch|rrobin,
 // --dump / --no-dump, --checksum, --non-periodic, --seed S, --json FILE.
 #include <mpi.h>
@@ -72,7 +72,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   // Temporal blocking (timed runs on the solver backends): S Jacobi steps per
   // launch on an S-deep ghost ring exchanged once per S steps.
   const int time_block =
-      backend == "mpi-staged" ? 1 : int(cli.get_int("time-block", iters > 0 && lw >= 64 && lh >= 64 ? 4 : 1));
+      backend == "mpi-staged" ? 1 : int(cli.get_int("time-block", iters > 0 && lw >= 64 && lh >= 64 ? 12 : 1));
   const TileGeom g = TileGeom::aligned(lw, lh, std::max(sw / 2, time_block), std::max(sh / 2, time_block),
                                        int(sizeof(T)));
   std::unique_ptr<RcclComm> comm;

@@ -31,6 +31,7 @@ struct Variant {
   std::function<void(hipStream_t)> launch;
   std::vector<float> ms;
   int steps = 1;  // Jacobi iterations per launch
+  std::function<void(hipStream_t)> ref;  // validated kernel computing the same thing
 };
 
 template <int ROWS, int CH, bool NT, int WX, bool NTL, int NW = 4>
@@ -74,12 +75,42 @@ Variant tb1(const float* in, float* out, const TileGeom& g) {
   return v;
 }
 
+// tmp: scratch tile for the two-pass reference of S > 8 (wrap only: two periodic
+// half-blocks equal one block; without wrap the frozen ghost ring differs).
+template <int S, int PF, bool WRAP = false, bool SKEW = true>
+Variant stream(const float* in, float* out, const TileGeom& g, int ch, float* tmp = nullptr) {
+  char buf[128];
+  std::snprintf(buf, sizeof(buf), "stream_s%d_pf%d_ch%d%s%s", S, PF, ch, WRAP ? "_wrap" : "", SKEW ? "" : "_chain");
+  Variant v{buf, [=](hipStream_t s) {
+              constexpr int OW = StreamShape<float, S>::OW;
+              const index_t strips = (g.width + OW - 1) / OW;
+              const dim3 grid(unsigned((strips + 3) / 4), unsigned((g.height + ch - 1) / ch));
+              stencil5_stream_kernel<float, S, PF, WRAP, SKEW><<<grid, 256, 0, s>>>(
+                  in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, index_t(ch), 0.2f,
+                  0.2f);
+            }};
+  v.steps = S;
+  if constexpr (S <= 8) {
+    v.ref = tb1<S, 128, 32, WRAP>(in, out, g).launch;
+  } else if constexpr (WRAP && S % 2 == 0) {
+    if (tmp) {
+      auto first = tb1<S / 2, 128, 32, true>(in, tmp, g).launch;
+      auto second = tb1<S / 2, 128, 32, true>(tmp, out, g).launch;
+      v.ref = [=](hipStream_t s) {
+        first(s);
+        second(s);
+      };
+    }
+  }
+  return v;
+}
+
 int main(int argc, char** argv) {
   const index_t W = argc > 1 ? atol(argv[1]) : 32768;
   const index_t H = argc > 2 ? atol(argv[2]) : 32768;
   const int rounds = argc > 3 ? atoi(argv[3]) : 5;
-  const TileGeom g = TileGeom::aligned(W, H, 8, 8, 4);  // 8-deep ghost ring: non-wrap tb variants up to S = 8
-  DeviceBuffer<float> a(g.alloc_elems()), b(g.alloc_elems());
+  const TileGeom g = TileGeom::aligned(W, H, 16, 16, 4);  // 16-deep ghost ring: non-wrap variants up to S = 16
+  DeviceBuffer<float> a(g.alloc_elems()), b(g.alloc_elems()), c(g.alloc_elems());
   // Random data: zero-filled operands raise the clock under load and inflate
   // the numbers (cdna_hip_programming.md §5.4 rule 25).
   kernels::fill<float>(a.get(), g.alloc_elems(), 0.f, nullptr);
@@ -101,20 +132,24 @@ int main(int argc, char** argv) {
                 }});
   vs.push_back(roll<3, 3, true, 4, false>(in, out, g));
   vs.push_back(roll<4, 4, true, 4, false>(in, out, g));
-  vs.push_back(tb1<2, 128, 32, false>(in, out, g));
-  vs.push_back(tb1<3, 128, 32, false>(in, out, g));
   vs.push_back(tb1<4, 128, 32, false>(in, out, g));
   vs.push_back(tb1<4, 128, 32, true>(in, out, g));
-  vs.push_back(tb1<4, 128, 24, false>(in, out, g));
   vs.push_back(tb1<4, 192, 24, false>(in, out, g));
-  vs.push_back(tb1<4, 128, 16, false>(in, out, g));
-  vs.push_back(tb1<5, 128, 32, false>(in, out, g));
   vs.push_back(tb1<6, 128, 32, false>(in, out, g));
-  vs.push_back(tb1<6, 128, 24, false>(in, out, g));
-  vs.push_back(tb1<8, 128, 32, false>(in, out, g));
-  vs.push_back(tb1<8, 128, 48, false>(in, out, g));
-  vs.push_back(tb1<4, 64, 32, false>(in, out, g));
-  vs.push_back(tb1<4, 64, 64, false>(in, out, g));
+  float* tmp = c.get();
+  vs.push_back(stream<8, 3, false, false>(in, out, g, 256));
+  vs.push_back(stream<12, 3, true, false>(in, out, g, 256, tmp));
+  for (int ch : {64, 128, 256, 512}) {
+    vs.push_back(stream<4, 3>(in, out, g, ch));
+    vs.push_back(stream<8, 3>(in, out, g, ch));
+    vs.push_back(stream<12, 3>(in, out, g, ch));
+    vs.push_back(stream<16, 3>(in, out, g, ch));
+    vs.push_back(stream<8, 3, true>(in, out, g, ch));
+    vs.push_back(stream<12, 3, true>(in, out, g, ch, tmp));
+    vs.push_back(stream<16, 3, true>(in, out, g, ch, tmp));
+  }
+  vs.push_back(stream<8, 6>(in, out, g, 256));
+  vs.push_back(stream<12, 6>(in, out, g, 256));
 
   Stream st;
   Event e0(true), e1(true);
@@ -128,6 +163,22 @@ int main(int argc, char** argv) {
     if (e != hipSuccess) {
       std::printf("{\"variant\": \"%s\", \"error\": \"%s\"}\n", v.name.c_str(), hipGetErrorString(e));
       continue;
+    }
+    if (v.ref) {
+      // Bitwise check against the validated LDS kernel (same evaluation order).
+      std::vector<float> got(size_t(g.alloc_elems())), want(size_t(g.alloc_elems()));
+      MXS_HIP_CHECK(hipMemcpy(got.data(), out, got.size() * 4, hipMemcpyDeviceToHost));
+      v.ref(st.get());
+      st.sync();
+      MXS_HIP_CHECK(hipMemcpy(want.data(), out, want.size() * 4, hipMemcpyDeviceToHost));
+      long long bad = 0;
+      for (index_t y = 0; y < H; ++y)
+        for (index_t x = 0; x < W; ++x) {
+          const size_t i = size_t(g.core_offset() + y * g.pitch + x);
+          bad += got[i] != want[i];
+        }
+      std::printf("{\"variant\": \"%s\", \"mismatches\": %lld}\n", v.name.c_str(), bad);
+      if (bad) continue;
     }
     ok.push_back(std::move(v));
   }

@@ -63,16 +63,20 @@ template <typename T>
 bool stencil5_periodic_supported(const TileGeom& g);
 
 // Temporal blocking: `steps` (S) Jacobi iterations in one launch over the core
-// rectangle [x0, x1) x [y0, y1), LDS-tiled (each workgroup stages its tile plus an
-// S-deep apron once, iterates S times in LDS, writes once: ~S x less HBM traffic
-// per iteration). The source must hold valid data S cells around the rectangle:
-// a ghost ring >= S deep exchanged for this super-step, or `wrap` (1x1 periodic
-// grid: reads wrap around the tile). Supported S: 1..8. Bitwise identical to S
-// single steps (same per-cell fma sequence).
-constexpr int kMaxTimeBlock = 8;
+// rectangle [x0, x1) x [y0, y1): every input byte crosses HBM once per S
+// iterations. The source must hold valid data S cells around the rectangle: a
+// ghost ring >= S deep exchanged for this super-step, or `wrap` (1x1 periodic
+// grid: reads wrap around the tile). Bitwise identical to S single steps (same
+// per-cell fma sequence). Variants:
+//   Auto         wave-streaming kernel (register windows per time level, no LDS)
+//                for the bulk, LDS tiles of matching shape for thin strips;
+//   LdsTile      LDS-tiled (each workgroup stages its tile plus an S-deep apron,
+//                iterates in LDS; S <= 8 for the bulk tile);
+//   RegisterRoll same as Auto.
+constexpr int kMaxTimeBlock = 16;
 template <typename T>
 void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0, index_t y1,
-                 Stencil5Coeffs c, bool wrap, hipStream_t s);
+                 Stencil5Coeffs c, bool wrap, hipStream_t s, StencilVariant v = StencilVariant::Auto);
 
 // Update an arbitrary core rectangle [x0, x1) x [y0, y1) (scalar path; used for the
 // boundary columns of the overlapped schedule and for tiny tiles).

@@ -87,7 +87,7 @@ class StencilSolver {
   index_t cells_per_iteration() const { return tile_.width * tile_.height; }
 
  private:
-  void enqueue_block(T* cur, T* nxt);   // block_ iterations
+  void enqueue_block(T* cur, T* nxt, int S);  // S <= block_ iterations, one exchange
   void enqueue_single(T* cur, T* nxt);  // 1 iteration (remainders)
   // `steps` iterations over core rows [r0, r1) x cols [c0, c1).
   void update(const T* in, T* out, int steps, index_t c0, index_t c1, index_t r0, index_t r1, hipStream_t s);

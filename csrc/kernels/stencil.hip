@@ -126,44 +126,62 @@ void launch_tb_tile(const T* in, T* out, const TileGeom& g, index_t x0, index_t 
                                                                  g.height, x0, x1, y0, y1, c0, c1);
 }
 
-// Tile shapes: the bulk tile is tuned (bench/stencil_tune.hip, profiles/
-// stencil_tuning/tune7-9): 128 fp32 columns (64 fp64: same bytes) x 32 rows per
-// 256-thread workgroup, single LDS buffer (23 KB at S = 4 -> 6 workgroups per
-// CU). The overlap schedule's boundary strips are S rows or S columns thin; a
-// bulk tile would recompute 8-32x the strip, so thin strips get a matching
-// thin tile (32 x 128 for column strips, 128 x 8 for row strips).
+// Wave-streaming kernel (stencil_device.hpp). Row chunk CH: the largest of
+// 512..64 that still yields >= 4096 waves (4 per SIMD); a chunk recomputes 2S
+// rows of apron, so tall chunks pay less, short ones fill the chip. Tuned with
+// bench/stencil_tune.hip (profiles/stencil_tuning/tune12-13): 32768^2 -> 512,
+// 8192 x 16384 -> 128, 8192^2 -> 64.
 template <typename T, int S, bool WRAP>
-void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
-               hipStream_t s) {
-  constexpr int TW = sizeof(T) == 4 ? 128 : 64;
-  constexpr int NW = sizeof(T) == 4 ? 32 : 16;
-  if constexpr (!WRAP) {
-    if (x1 - x0 <= NW) return launch_tb_tile<T, S, NW, 128, false>(in, out, g, x0, x1, y0, y1, c0, c1, s);
-    if (y1 - y0 <= 8) return launch_tb_tile<T, S, TW, 8, false>(in, out, g, x0, x1, y0, y1, c0, c1, s);
-  }
-  launch_tb_tile<T, S, TW, 32, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
+void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
+                   hipStream_t s) {
+  constexpr int OW = StreamShape<T, S>::OW;
+  const index_t strips = (x1 - x0 + OW - 1) / OW;
+  const index_t rows = y1 - y0;
+  index_t ch = 512;
+  while (ch > 64 && strips * ((rows + ch - 1) / ch) < 4096) ch /= 2;
+  const dim3 grid(unsigned((strips + kWavesPerBlock - 1) / kWavesPerBlock), unsigned((rows + ch - 1) / ch));
+  stencil5_stream_kernel<T, S, 3, WRAP><<<grid, kBlock, 0, s>>>(in, out, g.pitch, g.core_offset(), g.width, g.height,
+                                                                x0, x1, y0, y1, ch, c0, c1);
 }
 
-template <typename T, bool WRAP>
+// Dispatch by shape. Bulk rectangles take the wave-streaming kernel (Auto) or
+// the LDS tile (LdsTile, S <= 8): 128 fp32 columns (64 fp64: same bytes) x 32
+// rows per 256-thread workgroup, single LDS buffer. The overlap schedule's
+// boundary strips are only S rows or S columns thin; a bulk tile or a 256-column
+// wave strip would recompute 8-32x the strip, so thin strips get a matching thin
+// LDS tile (32 x 128 for column strips, 128 x 16 for row strips).
+template <typename T, int S, bool WRAP>
+void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
+               StencilVariant v, hipStream_t s) {
+  constexpr int TW = sizeof(T) == 4 ? 128 : 64;
+  constexpr int NW = sizeof(T) == 4 ? 32 : 16;
+  constexpr int NH = (sizeof(T) == 8 && S > 8) ? 64 : 128;  // keeps the fp64 thin tile under 64 KB of LDS
+  if constexpr (!WRAP) {
+    if (x1 - x0 <= NW) return launch_tb_tile<T, S, NW, NH, false>(in, out, g, x0, x1, y0, y1, c0, c1, s);
+    if (y1 - y0 <= 16) return launch_tb_tile<T, S, TW, 16, false>(in, out, g, x0, x1, y0, y1, c0, c1, s);
+  }
+  if constexpr (S <= 8) {
+    if (v == StencilVariant::LdsTile)
+      return launch_tb_tile<T, S, TW, 32, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
+  }
+  launch_stream<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
+}
+
+template <typename T, bool WRAP, int S = 1>
 void dispatch_tb(int steps, const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
-                 T c0, T c1, hipStream_t s) {
-  switch (steps) {
-    case 1: launch_tb<T, 1, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
-    case 2: launch_tb<T, 2, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
-    case 3: launch_tb<T, 3, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
-    case 4: launch_tb<T, 4, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
-    case 5: launch_tb<T, 5, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
-    case 6: launch_tb<T, 6, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
-    case 7: launch_tb<T, 7, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
-    case 8: launch_tb<T, 8, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s); break;
-    default: MXS_CHECK(false, "stencil5_tb: steps must be in [1, " << kMaxTimeBlock << "], got " << steps);
+                 T c0, T c1, StencilVariant v, hipStream_t s) {
+  if constexpr (S <= kMaxTimeBlock) {
+    if (steps == S) return launch_tb<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+    return dispatch_tb<T, WRAP, S + 1>(steps, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+  } else {
+    MXS_CHECK(false, "stencil5_tb: steps must be in [1, " << kMaxTimeBlock << "], got " << steps);
   }
 }
 }  // namespace
 
 template <typename T>
 void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0, index_t y1,
-                 Stencil5Coeffs c, bool wrap, hipStream_t s) {
+                 Stencil5Coeffs c, bool wrap, hipStream_t s, StencilVariant v) {
   if (x1 <= x0 || y1 <= y0) return;
   constexpr int N = Vec16<T>::N;
   MXS_CHECK(x0 >= 0 && y0 >= 0 && x1 <= g.width && y1 <= g.height, "stencil5_tb: rect out of the core");
@@ -172,6 +190,7 @@ void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, 
   const int sa = ((steps + N - 1) / N) * N;
   if (wrap) {
     MXS_CHECK(g.width % N == 0, "stencil5_tb wrap: width must be a multiple of the vector width");
+    MXS_CHECK(g.height >= steps, "stencil5_tb wrap: tile height " << g.height << " < time block " << steps);
   } else {
     MXS_CHECK(g.halo_x >= steps && g.halo_y >= steps,
               "stencil5_tb: ghost ring (" << g.halo_x << ") shallower than the time block (" << steps << ")");
@@ -179,8 +198,8 @@ void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, 
               "stencil5_tb: row padding too small for the x apron");
   }
   const T c0 = T(c.center), c1 = T(c.neighbor);
-  if (wrap) dispatch_tb<T, true>(steps, in, out, g, x0, x1, y0, y1, c0, c1, s);
-  else dispatch_tb<T, false>(steps, in, out, g, x0, x1, y0, y1, c0, c1, s);
+  if (wrap) dispatch_tb<T, true>(steps, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+  else dispatch_tb<T, false>(steps, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   MXS_HIP_CHECK_LAUNCH();
 }
 
@@ -218,7 +237,7 @@ void stencil_box(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1,
                                  Stencil5Coeffs, hipStream_t);                                                 \
   template void stencil5_periodic<T>(const T*, T*, const TileGeom&, Stencil5Coeffs, hipStream_t);              \
   template void stencil5_tb<T>(const T*, T*, const TileGeom&, int, index_t, index_t, index_t, index_t,          \
-                               Stencil5Coeffs, bool, hipStream_t);                                             \
+                               Stencil5Coeffs, bool, hipStream_t, StencilVariant);                             \
   template bool stencil5_periodic_supported<T>(const TileGeom&);                                               \
   template void stencil_box<T>(const T*, T*, const TileGeom&, index_t, index_t, index_t, index_t,               \
                                const BoxWeights&, hipStream_t);

@@ -503,6 +503,217 @@ constexpr size_t tb1_lds_bytes() {
   return tb_lds_bytes<T, S, TW, TH>() / 2;
 }
 
+// One vector of outputs from its three rows and the two scalars beside `mid`.
+template <typename T, typename V, int N>
+__device__ __forceinline__ V jac_vec(const V& up, const V& mid, const V& dn, T left, T right, T c0, T c1) {
+  V o;
+  o[0] = jac<T>(mid[0], up[0], dn[0], left, mid[1 % N], c0, c1);
+  if constexpr (N == 2) {
+    o[1] = jac<T>(mid[1], up[1], dn[1], mid[0], right, c0, c1);
+  } else {
+#pragma unroll
+    for (int q = 1; q < N - 1; ++q) o[q] = jac<T>(mid[q], up[q], dn[q], mid[q - 1], mid[q + 1], c0, c1);
+    o[N - 1] = jac<T>(mid[N - 1], up[N - 1], dn[N - 1], mid[N - 2], right, c0, c1);
+  }
+  return o;
+}
+
+// fp32 x4 form written on aligned register pairs, so the backend emits packed
+// v_pk_{add,mul,fma}_f32 without pair-building moves; the horizontal sums are
+// scalar adds written straight into pairs. Same per-element operations and
+// order as jac() (IEEE add is commutative), so results are bitwise identical.
+using f32x2 = float __attribute__((ext_vector_type(2)));
+using f32x4 = float __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 jac_vec4f(const f32x4& up, const f32x4& mid, const f32x4& dn, float left,
+                                           float right, float c0, float c1) {
+  const f32x2 ns_lo = up.xy + dn.xy, ns_hi = up.zw + dn.zw;
+  f32x2 we_lo, we_hi;
+  we_lo.x = left + mid.y;
+  we_lo.y = mid.x + mid.z;
+  we_hi.x = mid.y + mid.w;
+  we_hi.y = mid.z + right;
+  const f32x2 c0v = f32x2(c0), c1v = f32x2(c1);
+  const f32x2 lo = __builtin_elementwise_fma(c1v, ns_lo + we_lo, c0v * mid.xy);
+  const f32x2 hi = __builtin_elementwise_fma(c1v, ns_hi + we_hi, c0v * mid.zw);
+  f32x4 o;
+  o.xy = lo;
+  o.zw = hi;
+  return o;
+}
+
+template <typename T, typename V>
+__device__ __forceinline__ V jac_row(const V& up, const V& mid, const V& dn, T left, T right, T c0, T c1) {
+  if constexpr (sizeof(T) == 4) return jac_vec4f(up, mid, dn, left, right, c0, c1);
+  else return jac_vec<T, V, Vec16<T>::N>(up, mid, dn, left, right, c0, c1);
+}
+
+// ------------------------------------------------------- wave-streaming blocks
+// Temporal blocking without LDS and without vertical recompute. Each wave owns a
+// column strip (64 lanes x one 16-byte vector = 256 fp32 / 128 fp64 columns, of
+// which the outer SA columns per side are apron) and streams down a chunk of CH
+// rows. It keeps a three-row window per time level in registers: when input row
+// y arrives, level 1 row y-1 is computed from level-0 rows y-2..y, level 2 row
+// y-2 from level-1 rows y-3..y-1, ..., level S row y-S is stored. Row neighbours
+// come from the same lane's window; column neighbours from the adjacent lanes
+// through ds_bpermute. Every level advances once per input row, so HBM sees one
+// read and one write per cell per S steps (plus 2S/CH rows and 2SA/256 columns
+// of redundant apron). The window is three register slots per level used
+// round-robin (the loop is unrolled by a multiple of 3), so no row is ever
+// copied between registers: VALU work is just the stencil arithmetic.
+template <typename T>
+__device__ __forceinline__ T lane_fetch(T v, int byte_addr);
+template <>
+__device__ __forceinline__ float lane_fetch<float>(float v, int a) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(a, __float_as_int(v)));
+}
+template <>
+__device__ __forceinline__ double lane_fetch<double>(double v, int a) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(a, int(b & 0xffffffff));
+  const int hi = __builtin_amdgcn_ds_bpermute(a, int(b >> 32));
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
+template <typename T, int S>
+struct StreamShape {
+  static constexpr int N = Vec16<T>::N;
+  static constexpr int SA = ((S + N - 1) / N) * N;      // apron columns per side
+  static constexpr int OW = kWaveSize * N - 2 * SA;     // output columns per wave
+};
+
+// Workgroup = 4 waves on 4 adjacent strips of the same row chunk. PF = input
+// rows in flight per wave (a register ring, statically indexed; multiple of 3).
+template <typename T, int S, int PF, bool WRAP, bool SKEW = true>
+__global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                                 index_t pitch, index_t core_off, index_t W, index_t H,
+                                                                 index_t x_begin, index_t x_end, index_t y_begin,
+                                                                 index_t y_end, index_t CH, T c0, T c1) {
+  static_assert(PF % 3 == 0, "the window rotates through 3 slots: PF must be a multiple of 3");
+  using Sh = StreamShape<T, S>;
+  constexpr int N = Sh::N, SA = Sh::SA, OW = Sh::OW, AL = SA / N;
+  using V = typename Vec16<T>::type;
+  const int lane = threadIdx.x & (kWaveSize - 1);
+  const int wave = threadIdx.x / kWaveSize;
+  const index_t xw = x_begin + (index_t(blockIdx.x) * kWavesPerBlock + wave) * OW;
+  if (xw >= x_end) return;  // wave-uniform
+  const index_t ys = y_begin + index_t(blockIdx.y) * CH;
+  const index_t ye = ys + CH < y_end ? ys + CH : y_end;
+  const index_t gx = xw - SA + index_t(lane) * N;
+
+  index_t lx = gx;
+  bool load_ok = true;
+  if constexpr (WRAP) {
+    if (W >= kWaveSize * N) lx = gx < 0 ? gx + W : (gx >= W ? gx - W : gx);
+    else lx = ((gx % W) + W) % W;
+  } else {
+    load_ok = gx < W + SA;  // inside the row padding of TileGeom::aligned
+  }
+  const T* __restrict__ pin = in + core_off + lx;
+  const bool store_lane = lane >= AL && lane < kWaveSize - AL && gx < x_end;
+  const bool full_vec = gx + N <= x_end;
+  const int addr_l = ((lane + kWaveSize - 1) & (kWaveSize - 1)) << 2;
+  const int addr_r = ((lane + 1) & (kWaveSize - 1)) << 2;
+
+  // Next input row to fetch, as a (wrapped) row index.
+  const index_t y_first = ys - S;
+  index_t next = y_first;
+  if constexpr (WRAP) next = next < 0 ? next + H : next;
+  auto fetch = [&]() -> V {
+    V v = V(T(0));
+    if (load_ok) v = *reinterpret_cast<const V*>(pin + next * pitch);
+    ++next;
+    if constexpr (WRAP) next = next == H ? 0 : next;
+    return v;
+  };
+  T* __restrict__ pout = out + core_off + gx + ys * pitch;  // row of the first output (input j = 2S)
+
+  V win[3][S];
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int l = 0; l < S; ++l) win[q][l] = V(T(0));
+
+  const index_t n_in = (ye - ys) + 2 * S;
+  V pf[PF];
+#pragma unroll
+  for (int k = 0; k < PF; ++k) pf[k] = k < n_in ? fetch() : V(T(0));
+
+  if constexpr (SKEW) {
+    // Skewed schedule: in iteration j level l works on the row level l-1 made in
+    // iteration j-1, so the S levels of one iteration are independent (S-way
+    // ILP instead of an S-long dependent chain of bpermute -> VALU). Slots per
+    // level rotate with the phase p = j % 3: up = win[p], mid = win[p+1],
+    // dn = win[p+2]; level l writes its output into win[p][l+1], the slot that
+    // is level l+1's dn next iteration, after level l+1 has read it as up (so
+    // levels run top-down). Level S-1 outputs row y_first + j - 2S + 1.
+    const index_t n_it = (ye - ys) + 3 * S - 1;
+#pragma unroll 1
+    for (index_t i = 0; i < n_it; i += PF) {
+#pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const index_t j = i + k;
+        if (j < n_it) {
+          const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;  // static after the unroll
+          win[p2][0] = pf[k];
+          if (j + PF < n_in) pf[k] = fetch();
+          V top = V(T(0));
+#pragma unroll
+          for (int l = S - 1; l >= 0; --l) {
+            const V m = win[p1][l];
+            const T left = lane_fetch<T>(m[N - 1], addr_l);
+            const T right = lane_fetch<T>(m[0], addr_r);
+            const V o = jac_row<T, V>(win[p0][l], m, win[p2][l], left, right, c0, c1);
+            if (l == S - 1) top = o;
+            else win[p0][l + 1] = o;
+          }
+          if (j >= 3 * S - 1 && store_lane) {  // row ys + (j - 3S + 1)
+            T* p = pout + (j - (3 * S - 1)) * pitch;
+            if (full_vec) {
+              __builtin_nontemporal_store(top, reinterpret_cast<V*>(p));
+            } else {
+#pragma unroll
+              for (int q = 0; q < N; ++q)
+                if (gx + q < x_end) p[q] = top[q];
+            }
+          }
+        }
+      }
+    }
+    return;
+  }
+#pragma unroll 1
+  for (index_t i = 0; i < n_in; i += PF) {
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      const index_t j = i + k;
+      if (j < n_in) {
+        V nw = pf[k];
+        if (j + PF < n_in) pf[k] = fetch();
+        const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;  // static after the unroll
+#pragma unroll
+        for (int l = 0; l < S; ++l) {
+          const V m = win[p1][l];
+          const T left = lane_fetch<T>(m[N - 1], addr_l);
+          const T right = lane_fetch<T>(m[0], addr_r);
+          const V o = jac_row<T, V>(win[p0][l], m, nw, left, right, c0, c1);
+          win[p2][l] = nw;
+          nw = o;
+        }
+        if (j >= 2 * S && store_lane) {  // level-S row ys + (j - 2S)
+          T* p = pout + (j - 2 * S) * pitch;
+          if (full_vec) {
+            __builtin_nontemporal_store(nw, reinterpret_cast<V*>(p));
+          } else {
+#pragma unroll
+            for (int q = 0; q < N; ++q)
+              if (gx + q < x_end) p[q] = nw[q];
+          }
+        }
+      }
+    }
+  }
+}
+
 }  // namespace detail
 }  // namespace kernels
 }  // namespace mxs

@@ -146,16 +146,19 @@ PYBIND11_MODULE(_mxs_hip, m) {
   m.def(
       "stencil5_tb",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0,
-         index_t y1, double c0, double c1, bool wrap, const std::string& dt, std::uintptr_t s) {
+         index_t y1, double c0, double c1, bool wrap, const std::string& dt, std::uintptr_t s,
+         const std::string& variant) {
         kernels::Stencil5Coeffs c{c0, c1};
+        const kernels::StencilVariant v = parse_variant(variant);
         if (parse_dtype(dt) == DType::F32)
-          kernels::stencil5_tb<float>(ptr<float>(in), ptr<float>(out), g, steps, x0, x1, y0, y1, c, wrap, strm(s));
+          kernels::stencil5_tb<float>(ptr<float>(in), ptr<float>(out), g, steps, x0, x1, y0, y1, c, wrap, strm(s), v);
         else
-          kernels::stencil5_tb<double>(ptr<double>(in), ptr<double>(out), g, steps, x0, x1, y0, y1, c, wrap, strm(s));
+          kernels::stencil5_tb<double>(ptr<double>(in), ptr<double>(out), g, steps, x0, x1, y0, y1, c, wrap, strm(s),
+                                       v);
       },
       py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("steps"), py::arg("x0"), py::arg("x1"), py::arg("y0"),
       py::arg("y1"), py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2, py::arg("wrap") = false,
-      py::arg("dtype") = "f32", py::arg("stream") = 0);
+      py::arg("dtype") = "f32", py::arg("stream") = 0, py::arg("variant") = "auto");
   m.def(
       "stencil5_rect",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,

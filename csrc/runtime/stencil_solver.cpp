@@ -13,6 +13,9 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   // unpack / boundary launches should not queue behind the long interior sweep.
   block_ = cfg_.kind == StencilKind::Jacobi5 ? std::max(1, cfg_.time_block) : 1;
   MXS_CHECK(block_ <= kernels::kMaxTimeBlock, "time_block must be <= " << kernels::kMaxTimeBlock);
+  MXS_CHECK(block_ <= tile_.width && block_ <= tile_.height,
+            "time_block " << block_ << " exceeds the tile (" << tile_.width << "x" << tile_.height
+                          << "): its ghost ring would reach past the neighbouring tiles");
   radius_ = cfg_.kind == StencilKind::Box ? cfg_.box.radius : 1;
   const int depth = std::max(radius_, block_);  // cells a super-step reads beyond the core
   MXS_CHECK(tile_.halo_x >= depth && tile_.halo_y >= depth,
@@ -41,7 +44,7 @@ void StencilSolver<T>::update(const T* in, T* out, int steps, index_t c0, index_
   if (cfg_.kind == StencilKind::Box) {
     kernels::stencil_box<T>(in, out, tile_, c0, c1, r0, r1, cfg_.box, s);
   } else if (steps > 1) {
-    kernels::stencil5_tb<T>(in, out, tile_, steps, c0, c1, r0, r1, cfg_.coeffs, false, s);
+    kernels::stencil5_tb<T>(in, out, tile_, steps, c0, c1, r0, r1, cfg_.coeffs, false, s, cfg_.variant);
   } else if (c0 == 0 && c1 == tile_.width) {
     kernels::stencil5_rows<T>(in, out, tile_, r0, r1, cfg_.coeffs, s, cfg_.variant);
   } else {
@@ -65,13 +68,12 @@ void StencilSolver<T>::enqueue_single(T* cur, T* nxt) {
 // sweep forks onto the SIDE stream. RCCL calls must sit on the capture-origin
 // stream: captured from a forked stream, RCCL (ROCm 7.x) crashes at capture.
 template <typename T>
-void StencilSolver<T>::enqueue_block(T* cur, T* nxt) {
+void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
   const index_t h = tile_.height, w = tile_.width;
-  const int S = block_;
   hipStream_t m = main_.get(), side = side_.get();
   if (fused_) {
     if (S == 1) kernels::stencil5_periodic<T>(cur, nxt, tile_, cfg_.coeffs, m);
-    else kernels::stencil5_tb<T>(cur, nxt, tile_, S, 0, w, 0, h, cfg_.coeffs, true, m);
+    else kernels::stencil5_tb<T>(cur, nxt, tile_, S, 0, w, 0, h, cfg_.coeffs, true, m, cfg_.variant);
     return;
   }
   if (!cfg_.overlap) {
@@ -112,7 +114,7 @@ bool StencilSolver<T>::try_capture() {
     }
     bool ok = true;
     try {
-      enqueue_block(a, b);
+      enqueue_block(a, b, block_);
     } catch (const std::exception& e) {
       graph_status_ = std::string("capture failed: ") + e.what();
       ok = false;
@@ -145,12 +147,15 @@ void StencilSolver<T>::run(int iters) {
       graphs_[parity_].launch(main_.get());
       parity_ ^= 1;
     } else {
-      enqueue_block(cur_, nxt_);
+      enqueue_block(cur_, nxt_, block_);
     }
     std::swap(cur_, nxt_);
   }
-  for (int i = 0; i < rem; ++i) {
-    enqueue_single(cur_, nxt_);
+  // Remainder: one shorter super-step (S = rem <= block_ fits the ghost ring),
+  // run eagerly; a lone step takes the single-iteration path.
+  if (rem > 0) {
+    if (rem == 1) enqueue_single(cur_, nxt_);
+    else enqueue_block(cur_, nxt_, rem);
     std::swap(cur_, nxt_);
     parity_ ^= 1;  // keep the graph orientation in sync with the buffers
   }

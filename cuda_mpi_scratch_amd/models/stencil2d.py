@@ -55,9 +55,10 @@ class StencilConfig:
     loopback: bool = False           # single GPU: send self-neighbour halos through RCCL
     variant: str = "auto"            # stencil kernel variant: auto | roll | lds
     fuse_periodic: bool = True       # 1x1 periodic: fuse the self-exchange into the kernel addressing
-    # Jacobi iterations per halo exchange and per (LDS temporally blocked) launch on
-    # GPU; the ghost ring is made this deep. 1 = one exchange per iteration.
-    time_block: int = 4
+    # Jacobi iterations per halo exchange and per temporally blocked launch on GPU
+    # (wave-streaming kernel); the ghost ring is made this deep. 1 = one exchange
+    # per iteration. 12 is the measured optimum on MI355X (docs/PERF.md).
+    time_block: int = 12
     seed: int = 1234
     init: str = "random"             # random | rank
 
@@ -83,8 +84,9 @@ class Stencil2D:
         h = cfg.halo
         # Temporal blocking only for the GPU Jacobi solver and not for the reference's
         # exchange-only run (its dumps show a stencil_width/2 ghost ring).
-        self.time_block = (max(1, cfg.time_block) if (dev.type == "cuda" and cfg.kind == "jacobi5"
-                                                      and cfg.init != "rank") else 1)
+        # A ghost ring deeper than a neighbour's tile would need cells two tiles away.
+        self.time_block = (max(1, min(cfg.time_block, d.width, d.height))
+                           if (dev.type == "cuda" and cfg.kind == "jacobi5" and cfg.init != "rank") else 1)
         h = max(h, self.time_block)
         C = core()
         if dev.type == "cuda":
@@ -214,7 +216,8 @@ class Stencil2D:
         if self.solver is None:
             return "torch-p2p"
         tb = self.solver.time_block()
-        blk = f", time-blocked x{tb} (one {tb}-deep exchange + one LDS launch per {tb} iterations)" if tb > 1 else ""
+        blk = (f", time-blocked x{tb} (one {tb}-deep exchange + one wave-streaming pass per {tb} iterations)"
+               if tb > 1 else "")
         if self.solver.fused_periodic():
             return "fused-periodic (1x1 self-exchange in the kernel addressing)" + blk
         return f"{self.backend}" + (" + overlap" if self.solver.overlapped() else "") + blk

@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 def test_solver_matches_reference(gpu, backend, loopback, graph, overlap):
     w, h, iters = 300, 77, 7
     cfg = StencilConfig(global_width=w, global_height=h, dims="1x1", dtype="f32", backend=backend,
-                        loopback=loopback, graph=graph, overlap=overlap, seed=11)
+                        loopback=loopback, graph=graph, overlap=overlap, seed=11, time_block=1)
     st = Stencil2D(cfg)
     assert st.device.type == "cuda" and st.solver is not None
     st.run(iters)
@@ -89,10 +89,11 @@ def _multi_step_reference(full, steps, c0=0.2, c1=0.2):
     return u
 
 
+@pytest.mark.parametrize("variant", ["auto", "lds"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
-@pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 8])
+@pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 8, 12, 16])
 @pytest.mark.parametrize("shape", [(300, 70), (129, 33), (1024, 96)])
-def test_stencil5_tb_kernel_matches_steps(gpu, dtype, steps, shape):
+def test_stencil5_tb_kernel_matches_steps(gpu, dtype, steps, shape, variant):
     from cuda_mpi_scratch_amd import core, hip
     from cuda_mpi_scratch_amd.ops.stencil import dtype_name
 
@@ -106,7 +107,7 @@ def test_stencil5_tb_kernel_matches_steps(gpu, dtype, steps, shape):
     src = host.to(gpu)
     dst = torch.full_like(src, -3.0)
     hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, 0, w, 0, h, 0.2, 0.2, False, dtype_name(src),
-                      torch.cuda.current_stream().cuda_stream)
+                      torch.cuda.current_stream().cuda_stream, variant)
     torch.cuda.synchronize()
     got = dst.cpu().view(g.total_height(), g.pitch)[g.halo_y:g.halo_y + h, g.x_origin + g.halo_x:g.x_origin + g.halo_x + w]
     ref = _multi_step_reference(full, steps)[steps:steps + h, steps:steps + w]
@@ -115,7 +116,7 @@ def test_stencil5_tb_kernel_matches_steps(gpu, dtype, steps, shape):
 
 
 @pytest.mark.parametrize("backend,loopback", [("local", False), ("rccl", True)])
-@pytest.mark.parametrize("time_block", [2, 4, 6])
+@pytest.mark.parametrize("time_block", [2, 4, 6, 12])
 @pytest.mark.parametrize("overlap,graph", [(False, False), (True, True), (True, False)])
 def test_solver_time_blocked(gpu, backend, loopback, time_block, overlap, graph):
     w, h, iters = 264, 97, 15  # iters not a multiple of the block: remainder path too
@@ -125,12 +126,13 @@ def test_solver_time_blocked(gpu, backend, loopback, time_block, overlap, graph)
     assert st.solver.time_block() == time_block
     st.run(iters)
     st.synchronize()
+    assert st.graph_status() == ("captured" if graph else "not captured")
     ref = jacobi_reference_global(random_values(0, 0, w, h, w, 21), iters)
     assert (st.core_view().cpu() - ref).abs().max().item() < 1e-5
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
-@pytest.mark.parametrize("steps", [2, 4])
+@pytest.mark.parametrize("steps", [2, 4, 12])
 @pytest.mark.parametrize("rect", [(0, 300, 0, 4), (0, 8, 4, 66), (288, 300, 4, 66), (0, 300, 66, 70), (16, 40, 3, 50)])
 def test_stencil5_tb_kernel_strips(gpu, dtype, steps, rect):
     """Thin boundary strips (the overlap schedule's rows / columns) take their own
@@ -157,3 +159,29 @@ def test_stencil5_tb_kernel_strips(gpu, dtype, steps, rect):
     mask = torch.ones(h, w, dtype=torch.bool)
     mask[y0:y1, x0:x1] = False
     assert (got[mask] == -3.0).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("steps", [3, 8, 12, 16])
+@pytest.mark.parametrize("shape", [(264, 97), (1040, 300), (64, 40)])
+def test_stencil5_tb_wrap_matches_periodic_steps(gpu, dtype, steps, shape):
+    """Fused periodic (1x1 grid) S-step launch == S periodic Jacobi steps; covers
+    the wave-streaming kernel's wrap-around rows and columns (and the modulo path
+    of tiles narrower than one wave strip)."""
+    from cuda_mpi_scratch_amd import core, hip
+    from cuda_mpi_scratch_amd.ops.stencil import dtype_name
+
+    w, h = shape
+    g = core().TileGeom.aligned(w, h, 1, 1, torch.tensor([], dtype=dtype).element_size())
+    u = random_values(0, 0, w, h, w, steps, dtype=dtype)
+    host = torch.zeros(g.alloc_elems(), dtype=dtype)
+    host.view(g.total_height(), g.pitch)[g.halo_y:g.halo_y + h, g.x_origin + g.halo_x:g.x_origin + g.halo_x + w] = u
+    src = host.to(gpu)
+    dst = torch.zeros_like(src)
+    hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, 0, w, 0, h, 0.2, 0.2, True, dtype_name(src),
+                      torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = dst.cpu().view(g.total_height(), g.pitch)[g.halo_y:g.halo_y + h, g.x_origin + g.halo_x:g.x_origin + g.halo_x + w]
+    ref = jacobi_reference_global(u, steps)
+    tol = 2e-6 if dtype == torch.float32 else 1e-14
+    assert (got.double() - ref.double()).abs().max().item() <= tol
