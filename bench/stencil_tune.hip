@@ -77,15 +77,16 @@ Variant tb1(const float* in, float* out, const TileGeom& g) {
 
 // tmp: scratch tile for the two-pass reference of S > 8 (wrap only: two periodic
 // half-blocks equal one block; without wrap the frozen ghost ring differs).
-template <int S, int PF, bool WRAP = false, bool SKEW = true>
+template <int S, int PF, bool WRAP = false, bool SKEW = true, bool DPP = true>
 Variant stream(const float* in, float* out, const TileGeom& g, int ch, float* tmp = nullptr) {
   char buf[128];
-  std::snprintf(buf, sizeof(buf), "stream_s%d_pf%d_ch%d%s%s", S, PF, ch, WRAP ? "_wrap" : "", SKEW ? "" : "_chain");
+  std::snprintf(buf, sizeof(buf), "stream_s%d_pf%d_ch%d%s%s%s", S, PF, ch, WRAP ? "_wrap" : "", SKEW ? "" : "_chain",
+                DPP ? "" : "_bperm");
   Variant v{buf, [=](hipStream_t s) {
               constexpr int OW = StreamShape<float, S>::OW;
               const index_t strips = (g.width + OW - 1) / OW;
               const dim3 grid(unsigned((strips + 3) / 4), unsigned((g.height + ch - 1) / ch));
-              stencil5_stream_kernel<float, S, PF, WRAP, SKEW><<<grid, 256, 0, s>>>(
+              stencil5_stream_kernel<float, S, PF, WRAP, SKEW, DPP><<<grid, 256, 0, s>>>(
                   in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, index_t(ch), 0.2f,
                   0.2f);
             }};
@@ -137,19 +138,15 @@ int main(int argc, char** argv) {
   vs.push_back(tb1<4, 192, 24, false>(in, out, g));
   vs.push_back(tb1<6, 128, 32, false>(in, out, g));
   float* tmp = c.get();
-  vs.push_back(stream<8, 3, false, false>(in, out, g, 256));
-  vs.push_back(stream<12, 3, true, false>(in, out, g, 256, tmp));
   for (int ch : {64, 128, 256, 512}) {
-    vs.push_back(stream<4, 3>(in, out, g, ch));
     vs.push_back(stream<8, 3>(in, out, g, ch));
+    vs.push_back(stream<8, 3, false, true, false>(in, out, g, ch));
     vs.push_back(stream<12, 3>(in, out, g, ch));
-    vs.push_back(stream<16, 3>(in, out, g, ch));
-    vs.push_back(stream<8, 3, true>(in, out, g, ch));
+    vs.push_back(stream<12, 3, false, true, false>(in, out, g, ch));
     vs.push_back(stream<12, 3, true>(in, out, g, ch, tmp));
+    vs.push_back(stream<12, 3, true, true, false>(in, out, g, ch, tmp));
     vs.push_back(stream<16, 3, true>(in, out, g, ch, tmp));
   }
-  vs.push_back(stream<8, 6>(in, out, g, 256));
-  vs.push_back(stream<12, 6>(in, out, g, 256));
 
   Stream st;
   Event e0(true), e1(true);

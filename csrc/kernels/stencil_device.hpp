@@ -574,6 +574,37 @@ __device__ __forceinline__ double lane_fetch<double>(double v, int a) {
   return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
 
+// Whole-wavefront DPP shifts (CDNA keeps the GFX9 wave_shr / wave_shl controls):
+// lane i reads lane i-1 (kDppWaveShr1) or lane i+1 (kDppWaveShl1); the shifted-in
+// lane gets 0. As a DPP source modifier the shift folds into the consuming
+// v_add_f32, so a column neighbour costs no instruction and no LDS round trip.
+constexpr int kDppWaveShl1 = 0x130;
+constexpr int kDppWaveShr1 = 0x138;
+template <typename T, int CTRL>
+__device__ __forceinline__ T lane_shift(T v);
+template <>
+__device__ __forceinline__ float lane_shift<float, kDppWaveShr1>(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kDppWaveShr1, 0xf, 0xf, true));
+}
+template <>
+__device__ __forceinline__ float lane_shift<float, kDppWaveShl1>(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kDppWaveShl1, 0xf, 0xf, true));
+}
+template <>
+__device__ __forceinline__ double lane_shift<double, kDppWaveShr1>(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(b & 0xffffffff), kDppWaveShr1, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), kDppWaveShr1, 0xf, 0xf, false);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+template <>
+__device__ __forceinline__ double lane_shift<double, kDppWaveShl1>(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(b & 0xffffffff), kDppWaveShl1, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), kDppWaveShl1, 0xf, 0xf, false);
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+
 template <typename T, int S>
 struct StreamShape {
   static constexpr int N = Vec16<T>::N;
@@ -583,7 +614,7 @@ struct StreamShape {
 
 // Workgroup = 4 waves on 4 adjacent strips of the same row chunk. PF = input
 // rows in flight per wave (a register ring, statically indexed; multiple of 3).
-template <typename T, int S, int PF, bool WRAP, bool SKEW = true>
+template <typename T, int S, int PF, bool WRAP, bool SKEW = true, bool DPP = true>
 __global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                  index_t pitch, index_t core_off, index_t W, index_t H,
                                                                  index_t x_begin, index_t x_end, index_t y_begin,
@@ -660,8 +691,8 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __rest
 #pragma unroll
           for (int l = S - 1; l >= 0; --l) {
             const V m = win[p1][l];
-            const T left = lane_fetch<T>(m[N - 1], addr_l);
-            const T right = lane_fetch<T>(m[0], addr_r);
+            const T left = DPP ? lane_shift<T, kDppWaveShr1>(m[N - 1]) : lane_fetch<T>(m[N - 1], addr_l);
+            const T right = DPP ? lane_shift<T, kDppWaveShl1>(m[0]) : lane_fetch<T>(m[0], addr_r);
             const V o = jac_row<T, V>(win[p0][l], m, win[p2][l], left, right, c0, c1);
             if (l == S - 1) top = o;
             else win[p0][l + 1] = o;
