@@ -66,6 +66,8 @@ def main(argv=None) -> int:
     p.add_argument("--variant", default="auto", choices=["auto", "roll", "lds"])
     p.add_argument("--time-block", type=int, default=12, help="Jacobi steps per halo exchange / kernel pass")
     p.add_argument("--no-overlap", action="store_true")
+    p.add_argument("--loopback", action="store_true",
+                   help="1 GPU: route the self-neighbour halos through RCCL (exercises the multi-GPU schedule)")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-extras", action="store_true")
     args = p.parse_args(argv)
@@ -82,7 +84,7 @@ def main(argv=None) -> int:
     gw, gh = (int(v) for v in args.global_.lower().split("x"))
     cfg = StencilConfig(global_width=gw, global_height=gh, dims=f"{rows}x{cols}", dtype=args.dtype,
                         kind="jacobi5", backend="auto", overlap=not args.no_overlap, graph=not args.no_graph,
-                        variant=args.variant, time_block=args.time_block)
+                        variant=args.variant, time_block=args.time_block, loopback=args.loopback)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup)
     value = st.cells_per_step * args.steps / dt / 1e9

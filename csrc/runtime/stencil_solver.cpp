@@ -82,6 +82,25 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
     return;
   }
   const index_t d = std::max(radius_, S);  // dependency depth of the super-step
+  constexpr index_t N = 16 / index_t(sizeof(T));
+  // Temporally blocked Jacobi: the kernels take any vector-aligned column range,
+  // so the interior skips the edge columns and the four boundary strips run on
+  // the main stream as soon as the halo has landed, concurrently with the
+  // interior (disjoint outputs), instead of after it.
+  const index_t dl = (d + N - 1) / N * N, dr = (w - d) / N * N;
+  if (S > 1 && cfg_.kind == StencilKind::Jacobi5 && dl < dr) {
+    fork_.record(m);
+    fork_.wait_on(side);
+    update(cur, nxt, S, dl, dr, d, h - d, side);
+    interior_.record(side);
+    ex_->exchange(cur, m);
+    update(cur, nxt, S, 0, w, 0, d, m);
+    update(cur, nxt, S, 0, w, h - d, h, m);
+    update(cur, nxt, S, 0, dl, d, h - d, m);
+    update(cur, nxt, S, dr, w, d, h - d, m);
+    interior_.wait_on(m);
+    return;
+  }
   fork_.record(m);
   fork_.wait_on(side);
   update(cur, nxt, S, 0, w, d, h - d, side);  // interior (its edge columns are redone below)
@@ -93,8 +112,7 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
   // Column strips; the temporally blocked kernel needs a vector-aligned start, so
   // the right strip may start a few (interior) columns early: recomputing those
   // reproduces the same values.
-  constexpr index_t N = 16 / index_t(sizeof(T));
-  const index_t right0 = S > 1 ? ((w - d) / N) * N : w - d;
+  const index_t right0 = S > 1 ? dr : w - d;
   update(cur, nxt, S, 0, d, d, h - d, m);
   update(cur, nxt, S, right0, w, d, h - d, m);
 }
