@@ -18,7 +18,9 @@
 // More options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
 // --iters N, --warmup N, --time-block S (default 12 on timed runs), --no-overlap, --no-graph,
 // --loopback, --bind bunch|rrobin,
-// --dump / --no-dump, --checksum, --non-periodic, --seed S, --json FILE.
+// --dump / --no-dump, --checksum, --non-periodic, --seed S, --json FILE,
+// --checkpoint FILE / --resume FILE (collective MPI-IO global grid file, any
+// decomposition; same format as stencil2d_cpu and the Python package).
 #include <mpi.h>
 
 #include <algorithm>
@@ -30,6 +32,7 @@
 #include <vector>
 
 #include "app_common.hpp"
+#include "mxs/comm/mpi_checkpoint.hpp"
 #include "mxs/comm/mpi_env.hpp"
 #include "mxs/comm/mpi_halo.hpp"
 #include "mxs/comm/rccl_comm.hpp"
@@ -130,8 +133,17 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   } else {
     kernels::fill<T>(a.get(), g.alloc_elems(), T(0), init_stream.get());
     kernels::fill<T>(b.get(), g.alloc_elems(), T(0), init_stream.get());
-    kernels::fill_random<T>(a.get(), g, gx0, gy0, gw, std::uint64_t(cli.get_int("seed", 1234)), T(0), T(1),
-                            init_stream.get());
+    const std::uint64_t seed = std::uint64_t(cli.get_int("seed", 1234));
+    const GlobalBlock blk{gx0, gy0, gw, gh};
+    std::int64_t start_iter = 0;
+    if (cli.has("resume")) {
+      std::vector<T> h(size_t(g.alloc_elems()), T(0));
+      start_iter = read_grid_file<T>(MPI_COMM_WORLD, cli.get("resume"), h.data(), g, blk).iteration;
+      MXS_HIP_CHECK(hipMemcpy(a.get(), h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+      if (rank == 0) std::cout << "resumed from " << cli.get("resume") << " at iteration " << start_iter << '\n';
+    } else {
+      kernels::fill_random<T>(a.get(), g, gx0, gy0, gw, seed, T(0), T(1), init_stream.get());
+    }
     init_stream.sync();
     T* cur = a.get();
     T* nxt = b.get();
@@ -160,6 +172,11 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
     env.barrier();
     const double dt = env.max_over_ranks(MPI_Wtime() - t0);
     if (solver) cur = solver->current();
+    if (cli.has("checkpoint")) {
+      std::vector<T> h;
+      copy_tile_to_host(h, cur, g);
+      write_grid_file<T>(MPI_COMM_WORLD, cli.get("checkpoint"), h.data(), g, blk, start_iter + warmup + iters, seed);
+    }
     const double gcells = double(gw) * double(gh) * double(iters) / dt / 1e9;
     double checksum = std::nan("");
     const bool want_sum = cli.has("checksum") ? cli.flag("checksum") : (lw * lh <= (index_t(1) << 24));

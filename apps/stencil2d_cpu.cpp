@@ -10,7 +10,9 @@
 // Options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
 // --iters N (0 = one exchange, reference behaviour), --warmup N, --dump / --no-dump,
 // --non-periodic, --strict-square (reproduce the reference's perfect-square check),
-// --seed S, --json FILE.
+// --seed S, --json FILE, --checkpoint FILE (collective MPI-IO global grid file
+// after the last iteration), --resume FILE (start from such a file, any
+// decomposition).
 #include <mpi.h>
 
 #include <chrono>
@@ -21,6 +23,7 @@
 #include <vector>
 
 #include "app_common.hpp"
+#include "mxs/comm/mpi_checkpoint.hpp"
 #include "mxs/comm/mpi_env.hpp"
 #include "mxs/comm/mpi_host_halo.hpp"
 #include "mxs/core/cli.hpp"
@@ -62,7 +65,16 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, index_t lw, index
     }
   } else {
     MXS_CHECK(sw >= 3 && sh >= 3, "--iters needs a stencil of width >= 3 (ghost ring >= 1)");
-    fill_random_host<T>(a.data(), g, gx0, gy0, gw, std::uint64_t(cli.get_int("seed", 1234)));
+    const std::uint64_t seed = std::uint64_t(cli.get_int("seed", 1234));
+    const GlobalBlock blk{gx0, gy0, gw, gh};
+    std::int64_t start_iter = 0;
+    if (cli.has("resume")) {
+      const GridFileHeader hdr = read_grid_file<T>(MPI_COMM_WORLD, cli.get("resume"), a.data(), g, blk);
+      start_iter = hdr.iteration;
+      if (rank == 0) std::cout << "resumed from " << cli.get("resume") << " at iteration " << start_iter << '\n';
+    } else {
+      fill_random_host<T>(a.data(), g, gx0, gy0, gw, seed);
+    }
     const T c0 = T(cli.get_double("c-center", 0.2)), c1 = T(cli.get_double("c-neighbor", 0.2));
     T* cur = a.data();
     T* nxt = b.data();
@@ -94,6 +106,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, index_t lw, index
                 << std::endl;
       app::append_json(cli.get("json"), js.str());
     }
+    if (cli.has("checkpoint")) write_grid_file<T>(MPI_COMM_WORLD, cli.get("checkpoint"), cur, g, blk, start_iter + iters, seed);
     if (dump) {
       std::ofstream f(dump_file_name(topo, rank));
       write_dump_header(f, topo, rank, -1, lw, lh, sw, sh, "");

@@ -97,6 +97,7 @@ class Stencil2D:
         self.a = torch.empty(n, dtype=self.dtype, device=dev)
         self.b = torch.empty(n, dtype=self.dtype, device=dev)
         self._init_data()
+        self.iteration = 0  # Jacobi iterations applied to the field (checkpoint header)
 
         backend = cfg.backend
         if dev.type != "cuda":
@@ -144,6 +145,7 @@ class Stencil2D:
     def run(self, iters: int):
         if iters <= 0:
             return
+        self.iteration += iters
         if self.solver is not None:
             self.solver.run(iters)
             return
@@ -203,6 +205,19 @@ class Stencil2D:
         for x0, y0, t in parts:
             out[y0:y0 + t.shape[0], x0:x0 + t.shape[1]] = t
         return out
+
+    def save_checkpoint(self, path: str):
+        """Collective: write the global field to one decomposition-independent
+        grid file (format shared with the C++ apps' --checkpoint)."""
+        from ..utils import checkpoint
+
+        return checkpoint.save(self, path)
+
+    def load_checkpoint(self, path: str):
+        """Collective: resume from a grid file written by any decomposition."""
+        from ..utils import checkpoint
+
+        return checkpoint.load(self, path)
 
     @property
     def cells_per_step(self) -> int:
@@ -269,6 +284,10 @@ def main(argv=None) -> int:
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--loopback", action="store_true")
     p.add_argument("--variant", default="auto", choices=["auto", "roll", "lds"])
+    p.add_argument("--time-block", type=int, default=StencilConfig.time_block)
+    p.add_argument("--seed", type=int, default=StencilConfig.seed)
+    p.add_argument("--checkpoint", default=None, help="write the final field to this grid file")
+    p.add_argument("--resume", default=None, help="start from this grid file (any decomposition)")
     p.add_argument("--json", default=None)
     args = p.parse_args(argv)
     ctx = dist_init()
@@ -280,8 +299,13 @@ def main(argv=None) -> int:
         gw, gh = _parse_wh(args.global_ or "8192x8192")
     cfg = StencilConfig(global_width=gw, global_height=gh, dims=f"{rows}x{cols}", dtype=args.dtype,
                         backend=args.backend, overlap=not args.no_overlap, graph=not args.no_graph,
-                        loopback=args.loopback, variant=args.variant)
+                        loopback=args.loopback, variant=args.variant, time_block=args.time_block,
+                        seed=args.seed)
     st = Stencil2D(cfg, ctx)
+    if args.resume:
+        hdr = st.load_checkpoint(args.resume)
+        if ctx.is_root:
+            print(f"resumed from {args.resume} at iteration {hdr.iteration}", file=sys.stderr)
     st.run(args.warmup)
     st.synchronize()
     ctx.barrier()
@@ -293,7 +317,9 @@ def main(argv=None) -> int:
     gcells = st.cells_per_step * args.iters / dt / 1e9
     rec = {"metric": "stencil2d_gcells_per_s", "value": gcells, "ms_per_iter": dt / args.iters * 1e3,
            "ranks": ctx.world_size, "dims": f"{rows}x{cols}", "config": asdict(cfg), "backend": st.backend,
-           "graph": st.graph_status()}
+           "graph": st.graph_status(), "iteration": st.iteration}
+    if args.checkpoint:
+        st.save_checkpoint(args.checkpoint)
     if ctx.is_root:
         print(json.dumps(rec))
         if args.json:

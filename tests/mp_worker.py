@@ -43,6 +43,25 @@ def task_jacobi(args):
     return out
 
 
+def task_checkpoint(args):
+    """Run `iters` iterations, optionally resuming from / saving to a grid file."""
+    ctx = init(backend="gloo", device="cpu")
+    cfg = StencilConfig(global_width=args["w"], global_height=args["h"], dims=args["dims"],
+                        dtype=args.get("dtype", "f64"), seed=args.get("seed", 5))
+    st = Stencil2D(cfg, ctx, device="cpu")
+    if args.get("resume"):
+        st.load_checkpoint(args["resume"])
+    st.run(args["iters"])
+    if args.get("save"):
+        st.save_checkpoint(args["save"])
+    g = st.gather_global()
+    ctx.destroy()
+    out = {"rank": ctx.rank, "iteration": st.iteration}
+    if ctx.rank == 0:
+        out["grid"] = g.double().tolist()
+    return out
+
+
 def task_halo_property(args):
     """Non-square tiles and grids: after one exchange every ghost cell holds the
     owning neighbour's core value (cell value = global linear index)."""

@@ -74,6 +74,20 @@ def test_stencil_gpu_time_block_matches_cpu_app(gpu, tmp_path, extra):
     assert abs(a - b) <= 1e-9 * abs(b)
 
 
+def test_stencil_gpu_checkpoint_resume_matches_cpu(gpu, tmp_path):
+    """GPU app: 5 iterations + checkpoint, resume + 7 (time-blocked) == 12 CPU iterations, bitwise."""
+    common = ["--global", "200x72", "--dims", "1x1", "--dtype", "f64", "--stencil", "3", "--warmup", "0"]
+    a, b, c = (str(tmp_path / n) for n in ("a.bin", "b.bin", "c.bin"))
+    r = mpirun(1, "stencil2d", *common, "--iters", "5", "--checkpoint", a, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = mpirun(1, "stencil2d", *common, "--iters", "7", "--resume", a, "--checkpoint", b, cwd=tmp_path)
+    assert r.returncode == 0 and "at iteration 5" in r.stdout, r.stderr[-3000:]
+    r = subprocess.run([MPIEXEC, "-n", "1", os.path.join(BIN, "stencil2d_cpu"), *common[:-2], "--iters", "12",
+                        "--checkpoint", c], capture_output=True, text=True, timeout=120, cwd=tmp_path)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert open(b, "rb").read() == open(c, "rb").read()
+
+
 def test_stencil_gpu_timed_run_reports_rate(gpu, tmp_path):
     r = mpirun(1, "stencil2d", "--global", "4096x4096", "--dtype", "f32", "--iters", "50", "--stencil", "3",
                cwd=tmp_path)
