@@ -20,7 +20,9 @@
 // --loopback, --bind bunch|rrobin,
 // --dump / --no-dump, --checksum, --non-periodic, --seed S, --json FILE,
 // --checkpoint FILE / --resume FILE (collective MPI-IO global grid file, any
-// decomposition; same format as stencil2d_cpu and the Python package).
+// decomposition; same format as stencil2d_cpu and the Python package),
+// --comm-timeout SECONDS (halo watchdog, default 300), --fault-inject
+// RANK:ITER[:exit|hang|error] (failure-path testing).
 #include <mpi.h>
 
 #include <algorithm>
@@ -147,12 +149,19 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
     init_stream.sync();
     T* cur = a.get();
     T* nxt = b.get();
+    const FaultSpec fault = parse_fault_spec(cli.get("fault-inject", ""));
+    long long it = 0;
     auto steps = [&](long long n) {
-      if (solver) {
+      if (solver && !fault.armed()) {
         solver->run(int(n));
         return;
       }
       for (long long i = 0; i < n; ++i) {
+        maybe_inject_fault(fault, rank, it++);
+        if (solver) {
+          solver->run(1);
+          continue;
+        }
         staged->exchange(cur, init_stream.get());
         kernels::stencil5_rows<T>(cur, nxt, g, 0, lh, cfg.coeffs, init_stream.get());
         std::swap(cur, nxt);
@@ -216,6 +225,7 @@ int main(int argc, char** argv) {
   MpiEnv env(&argc, &argv);
   Cli cli(argc, argv, {"dump", "no-dump", "non-periodic", "strict-square", "no-overlap", "no-graph", "loopback",
                        "pageable", "checksum"});
+  comm_timeout() = cli.get_double("comm-timeout", 300.0);
   const DeviceBinding dev = bind_device(env, cli.get("bind", "bunch"));
   const int n = env.size();
   int rows, cols;

@@ -12,7 +12,8 @@
 // --non-periodic, --strict-square (reproduce the reference's perfect-square check),
 // --seed S, --json FILE, --checkpoint FILE (collective MPI-IO global grid file
 // after the last iteration), --resume FILE (start from such a file, any
-// decomposition).
+// decomposition), --comm-timeout SECONDS (halo watchdog), --fault-inject
+// RANK:ITER[:exit|hang|error] (failure-path testing).
 #include <mpi.h>
 
 #include <chrono>
@@ -78,7 +79,10 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, index_t lw, index
     const T c0 = T(cli.get_double("c-center", 0.2)), c1 = T(cli.get_double("c-neighbor", 0.2));
     T* cur = a.data();
     T* nxt = b.data();
+    const FaultSpec fault = parse_fault_spec(cli.get("fault-inject", ""));
+    long long it = 0;
     auto step = [&]() {
+      maybe_inject_fault(fault, rank, it++);
       halo.exchange(cur);
       jacobi5_host<T>(cur, nxt, g, 0, lh, c0, c1);
       std::swap(cur, nxt);
@@ -121,6 +125,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, index_t lw, index
 int main(int argc, char** argv) {
   MpiEnv env(&argc, &argv);
   Cli cli(argc, argv, {"dump", "no-dump", "non-periodic", "strict-square"});
+  comm_timeout() = cli.get_double("comm-timeout", 0.0);
   const int n = env.size();
   // Process grid: the reference's sqrt(N) x sqrt(N) when N is a perfect square,
   // otherwise MPI_Dims_create (the reference refused).

@@ -14,8 +14,10 @@
 #include <cstdlib>
 #include <sstream>
 #include <string>
+#include <vector>
 
 #include "mxs/core/error.hpp"
+#include "mxs/core/fault.hpp"
 
 namespace mxs {
 
@@ -41,6 +43,24 @@ inline void mpi_check(int code, const char* expr, const char* file, int line) {
 }
 
 #define MXS_MPI_CHECK(expr) ::mxs::mpi_check((expr), #expr, __FILE__, __LINE__)
+
+// MPI_Waitall under the communication watchdog (mxs/core/fault.hpp): with a
+// comm_timeout() set, polls MPI_Testall and fails after the timeout instead of
+// blocking forever on a dead or hung peer.
+inline void mpi_wait_all(std::vector<MPI_Request>& req, const char* what) {
+  if (req.empty()) return;
+  if (comm_timeout() <= 0) {
+    MXS_MPI_CHECK(MPI_Waitall(int(req.size()), req.data(), MPI_STATUSES_IGNORE));
+    return;
+  }
+  wait_with_timeout(
+      [&] {
+        int flag = 0;
+        MXS_MPI_CHECK(MPI_Testall(int(req.size()), req.data(), &flag, MPI_STATUSES_IGNORE));
+        return flag != 0;
+      },
+      what, [] {});
+}
 
 enum class MpiErrors { Abort, Throw };
 

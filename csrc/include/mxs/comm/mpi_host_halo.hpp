@@ -48,7 +48,7 @@ class MpiHostHalo {
     size_t k = 0;
     for (auto& r : recvs_) MXS_MPI_CHECK(MPI_Irecv(tile, 1, r.type.get(), r.peer, r.tag, comm_, &req[k++]));
     for (auto& s : sends_) MXS_MPI_CHECK(MPI_Isend(tile, 1, s.type.get(), s.peer, s.tag, comm_, &req[k++]));
-    MXS_MPI_CHECK(MPI_Waitall(int(req.size()), req.data(), MPI_STATUSES_IGNORE));
+    mpi_wait_all(req, "halo exchange (MPI)");
   }
   int messages_per_exchange() const { return int(sends_.size() + recvs_.size()); }
 

@@ -59,6 +59,10 @@ class RcclComm {
   bool healthy(std::string* msg = nullptr) const;
   // Tear the communicator down without waiting for peers (after a failure).
   void abort();
+  // Wait for `stream` under the communication watchdog (mxs/core/fault.hpp):
+  // fails on an RCCL async error, or after comm_timeout() seconds (the
+  // communicator is aborted first so the error path cannot block on it).
+  void wait(hipStream_t stream, const char* what) const;
 
   // Sum-allreduce `count` elements in place or out of place on `stream`.
   template <typename T>

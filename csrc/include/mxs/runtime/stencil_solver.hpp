@@ -99,6 +99,7 @@ class StencilSolver {
   int radius_ = 1;
   T* cur_;
   T* nxt_;
+  const RcclComm* comm_ = nullptr;  // watchdog waits (synchronize) when set
   std::unique_ptr<HaloExchanger<T>> ex_;
   Stream main_, side_;
   Event fork_, interior_;

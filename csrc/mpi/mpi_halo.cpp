@@ -33,7 +33,7 @@ void MpiStagedHalo<T>::exchange(T* tile, hipStream_t stream) {
     MXS_MPI_CHECK(MPI_Irecv(hrecv_ + m.offset, int(m.count * sizeof(T)), MPI_BYTE, m.peer, 0, comm_, &req[k++]));
   for (const auto& m : plan_.sends)
     MXS_MPI_CHECK(MPI_Isend(hsend_ + m.offset, int(m.count * sizeof(T)), MPI_BYTE, m.peer, 0, comm_, &req[k++]));
-  MXS_MPI_CHECK(MPI_Waitall(int(req.size()), req.data(), MPI_STATUSES_IGNORE));
+  mpi_wait_all(req, "halo exchange (MPI staged)");
   MXS_HIP_CHECK(hipMemcpyAsync(drecv_.get(), hrecv_, size_t(plan_.recv_elems) * sizeof(T), hipMemcpyHostToDevice,
                                stream));
   kernels::copy2d_batch<T>(tile, dsend_.get(), drecv_.get(), progs_.unpack, stream);

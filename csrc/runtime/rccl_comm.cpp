@@ -2,6 +2,8 @@
 
 #include <cstring>
 
+#include "mxs/core/fault.hpp"
+
 namespace mxs {
 
 std::string RcclComm::make_unique_id() {
@@ -31,6 +33,19 @@ bool RcclComm::healthy(std::string* msg) const {
     return false;
   }
   return true;
+}
+
+void RcclComm::wait(hipStream_t stream, const char* what) const {
+  wait_with_timeout(
+      [&] {
+        const hipError_t q = hipStreamQuery(stream);
+        if (q == hipSuccess) return true;
+        if (q != hipErrorNotReady) MXS_HIP_CHECK(q);
+        std::string msg;
+        if (!healthy(&msg)) raise_error(std::string(what) + ": RCCL communicator failed: " + msg);
+        return false;
+      },
+      what, [&] { (void)ncclCommAbort(comm_); });
 }
 
 void RcclComm::abort() {

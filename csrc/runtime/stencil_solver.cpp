@@ -3,12 +3,14 @@
 #include <algorithm>
 #include <utility>
 
+#include "mxs/core/fault.hpp"
+
 namespace mxs {
 
 template <typename T>
 StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGeom& tile, T* buf_a, T* buf_b,
                                 const RcclComm* comm, const SolverConfig& cfg)
-    : tile_(tile), cfg_(cfg), cur_(buf_a), nxt_(buf_b), main_(true, -1), side_(true, 0) {
+    : tile_(tile), cfg_(cfg), cur_(buf_a), nxt_(buf_b), comm_(comm), main_(true, -1), side_(true, 0) {
   // The main stream gets the higher priority (lower number): its short pack /
   // unpack / boundary launches should not queue behind the long interior sweep.
   block_ = cfg_.kind == StencilKind::Jacobi5 ? std::max(1, cfg_.time_block) : 1;
@@ -191,6 +193,9 @@ void StencilSolver<T>::exchange_only() {
 
 template <typename T>
 void StencilSolver<T>::synchronize() {
+  // With a remote peer and a watchdog timeout, wait by polling so a dead or
+  // hung peer fails the job instead of blocking it.
+  if (comm_ && comm_timeout() > 0) comm_->wait(main_.get(), "stencil halo exchange (RCCL)");
   main_.sync();
   side_.sync();
 }

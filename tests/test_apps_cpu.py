@@ -155,3 +155,24 @@ def test_dot_app_float_accumulator_saturates_on_cpu():
     assert "dot product result: 6.71089e+07" in r.stdout
     r = mpirun(4, "dot", "--device", "cpu", "--reps", "1")
     assert "dot product result: 2.68435e+08" in r.stdout
+
+
+@pytest.mark.parametrize("mode,expect", [("hang", "timed out after"), ("exit", "[fault-inject] rank 1"),
+                                         ("error", "injected error")])
+def test_fault_injection_ends_the_job(tmp_path, mode, expect):
+    """a hung, dead or failing rank ends the whole job (watchdog ->
+    MPI_Abort), it never leaves the peers blocked."""
+    import time
+
+    t0 = time.time()
+    r = mpirun(2, "stencil2d_cpu", "--global", "64x64", "--iters", "50", "--stencil", "3",
+               "--fault-inject", f"1:10:{mode}", "--comm-timeout", "2", cwd=tmp_path, timeout=90)
+    assert r.returncode != 0
+    assert expect in r.stdout + r.stderr
+    assert time.time() - t0 < 60
+
+
+def test_comm_timeout_does_not_fire_on_healthy_run(tmp_path):
+    r = mpirun(4, "stencil2d_cpu", "--global", "64x48", "--iters", "20", "--stencil", "3", "--comm-timeout", "5",
+               cwd=tmp_path)
+    assert r.returncode == 0, r.stderr

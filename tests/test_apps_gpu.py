@@ -120,3 +120,12 @@ def test_dot_atomics(gpu):
     r = subprocess.run([os.path.join(BIN, "dot_atomics")], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0
     assert "GPU: 1024" in r.stdout and "CPU: 1024" in r.stdout
+
+
+def test_stencil_gpu_fault_injection_hang_is_detected(gpu, tmp_path):
+    """A hung rank on the GPU path (mpi-staged, 2 ranks on one GPU): the peer's
+    watchdog fires and MPI_Abort ends the job."""
+    r = mpirun(2, "stencil2d", "--global", "256x128", "--dtype", "f32", "--iters", "40", "--stencil", "3",
+               "--warmup", "0", "--fault-inject", "1:5:hang", "--comm-timeout", "3", cwd=tmp_path, timeout=120)
+    assert r.returncode != 0
+    assert "timed out after" in r.stdout + r.stderr
