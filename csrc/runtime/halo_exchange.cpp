@@ -1,4 +1,5 @@
 #include "mxs/halo/exchange.hpp"
+#include "mxs/core/trace.hpp"
 
 namespace mxs {
 
@@ -67,12 +68,14 @@ HaloExchanger<T>::HaloExchanger(const HaloPlan& plan, HaloBackend backend, const
 
 template <typename T>
 void HaloExchanger<T>::pack(T* tile, hipStream_t stream) {
+  MXS_TRACE_RANGE("halo.pack");
   kernels::copy2d_batch<T>(tile, send_.get(), recv_.get(), progs_.pack, stream);
 }
 
 template <typename T>
 void HaloExchanger<T>::transfer(hipStream_t stream) {
   if (plan_.sends.empty()) return;
+  MXS_TRACE_RANGE("halo.rccl_sendrecv");
   comm_->group_start();
   for (const auto& m : plan_.recvs) comm_->recv<T>(recv_.get() + m.offset, size_t(m.count), m.peer, stream);
   for (const auto& m : plan_.sends) comm_->send<T>(send_.get() + m.offset, size_t(m.count), m.peer, stream);
@@ -81,11 +84,13 @@ void HaloExchanger<T>::transfer(hipStream_t stream) {
 
 template <typename T>
 void HaloExchanger<T>::unpack(T* tile, hipStream_t stream) {
+  MXS_TRACE_RANGE("halo.unpack");
   kernels::copy2d_batch<T>(tile, send_.get(), recv_.get(), progs_.unpack, stream);
 }
 
 template <typename T>
 void HaloExchanger<T>::exchange(T* tile, hipStream_t stream) {
+  MXS_TRACE_RANGE("halo.exchange");
   pack(tile, stream);
   transfer(stream);
   unpack(tile, stream);

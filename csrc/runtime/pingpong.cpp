@@ -6,6 +6,7 @@
 #include <chrono>
 #include <vector>
 
+#include "mxs/core/trace.hpp"
 #include "mxs/runtime/hip_utils.hpp"
 
 namespace mxs {
@@ -59,6 +60,7 @@ void round_trip(const RcclComm& comm, int peer, void* sendbuf, void* recvbuf, si
 
 PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void* recvbuf, size_t bytes, int warmup,
                             int reps, PingPongMode mode, hipStream_t stream) {
+  MXS_TRACE_RANGE("pingpong.rccl");
   PingPongStats st;
   st.bytes = bytes;
   MXS_CHECK(peer >= 0 && peer < comm.size(), "pingpong: bad peer " << peer);
@@ -143,6 +145,7 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
 
 PingPongStats pingpong_local(LocalPath path, void* dbuf_a, void* dbuf_b, size_t bytes, int warmup, int reps,
                              hipStream_t stream) {
+  MXS_TRACE_RANGE("pingpong.local");
   PingPongStats st;
   st.bytes = bytes;
   std::vector<unsigned char> pattern(bytes);

@@ -4,6 +4,7 @@
 #include <utility>
 
 #include "mxs/core/fault.hpp"
+#include "mxs/core/trace.hpp"
 
 namespace mxs {
 
@@ -71,6 +72,7 @@ void StencilSolver<T>::enqueue_single(T* cur, T* nxt) {
 // stream: captured from a forked stream, RCCL (ROCm 7.x) crashes at capture.
 template <typename T>
 void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
+  MXS_TRACE_RANGE("stencil.superstep");
   const index_t h = tile_.height, w = tile_.width;
   hipStream_t m = main_.get(), side = side_.get();
   if (fused_) {
@@ -121,6 +123,7 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
 
 template <typename T>
 bool StencilSolver<T>::try_capture() {
+  MXS_TRACE_RANGE("stencil.graph_capture");
   graph_tried_ = true;
   // One graph per orientation: graphs_[0] = cur->nxt, graphs_[1] = nxt->cur.
   for (int k = 0; k < 2; ++k) {
@@ -160,10 +163,12 @@ bool StencilSolver<T>::try_capture() {
 
 template <typename T>
 void StencilSolver<T>::run(int iters) {
+  MXS_TRACE_RANGE("stencil.run");
   const int supers = iters / block_, rem = iters % block_;
   for (int i = 0; i < supers; ++i) {
     if (cfg_.use_graph && !graph_tried_) try_capture();
     if (graphs_[0].valid()) {
+      MXS_TRACE_RANGE("stencil.graph_launch");
       graphs_[parity_].launch(main_.get());
       parity_ ^= 1;
     } else {
