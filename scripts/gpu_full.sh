@@ -10,7 +10,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -1 gpurun_out/smoke.log
 timeout -k 10 300 python bench.py > gpurun_out/bench.log 2>&1 || { echo bench failed; tail -30 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_bench" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 50 --warmup 5 --no-extras > gpurun_out/prof_bench.log 2>&1
-echo "rocprof rc=$?"
+bash scripts/profile.sh bench python3 "$GRAFT_REPO_ROOT/bench.py" --steps 48 --warmup 12 --no-extras > gpurun_out/prof_bench.log 2>&1
+echo "profile rc=$?"
 [ -n "$WITH_TUNE" ] && { TUNE_TAG=$WITH_TUNE bash scripts/gpu_tune.sh || exit 1; }
 exit 0

@@ -28,21 +28,13 @@ def main(d: str) -> int:
             name = name if len(name) < 110 else name[:107] + "..."
             print(f"| `{name}` | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
                   f"{float(r['AverageNs']) / 1e3:.1f} | {100 * float(r['TotalDurationNs']) / total:.1f} |")
-    mk = _rows(os.path.join(d, "**", "*marker_api_trace.csv"))
+    mk = _rows(os.path.join(d, "**", "*marker_api_stats.csv"))
     if mk:
-        agg = defaultdict(lambda: [0, 0.0])
-        for r in mk:
-            msg = r.get("Message") or r.get("Operation") or "?"
-            try:
-                dt = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
-            except (KeyError, ValueError):
-                continue
-            agg[msg][0] += 1
-            agg[msg][1] += dt
-        print("\n| roctx range | count | total ms (host) |")
-        print("|---|---:|---:|")
-        for k, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-            print(f"| {k} | {n} | {t / 1e6:.3f} |")
+        print("\n| roctx range | count | total ms (host) | avg us |")
+        print("|---|---:|---:|---:|")
+        for r in sorted(mk, key=lambda r: -float(r["TotalDurationNs"])):
+            print(f"| {r['Name']} | {r['Calls']} | {float(r['TotalDurationNs']) / 1e6:.3f} | "
+                  f"{float(r['AverageNs']) / 1e3:.1f} |")
     return 0
 
 
