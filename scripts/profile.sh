@@ -15,7 +15,7 @@ tag=${1:?usage: profile.sh TAG [command...]}
 shift
 [ $# -eq 0 ] && set -- python3 bench.py --steps 48 --warmup 12 --no-extras
 out="$PWD/gpurun_out/prof_$tag"
-mkdir -p "$out"
+rm -rf "$out"; mkdir -p "$out"
 timeout -k 10 600 rocprofv3 --kernel-trace --marker-trace --stats --output-format csv -d "$out" -o run -- "$@" \
   > "$out/run.log" 2>&1
 rc=$?
