@@ -129,3 +129,23 @@ def test_stencil_gpu_fault_injection_hang_is_detected(gpu, tmp_path):
                "--warmup", "0", "--fault-inject", "1:5:hang", "--comm-timeout", "3", cwd=tmp_path, timeout=120)
     assert r.returncode != 0
     assert "timed out after" in r.stdout + r.stderr
+
+
+def test_gpu_tutorial_neighbors1d_rccl(gpu):
+    """Device-buffer RCCL variant of mpi_neighbors1d (1 rank: RCCL refuses two ranks on one GPU)."""
+    r = mpirun(1, "gpu_neighbors1d_rccl")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.startswith("0/0:\t(-1, 0, -1)\t- ")
+
+
+def test_gpu_tutorial_groups_rccl(gpu):
+    r = mpirun(1, "gpu_groups_rccl")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "received: 0\t(host 0)" in r.stdout and "Allreduce total: 0 (host 0)" in r.stdout
+
+
+def test_gpu_tutorial_indexed_gather(gpu):
+    r = mpirun(3, "gpu_indexed_gather")
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = sorted(r.stdout.strip().split("\n"))
+    assert lines == [f"rank {i}: 5,6,7,8,12,13," for i in range(3)]
