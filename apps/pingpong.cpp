@@ -13,6 +13,10 @@
 // --transport mpi-staged  D2H -> MPI (blocking Send/Recv, or Isend/Irecv with --mode async)
 //                         -> H2D; --page-locked uses hipHostMalloc buffers (host_allocator.h)
 // --transport loopback    1 rank: RCCL self send/recv; d2d / pinned / pageable: local paths
+// --transport ipc         HIP IPC mailboxes: one persistent kernel per rank writes the
+//                         payload straight into the peer's HBM over xGMI and spins on a
+//                         system-scope flag (device-initiated, no host in the loop)
+// --transport ipc-loopback 1 rank: the same kernels, ping and pong on two streams
 #include <mpi.h>
 
 #include <algorithm>
@@ -29,6 +33,7 @@
 #include "mxs/core/device.hpp"
 #include "mxs/core/pinned_allocator.hpp"
 #include "mxs/runtime/hip_utils.hpp"
+#include "mxs/runtime/ipc.hpp"
 #include "mxs/runtime/pingpong.hpp"
 
 using namespace mxs;
@@ -120,7 +125,7 @@ int main(int argc, char** argv) {
                                                          : "loopback";
   const std::string mode = cli.get("mode", "blocking");
   const int warmup = int(cli.get_int("warmup", 5)), reps = int(cli.get_int("reps", 20));
-  if (env.size() < 2 && (transport == "rccl" || transport == "mpi-staged")) {
+  if (env.size() < 2 && (transport == "rccl" || transport == "mpi-staged" || transport == "ipc")) {
     if (env.rank() == 0) std::cerr << "transport " << transport << " needs 2 ranks" << std::endl;
     return 1;
   }
@@ -146,6 +151,20 @@ int main(int argc, char** argv) {
     }
   }
   const bool active = env.rank() < 2;
+  // HIP IPC: mailboxes exchanged between ranks 0 and 1 (runtime/ipc.hpp).
+  std::unique_ptr<IpcMailbox> mailbox;
+  std::unique_ptr<IpcPeerMailbox> peer_box;
+  if (transport == "ipc" && active) {
+    mailbox = std::make_unique<IpcMailbox>(maxb);
+    std::string mine = mailbox->handle(), theirs(mine.size(), '\0');
+    const int other = 1 - env.rank();
+    MXS_MPI_CHECK(MPI_Sendrecv(&mine[0], int(mine.size()), MPI_BYTE, other, 7, &theirs[0], int(theirs.size()),
+                               MPI_BYTE, other, 7, MPI_COMM_WORLD, MPI_STATUS_IGNORE));
+    peer_box = std::make_unique<IpcPeerMailbox>(theirs);
+    std::vector<unsigned char> pattern(maxb);
+    for (size_t i = 0; i < maxb; ++i) pattern[i] = static_cast<unsigned char>((i * 131 + 7) % 251);
+    MXS_HIP_CHECK(hipMemcpy(dsend.get(), pattern.data(), maxb, hipMemcpyHostToDevice));
+  }
   for (size_t bytes : sizes) {
     PingPongStats st;
     if (!active) continue;
@@ -154,6 +173,19 @@ int main(int argc, char** argv) {
                            : mode == "overlap" ? PingPongMode::Overlap : PingPongMode::Blocking;
       const int peer = transport == "loopback" ? env.rank() : 1 - env.rank();
       st = pingpong_rccl(*comm, peer, dsend.get(), drecv.get(), bytes, warmup, reps, m, stream.get());
+    } else if (transport == "ipc") {
+      IpcPingPongConfig c;
+      c.bytes = bytes;
+      c.warmup = warmup;
+      c.reps = std::max(reps, 1);
+      char token = 0;
+      const int other = 1 - env.rank();
+      MXS_MPI_CHECK(MPI_Sendrecv(&token, 1, MPI_BYTE, other, 8, &token, 1, MPI_BYTE, other, 8, MPI_COMM_WORLD,
+                                 MPI_STATUS_IGNORE));
+      st = pingpong_ipc(*mailbox, peer_box->base(), dsend.get(), env.rank() == 0, c, stream.get());
+      MXS_HIP_CHECK(hipMemcpy(drecv.get(), mailbox->data(), bytes, hipMemcpyDeviceToDevice));
+    } else if (transport == "ipc-loopback") {
+      st = pingpong_ipc_loopback(bytes, warmup, std::max(reps, 1));
     } else if (transport == "mpi-staged") {
       st = pinned ? staged(env, pin_s, pin_r, dsend.get(), drecv.get(), bytes, warmup, reps, mode == "async")
                   : staged(env, pg_s, pg_r, dsend.get(), drecv.get(), bytes, warmup, reps, mode == "async");

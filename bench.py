@@ -103,14 +103,23 @@ def main(argv=None) -> int:
             extras["stencil_8192sq_f32_1gpu_gcells_per_s"] = round(st1.cells_per_step * 600 / dt1 / 1e9, 2)
             del st1
         else:
-            pp = PingPong(ctx, "rccl", 256 << 20)
-            small = pp.run(8, "async", 20, 200)
-            big = pp.run(256 << 20, "async", 3, 20)
-            if ctx.is_root:
-                extras["pingpong_8B_latency_us"] = round(small.get("latency_us", 0.0), 2)
-                extras["pingpong_256MiB_gbps"] = round(big.get("gbps", 0.0), 2)
-                extras["pingpong_verified"] = bool(small.get("passed")) and bool(big.get("passed"))
-            del pp
+            # GPU-GPU ping-pong between ranks 0 and 1 (BASELINE's second metric):
+            # RCCL send/recv, and device-initiated HIP IPC. Failures are reported
+            # in extras and never stop the headline line.
+            for transport in ("rccl", "ipc"):
+                try:
+                    pp = PingPong(ctx, transport, 256 << 20)
+                    small = pp.run(8, "async", 20, 200)
+                    big = pp.run(256 << 20, "async", 3, 20)
+                    if ctx.is_root:
+                        extras[f"pingpong_{transport}_8B_latency_us"] = round(small.get("latency_us", 0.0), 2)
+                        extras[f"pingpong_{transport}_256MiB_gbps"] = round(big.get("gbps", 0.0), 2)
+                        extras[f"pingpong_{transport}_verified"] = bool(small.get("passed")) and bool(big.get("passed"))
+                    del pp
+                except Exception as e:  # noqa: BLE001
+                    extras[f"pingpong_{transport}_error"] = str(e)[:200]
+                torch.cuda.synchronize()
+                ctx.barrier()
         ctx.barrier()
 
     if ctx.is_root:

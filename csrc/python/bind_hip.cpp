@@ -17,6 +17,7 @@
 #include "mxs/comm/rccl_comm.hpp"
 #include "mxs/halo/exchange.hpp"
 #include "mxs/kernels/kernels.hpp"
+#include "mxs/runtime/ipc.hpp"
 #include "mxs/runtime/pingpong.hpp"
 #include "mxs/runtime/stencil_solver.hpp"
 
@@ -359,4 +360,32 @@ PYBIND11_MODULE(_mxs_hip, m) {
       },
       py::arg("path"), py::arg("buf_a"), py::arg("buf_b"), py::arg("nbytes"), py::arg("warmup") = 5,
       py::arg("reps") = 20, py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>());
+
+  // Device-initiated ping-pong over HIP IPC mappings (runtime/ipc.hpp).
+  py::class_<IpcMailbox>(m, "IpcMailbox")
+      .def(py::init<size_t>(), py::arg("capacity"))
+      .def("handle", [](const IpcMailbox& b) { return py::bytes(b.handle()); })
+      .def("base", [](const IpcMailbox& b) { return reinterpret_cast<std::uintptr_t>(b.base()); })
+      .def("data", [](const IpcMailbox& b) { return reinterpret_cast<std::uintptr_t>(b.data()); })
+      .def_property_readonly("capacity", &IpcMailbox::capacity);
+  py::class_<IpcPeerMailbox>(m, "IpcPeerMailbox")
+      .def(py::init([](py::bytes h) { return new IpcPeerMailbox(std::string(h)); }), py::arg("handle"))
+      .def("base", [](const IpcPeerMailbox& b) { return reinterpret_cast<std::uintptr_t>(b.base()); });
+  m.def(
+      "pingpong_ipc",
+      [](const IpcMailbox& mine, std::uintptr_t peer_base, std::uintptr_t src, bool ping, size_t bytes, int warmup,
+         int reps, int workgroups, double timeout_s, std::uintptr_t s) {
+        IpcPingPongConfig cfg;
+        cfg.bytes = bytes;
+        cfg.warmup = warmup;
+        cfg.reps = reps;
+        cfg.workgroups = workgroups;
+        cfg.timeout_s = timeout_s;
+        return pingpong_ipc(mine, ptr<unsigned char>(peer_base), ptr<void>(src), ping, cfg, strm(s));
+      },
+      py::arg("mailbox"), py::arg("peer_base"), py::arg("src"), py::arg("ping"), py::arg("nbytes"),
+      py::arg("warmup") = 5, py::arg("reps") = 50, py::arg("workgroups") = 0, py::arg("timeout_s") = 20.0,
+      py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>());
+  m.def("pingpong_ipc_loopback", &pingpong_ipc_loopback, py::arg("nbytes"), py::arg("warmup") = 5,
+        py::arg("reps") = 50, py::arg("workgroups") = 0, py::call_guard<py::gil_scoped_release>());
 }

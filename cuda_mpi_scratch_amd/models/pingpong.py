@@ -11,6 +11,10 @@ Transports:
   ``rccl``   native RCCL send/recv between rank 0 and rank 1 (xGMI), modes
              blocking (host sync per round trip), async (stream-pipelined,
              hipEvent-timed) and overlap (async beside an HBM-streaming kernel);
+  ``ipc``    device-initiated: HIP IPC mailboxes in each rank's HBM, one
+             persistent kernel per rank writes the payload into the peer's
+             mailbox over xGMI and spins on a system-scope flag for the echo
+             (no host in the loop; ``ipc-loopback``: both kernels on one GPU);
   ``torch``  torch.distributed send/recv on the default group (RCCL or gloo);
   ``local``  single-GPU baselines: D2D copy, pinned and pageable host staging
              (the HOST_COPY / PAGE_LOCKED paths), and RCCL self-loopback.
@@ -56,6 +60,19 @@ class PingPong:
         if transport == "rccl" or transport == "loopback":
             self.comm = make_rccl_comm(ctx)
         self.peer = 1 - ctx.rank if ctx.world_size > 1 else ctx.rank
+        self.mailbox = self.peer_mailbox = None
+        if transport == "ipc":
+            if ctx.world_size < 2:
+                raise ValueError("transport ipc needs 2 ranks (use ipc-loopback on one)")
+            H = hip()
+            self.mailbox = H.IpcMailbox(max_bytes) if self.active else None
+            h0 = ctx.broadcast_bytes(self.mailbox.handle() if ctx.rank == 0 else None, src=0)
+            h1 = ctx.broadcast_bytes(self.mailbox.handle() if ctx.rank == 1 else None, src=1)
+            if self.active:
+                self.peer_mailbox = H.IpcPeerMailbox(h1 if ctx.rank == 0 else h0)
+                pattern = (torch.arange(max_bytes, dtype=torch.int64, device=dev) * 131 + 7) % 251
+                self.send.copy_(pattern.to(torch.uint8))
+                torch.cuda.synchronize()
 
     @property
     def active(self) -> bool:
@@ -77,6 +94,15 @@ class PingPong:
             p = {"d2d": H.LocalPath.DEVICE_COPY, "pinned": H.LocalPath.PINNED_STAGING,
                  "pageable": H.LocalPath.PAGEABLE_STAGING}[self.transport]
             st = H.pingpong_local(p, self.send.data_ptr(), self.recv.data_ptr(), nbytes, warmup, reps, stream)
+        elif self.transport == "ipc":
+            if not self.active:
+                return rec
+            # No host barrier: the persistent kernels tolerate start skew (and
+            # fail by device deadline, never by hanging a collective).
+            st = H.pingpong_ipc(self.mailbox, self.peer_mailbox.base(), self.send.data_ptr(), self.ctx.rank == 0,
+                                nbytes, warmup, max(reps, 1), 0, 20.0, stream)
+        elif self.transport == "ipc-loopback":
+            st = H.pingpong_ipc_loopback(nbytes, warmup, max(reps, 1))
         elif self.transport == "torch":
             return self._run_torch(nbytes, warmup, reps, rec)
         else:
@@ -133,7 +159,7 @@ def main(argv=None) -> int:
                    help="reference positional arg: number of doubles (one size)")
     p.add_argument("--sweep", default="8:268435456")
     p.add_argument("--transport", default="rccl",
-                   choices=["rccl", "loopback", "torch", "d2d", "pinned", "pageable"])
+                   choices=["rccl", "loopback", "ipc", "ipc-loopback", "torch", "d2d", "pinned", "pageable"])
     p.add_argument("--mode", default="blocking", choices=["blocking", "async", "overlap"])
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--reps", type=int, default=20)

@@ -149,3 +149,17 @@ def test_gpu_tutorial_indexed_gather(gpu):
     assert r.returncode == 0, r.stderr[-3000:]
     lines = sorted(r.stdout.strip().split("\n"))
     assert lines == [f"rank {i}: 5,6,7,8,12,13," for i in range(3)]
+
+
+def test_pingpong_ipc_two_processes_one_gpu(gpu):
+    """HIP IPC mailboxes between two processes (same GPU here; xGMI peers on a node):
+    device-initiated round trips, echo verified, tail bytes and multi-workgroup sizes."""
+    r = mpirun(2, "pingpong", "--transport", "ipc", "--sweep", "8,4099,1048576,16777216", "--reps", "20")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count('"passed": true') == 4, r.stdout
+
+
+def test_pingpong_ipc_reference_output(gpu):
+    r = mpirun(2, "pingpong", "--transport", "ipc", "131072")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.startswith("PASSED\nMessage size(MB): 1\nRound-trip time(ms): ")

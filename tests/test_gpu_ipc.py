@@ -1,0 +1,33 @@
+"""Device-initiated IPC ping-pong kernels (runtime/ipc.hpp) on one GPU: ping and
+pong persistent kernels on two streams of one process exchange through two
+mailboxes with the same protocol as the two-process path."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("nbytes", [8, 100, 4099, 65536, 1 << 20, 1 << 24])
+def test_ipc_loopback_roundtrips_verified(gpu, nbytes):
+    from cuda_mpi_scratch_amd import hip
+
+    st = hip().pingpong_ipc_loopback(nbytes, 3, 20)
+    assert st.verified
+    assert st.reps == 20
+    assert 0 < st.min_rtt_us <= st.median_rtt_us <= st.max_rtt_us
+
+
+def test_ipc_loopback_multi_workgroup_forced(gpu):
+    from cuda_mpi_scratch_amd import hip
+
+    st = hip().pingpong_ipc_loopback(1 << 20, 2, 10, 16)
+    assert st.verified
+
+
+def test_python_pingpong_ipc_loopback_transport(gpu):
+    from cuda_mpi_scratch_amd.models.pingpong import PingPong
+    from cuda_mpi_scratch_amd.parallel import init
+
+    ctx = init(backend="gloo")
+    pp = PingPong(ctx, "ipc-loopback", 1 << 16)
+    rec = pp.run(4096, "async", 2, 10)
+    assert rec["passed"] and rec["latency_us"] > 0
