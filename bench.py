@@ -40,16 +40,21 @@ def _ms(x):
     return round(x * 1e3, 4)
 
 
+def _sync():
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+
+
 def timed_run(st, ctx, steps: int, warmup: int) -> float:
     st.run(warmup)
     st.synchronize()
-    torch.cuda.synchronize()
+    _sync()
     ctx.barrier()
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     st.run(steps)
     st.synchronize()
-    torch.cuda.synchronize()
+    _sync()
     ctx.barrier()
     t1 = time.perf_counter()
     return ctx.allreduce_max(t1 - t0)
@@ -118,7 +123,7 @@ def main(argv=None) -> int:
                     del pp
                 except Exception as e:  # noqa: BLE001
                     extras[f"pingpong_{transport}_error"] = str(e)[:200]
-                torch.cuda.synchronize()
+                _sync()
                 ctx.barrier()
         ctx.barrier()
 

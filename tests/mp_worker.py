@@ -62,6 +62,21 @@ def task_checkpoint(args):
     return out
 
 
+def task_bench(args):
+    """bench.py main() on every rank (CPU / gloo): the contract line from rank 0."""
+    import contextlib
+    import io
+
+    sys.path.insert(0, ROOT)
+    import bench
+
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        rc = bench.main(args["argv"])
+    lines = [ln for ln in buf.getvalue().splitlines() if ln.startswith("{")]
+    return {"rank": int(os.environ["RANK"]), "rc": rc, "line": lines[-1] if lines else None}
+
+
 def task_halo_property(args):
     """Non-square tiles and grids: after one exchange every ghost cell holds the
     owning neighbour's core value (cell value = global linear index)."""
