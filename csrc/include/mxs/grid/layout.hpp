@@ -12,6 +12,10 @@
 #pragma once
 
 #include <ostream>
+#ifdef MXS_DEBUG_BOUNDS
+#include <cstdio>
+#include <cstdlib>
+#endif
 
 #include "mxs/core/config.hpp"
 
@@ -54,13 +58,35 @@ inline std::ostream& operator<<(std::ostream& os, const Array2D& a) {
   return os;
 }
 
+#ifdef MXS_DEBUG_BOUNDS
+[[noreturn]] inline void bounds_fail(index_t x, index_t y) {
+  std::fprintf(stderr, "Accessor2D: (%lld, %lld) outside the window\n", static_cast<long long>(x),
+               static_cast<long long>(y));
+  std::abort();
+}
+#endif
+
 // Random access into a window of a buffer.
 template <typename T>
 class Accessor2D {
  public:
   MXS_HD Accessor2D() = default;
   MXS_HD Accessor2D(T* data, const Array2D& layout) : data_(data), layout_(layout) {}
-  MXS_HD T& operator()(index_t x, index_t y) const { return data_[layout_.index(x, y)]; }
+  // -DMXS_DEBUG_BOUNDS: every access is checked against the window (host: assert
+  // with the offending coordinates; device: __builtin_trap, a visible fault
+  // instead of a silent out-of-window read) — SURVEY §5.2.
+  MXS_HD T& operator()(index_t x, index_t y) const {
+#ifdef MXS_DEBUG_BOUNDS
+    if (x < 0 || y < 0 || x >= layout_.width || y >= layout_.height) {
+#if defined(__HIP_DEVICE_COMPILE__)
+      __builtin_trap();
+#else
+      bounds_fail(x, y);
+#endif
+    }
+#endif
+    return data_[layout_.index(x, y)];
+  }
   MXS_HD const Array2D& layout() const { return layout_; }
   MXS_HD T* data() const { return data_; }
 

@@ -19,6 +19,17 @@ def test_cpp_unit_tests(build_dir):
     assert "all passed" in r.stdout
 
 
+def test_debug_bounds_accessor(build_dir):
+    """-DMXS_DEBUG_BOUNDS build: in-window accesses pass, one past the core aborts loudly."""
+    exe = os.path.join(build_dir, "mxs_bounds_test")
+    if not os.path.exists(exe):
+        pytest.skip("bounds test not built")
+    ok = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert ok.returncode == 0 and "sum 276" in ok.stdout
+    bad = subprocess.run([exe, "oob"], capture_output=True, text=True, timeout=60)
+    assert bad.returncode != 0 and "(6, 0) outside the window" in bad.stderr
+
+
 def test_region_text_format():
     g = C.Array2D(20, 20, 20)
     core = C.sub_array_region(g, 5, 5, C.RegionID.CENTER)
