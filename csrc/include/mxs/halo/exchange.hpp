@@ -18,6 +18,9 @@
 //   Local : every neighbour is the rank itself (1x1 periodic grid) — only step 1.
 //   Rccl  : RCCL point-to-point over xGMI. A 1-rank communicator is legal (self
 //           send/recv), which lets one GPU exercise the full RCCL path.
+//   Ipc   : direct writes into the peers' receive buffers through HIP IPC
+//           mappings, device-side ready/free counters (halo/ipc_transport.hpp);
+//           no RCCL, graph-capturable, works for ranks that share a GPU.
 // The MPI backends (host datatypes, pinned-host staging) live in
 // comm/mpi_halo.hpp because they need <mpi.h>.
 #pragma once
@@ -27,13 +30,22 @@
 #include <memory>
 
 #include "mxs/comm/rccl_comm.hpp"
+#include "mxs/halo/ipc_transport.hpp"
 #include "mxs/halo/plan.hpp"
 #include "mxs/kernels/kernels.hpp"
 #include "mxs/runtime/hip_utils.hpp"
 
 namespace mxs {
 
-enum class HaloBackend : int { Local = 0, Rccl = 1 };
+enum class HaloBackend : int { Local = 0, Rccl = 1, Ipc = 2 };
+
+// What the Ipc backend needs to set itself up (collective over all ranks).
+struct HaloBootstrap {
+  int rank = 0;
+  int world_size = 1;
+  HostAllgather allgather;
+  double timeout_s = 60.0;  // device-side deadline of any IPC wait
+};
 
 // Copy descriptors for the pack (tile -> send buffer, plus self copies) and
 // unpack (recv buffer -> tile) launches of a plan. Slot 0 = tile, 1 = send
@@ -47,8 +59,11 @@ HaloCopyPrograms build_halo_copy_programs(const HaloPlan& plan);
 template <typename T>
 class HaloExchanger {
  public:
-  // `comm` may be null only when the plan has no remote peers.
-  HaloExchanger(const HaloPlan& plan, HaloBackend backend, const RcclComm* comm);
+  // `comm` may be null only when the plan has no remote peers (or for Ipc).
+  // `boot` is required by the Ipc backend (collective construction).
+  HaloExchanger(const HaloPlan& plan, HaloBackend backend, const RcclComm* comm,
+                const HaloBootstrap* boot = nullptr);
+  ~HaloExchanger();
 
   // Enqueue a full exchange for `tile` on `stream`.
   void exchange(T* tile, hipStream_t stream);
@@ -63,6 +78,8 @@ class HaloExchanger {
   T* recv_buffer() const { return recv_.get(); }
   // Bytes this rank puts on the wire per exchange (excluding self copies).
   size_t wire_bytes() const { return size_t(plan_.send_elems) * sizeof(T); }
+  // Raises if a device-side wait of the Ipc backend timed out (stream idle).
+  void check() const;
 
  private:
   HaloPlan plan_;
@@ -70,6 +87,7 @@ class HaloExchanger {
   const RcclComm* comm_;
   HaloCopyPrograms progs_;
   DeviceBuffer<T> send_, recv_;
+  std::unique_ptr<IpcHaloTransport<T>> ipc_;
 };
 
 }  // namespace mxs

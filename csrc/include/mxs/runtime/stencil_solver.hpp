@@ -58,6 +58,8 @@ struct SolverConfig {
   kernels::Stencil5Coeffs coeffs;
   kernels::BoxWeights box;
   kernels::StencilVariant variant = kernels::StencilVariant::Auto;
+  // HaloBackend::Ipc: host allgather used once at construction (collective).
+  HostAllgather bootstrap;
 };
 
 template <typename T>

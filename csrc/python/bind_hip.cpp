@@ -39,6 +39,19 @@ DType parse_dtype(const std::string& d) {
   throw std::invalid_argument("unsupported dtype '" + d + "' (use f32 or f64)");
 }
 
+// Python callable (bytes -> list[bytes], collective) as the IPC backend's host
+// allgather. Only called during construction, with the GIL held.
+HostAllgather wrap_allgather(py::object fn) {
+  if (fn.is_none()) return {};
+  return [fn](const std::string& blob) {
+    py::gil_scoped_acquire gil;
+    py::list parts = fn(py::bytes(blob));
+    std::vector<std::string> out;
+    for (auto item : parts) out.push_back(std::string(py::bytes(py::reinterpret_borrow<py::object>(item))));
+    return out;
+  };
+}
+
 kernels::StencilVariant parse_variant(const std::string& v) {
   if (v == "auto") return kernels::StencilVariant::Auto;
   if (v == "roll") return kernels::StencilVariant::RegisterRoll;
@@ -248,17 +261,26 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def("group_end", &RcclComm::group_end);
 
   // ------------------------------------------------------------------ halo
-  py::enum_<HaloBackend>(m, "HaloBackend").value("LOCAL", HaloBackend::Local).value("RCCL", HaloBackend::Rccl);
+  py::enum_<HaloBackend>(m, "HaloBackend")
+      .value("LOCAL", HaloBackend::Local)
+      .value("RCCL", HaloBackend::Rccl)
+      .value("IPC", HaloBackend::Ipc);
   py::class_<ExchangerHandle>(m, "HaloExchanger")
-      .def(py::init([](const HaloPlan& plan, HaloBackend b, const RcclComm* comm, const std::string& dt) {
+      .def(py::init([](const HaloPlan& plan, HaloBackend b, const RcclComm* comm, const std::string& dt,
+                       py::object bootstrap, int world_size) {
              auto h = std::make_unique<ExchangerHandle>();
              h->dt = parse_dtype(dt);
-             if (h->dt == DType::F32) h->f = std::make_unique<HaloExchanger<float>>(plan, b, comm);
-             else h->d = std::make_unique<HaloExchanger<double>>(plan, b, comm);
+             HaloBootstrap boot;
+             boot.rank = plan.rank;
+             boot.world_size = world_size;
+             boot.allgather = wrap_allgather(bootstrap);
+             if (h->dt == DType::F32) h->f = std::make_unique<HaloExchanger<float>>(plan, b, comm, &boot);
+             else h->d = std::make_unique<HaloExchanger<double>>(plan, b, comm, &boot);
              return h;
            }),
            py::arg("plan"), py::arg("backend"), py::arg("comm") = nullptr, py::arg("dtype") = "f32",
-           py::keep_alive<1, 4>())
+           py::arg("bootstrap") = py::none(), py::arg("world_size") = 1, py::keep_alive<1, 4>())
+      .def("check", [](const ExchangerHandle& h) { h.dt == DType::F32 ? h.f->check() : h.d->check(); })
       .def(
           "exchange",
           [](ExchangerHandle& h, std::uintptr_t tile, std::uintptr_t s) {
@@ -274,8 +296,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def(py::init([](const CartTopology& topo, int rank, const TileGeom& tile, std::uintptr_t a, std::uintptr_t b,
                        const RcclComm* comm, const std::string& dt, HaloBackend backend, bool overlap,
                        bool use_graph, bool loopback_self, StencilKind kind, double c0, double c1, int box_radius,
-                       const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block) {
+                       const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
+                       py::object bootstrap) {
              SolverConfig cfg;
+             cfg.bootstrap = wrap_allgather(bootstrap);
              cfg.backend = backend;
              cfg.overlap = overlap;
              cfg.use_graph = use_graph;
@@ -300,7 +324,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("overlap") = true, py::arg("use_graph") = true, py::arg("loopback_self") = false,
            py::arg("kind") = StencilKind::Jacobi5, py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2,
            py::arg("box_radius") = 1, py::arg("box_weights") = std::vector<float>{}, py::arg("variant") = "auto",
-           py::arg("fuse_periodic") = true, py::arg("time_block") = 1,
+           py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
            py::keep_alive<1, 7>())
       .def("step", [](SolverHandle& h) { h.visit([](auto& s) { s.step(); }); })
       .def(

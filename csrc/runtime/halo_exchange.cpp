@@ -56,14 +56,28 @@ HaloCopyPrograms build_halo_copy_programs(const HaloPlan& plan) {
 }
 
 template <typename T>
-HaloExchanger<T>::HaloExchanger(const HaloPlan& plan, HaloBackend backend, const RcclComm* comm)
+HaloExchanger<T>::HaloExchanger(const HaloPlan& plan, HaloBackend backend, const RcclComm* comm,
+                                const HaloBootstrap* boot)
     : plan_(plan), backend_(backend), comm_(comm), progs_(build_halo_copy_programs(plan)) {
   if (!plan_.sends.empty()) {
-    MXS_CHECK(backend_ == HaloBackend::Rccl, "plan has remote peers: the Local backend cannot serve it");
-    MXS_CHECK(comm_ != nullptr, "Rccl halo backend needs a communicator");
+    MXS_CHECK(backend_ != HaloBackend::Local, "plan has remote peers: the Local backend cannot serve it");
+    if (backend_ == HaloBackend::Rccl) MXS_CHECK(comm_ != nullptr, "Rccl halo backend needs a communicator");
   }
   send_.reset(plan_.send_elems);
   recv_.reset(plan_.recv_elems);
+  if (backend_ == HaloBackend::Ipc) {
+    MXS_CHECK(boot != nullptr, "Ipc halo backend needs a HaloBootstrap (rank, world size, host allgather)");
+    ipc_ = std::make_unique<IpcHaloTransport<T>>(plan_, send_.get(), recv_.get(), boot->rank, boot->world_size,
+                                                 boot->allgather, boot->timeout_s);
+  }
+}
+
+template <typename T>
+HaloExchanger<T>::~HaloExchanger() = default;
+
+template <typename T>
+void HaloExchanger<T>::check() const {
+  if (ipc_) ipc_->check();
 }
 
 template <typename T>
@@ -74,6 +88,11 @@ void HaloExchanger<T>::pack(T* tile, hipStream_t stream) {
 
 template <typename T>
 void HaloExchanger<T>::transfer(hipStream_t stream) {
+  if (ipc_) {
+    ipc_->put(stream);
+    ipc_->wait(stream);
+    return;
+  }
   if (plan_.sends.empty()) return;
   MXS_TRACE_RANGE("halo.rccl_sendrecv");
   comm_->group_start();
@@ -86,6 +105,7 @@ template <typename T>
 void HaloExchanger<T>::unpack(T* tile, hipStream_t stream) {
   MXS_TRACE_RANGE("halo.unpack");
   kernels::copy2d_batch<T>(tile, send_.get(), recv_.get(), progs_.unpack, stream);
+  if (ipc_) ipc_->release(stream);  // receive buffer consumed: senders may write the next exchange
 }
 
 template <typename T>

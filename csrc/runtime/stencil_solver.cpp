@@ -25,7 +25,13 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
             "ghost ring (" << tile_.halo_x << ") shallower than the stencil radius x time block (" << depth << ")");
   const bool corners = cfg_.corners || cfg_.kind == StencilKind::Box || block_ > 1;
   const HaloPlan plan = make_halo_plan(topo, rank, tile_, corners, cfg_.loopback_self);
-  ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm);
+  HaloBootstrap boot;
+  boot.rank = rank;
+  boot.world_size = topo.size();
+  boot.allgather = cfg_.bootstrap;
+  boot.timeout_s = comm_timeout() > 0 ? comm_timeout() : 60.0;
+  ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm, &boot);
+  cfg_.bootstrap = nullptr;  // setup only; drop it (it may hold a Python callable)
   // Overlap only pays when there is a wire transfer to hide and an interior.
   if (plan.sends.empty() || tile_.height <= 2 * depth || tile_.width <= 2 * depth) cfg_.overlap = false;
   const bool all_self = plan.sends.empty() && int(plan.self_copies.size()) == (corners ? kNumDirs : 4);
@@ -203,6 +209,7 @@ void StencilSolver<T>::synchronize() {
   if (comm_ && comm_timeout() > 0) comm_->wait(main_.get(), "stencil halo exchange (RCCL)");
   main_.sync();
   side_.sync();
+  ex_->check();  // IPC backend: device-side waits carry their own deadline
 }
 
 template class StencilSolver<float>;

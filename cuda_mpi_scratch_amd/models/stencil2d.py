@@ -21,6 +21,7 @@ from __future__ import annotations
 import argparse
 import json
 import math
+import os
 import sys
 import time
 from dataclasses import asdict, dataclass, field
@@ -49,7 +50,7 @@ class StencilConfig:
     box_weights: list = field(default_factory=list)
     c_center: float = 0.2
     c_neighbor: float = 0.2
-    backend: str = "auto"            # auto | rccl | local | torch
+    backend: str = "auto"            # auto | rccl | ipc | local | torch
     overlap: bool = True
     graph: bool = True
     loopback: bool = False           # single GPU: send self-neighbour halos through RCCL
@@ -103,24 +104,30 @@ class Stencil2D:
         if dev.type != "cuda":
             backend = "torch"
         elif backend == "auto":
-            backend = "local" if (self.ctx.world_size == 1 and not cfg.loopback) else "rccl"
+            if self.ctx.world_size == 1:
+                backend = "rccl" if cfg.loopback else "local"
+            else:
+                # RCCL refuses two ranks on one GPU: ranks sharing GPUs use the IPC backend.
+                local = int(os.environ.get("LOCAL_WORLD_SIZE", self.ctx.world_size))
+                backend = "ipc" if local > max(1, torch.cuda.device_count()) else "rccl"
         self.backend = backend
         self.comm = None
         self.solver = None
         self._cur, self._nxt = self.a, self.b
-        if backend in ("rccl", "local"):
+        if backend in ("rccl", "local", "ipc"):
             H = hip()
             if backend == "rccl":
                 self.comm = make_rccl_comm(self.ctx)
             torch.cuda.synchronize()
             kind = H.StencilKind.BOX if cfg.kind == "box" else H.StencilKind.JACOBI5
-            be = H.HaloBackend.RCCL if backend == "rccl" else H.HaloBackend.LOCAL
+            be = {"rccl": H.HaloBackend.RCCL, "local": H.HaloBackend.LOCAL, "ipc": H.HaloBackend.IPC}[backend]
+            boot = self.ctx.allgather_bytes if backend == "ipc" else None
             weights = [float(w) for w in cfg.box_weights] if cfg.kind == "box" else []
             radius = (int(round(math.sqrt(len(weights)))) - 1) // 2 if weights else 1
             self.solver = H.StencilSolver(d.topo, d.rank, self.geom, self.a.data_ptr(), self.b.data_ptr(), self.comm,
                                           cfg.dtype, be, cfg.overlap, cfg.graph, cfg.loopback, kind, cfg.c_center,
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
-                                          self.time_block)
+                                          self.time_block, boot)
         else:
             self.plan = make_plan(d, self.geom, corners=True)
             self.halo = TorchHalo(self.plan, self.ctx)
@@ -279,7 +286,7 @@ def main(argv=None) -> int:
     p.add_argument("--dtype", default="f32", choices=list(_DTYPES))
     p.add_argument("--iters", type=int, default=100)
     p.add_argument("--warmup", type=int, default=10)
-    p.add_argument("--backend", default="auto", choices=["auto", "rccl", "local", "torch"])
+    p.add_argument("--backend", default="auto", choices=["auto", "rccl", "ipc", "local", "torch"])
     p.add_argument("--no-overlap", action="store_true")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--loopback", action="store_true")

@@ -95,6 +95,16 @@ class DistContext:
             return payload
         return bytes(store.get(k))
 
+    def allgather_bytes(self, payload: bytes, key: str | None = None) -> list[bytes]:
+        """Every rank contributes a byte string, every rank gets all of them in rank
+        order (through the rendezvous store: control-plane sized payloads only)."""
+        if not self.is_distributed:
+            return [payload]
+        store = dist.distributed_c10d._get_default_store()
+        k = key or f"mxs/allgather/{next(_uid_counter)}"
+        store.set(f"{k}/{self.rank}", payload)
+        return [bytes(store.get(f"{k}/{r}")) for r in range(self.world_size)]
+
     def destroy(self) -> None:
         if self.owns_group and dist.is_initialized():
             dist.destroy_process_group()

@@ -15,14 +15,18 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
-def run_ranks(task: str, nprocs: int, args: dict, timeout: int = 240) -> list[dict]:
+def run_ranks(task: str, nprocs: int, args: dict, timeout: int = 240, gpu: bool = False) -> list[dict]:
+    """`gpu=True`: every rank sees the (single) GPU — ranks share it, as in the
+    IPC-backend tests; otherwise GPUs are hidden (CPU / gloo)."""
     port = free_port()
     procs = []
     for r in range(nprocs):
         env = dict(os.environ)
-        env.update(RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
-                   OMP_NUM_THREADS="1")
+        env.update(RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(nprocs),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1",
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        if not gpu:
+            env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "mp_worker.py"), task, json.dumps(args)],
                                       env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     results = []

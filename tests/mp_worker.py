@@ -77,6 +77,27 @@ def task_bench(args):
     return {"rank": int(os.environ["RANK"]), "rc": rc, "line": lines[-1] if lines else None}
 
 
+def task_gpu_solver(args):
+    """Native solver on a shared GPU (IPC halo backend): random init, N iterations,
+    global grid back on rank 0."""
+    ctx = init(backend="gloo", device="cuda")
+    cfg = StencilConfig(global_width=args["w"], global_height=args["h"], dims=args["dims"],
+                        dtype=args.get("dtype", "f32"), seed=args.get("seed", 5), backend=args.get("backend", "auto"),
+                        overlap=args.get("overlap", True), graph=args.get("graph", True),
+                        time_block=args.get("time_block", 12))
+    st = Stencil2D(cfg, ctx)
+    st.run(args["iters"])
+    st.synchronize()
+    g = st.gather_global()
+    out = {"rank": ctx.rank, "backend": st.backend, "halo": st.halo_mode(), "graph": st.graph_status(),
+           "native": st.solver is not None}
+    if ctx.rank == 0:
+        out["grid"] = g.double().tolist()
+    ctx.barrier()
+    ctx.destroy()
+    return out
+
+
 def task_halo_property(args):
     """Non-square tiles and grids: after one exchange every ghost cell holds the
     owning neighbour's core value (cell value = global linear index)."""
