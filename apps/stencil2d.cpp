@@ -5,9 +5,11 @@
 // device data moves by one of:
 //   --backend rccl        per-peer ncclSend/ncclRecv over xGMI (default when every
 //                         rank has its own GPU), compute/comm overlap + hipGraph;
+//   --backend ipc         HIP IPC: direct writes into the peers' receive buffers,
+//                         device-side ready/free counters, overlap + hipGraph
+//                         (default when ranks share a GPU, where RCCL refuses);
 //   --backend mpi-staged  HIP pack -> pinned host staging -> MPI -> HIP unpack
-//                         (default when ranks share a GPU; --pageable for the
-//                         non-PAGE_LOCKED variant);
+//                         (--pageable for the non-PAGE_LOCKED variant);
 //   --backend local       1x1 periodic grid: a single HIP self-copy launch.
 //
 //   mpiexec -n 9 stencil2d            # reference run: 16x16 tiles, 5x5 stencil, fp64,
@@ -71,7 +73,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   const bool loopback = cli.flag("loopback");
   if (backend == "auto") {
     if (env.size() == 1) backend = loopback ? "rccl" : "local";
-    else if (env.local_size() > dev.devices_used) backend = "mpi-staged";  // GPUs shared: RCCL refuses
+    else if (env.local_size() > dev.devices_used) backend = "ipc";  // GPUs shared: RCCL refuses
     else backend = "rccl";
   }
   // Temporal blocking (timed runs on the solver backends): S Jacobi steps per
@@ -88,7 +90,8 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   MPI_Comm cart = make_cart_comm(topo);
 
   SolverConfig cfg;
-  cfg.backend = backend == "rccl" ? HaloBackend::Rccl : HaloBackend::Local;
+  cfg.backend = backend == "rccl" ? HaloBackend::Rccl : backend == "ipc" ? HaloBackend::Ipc : HaloBackend::Local;
+  if (backend == "ipc") cfg.bootstrap = [](const std::string& b) { return mpi_allgather_bytes(MPI_COMM_WORLD, b); };
   cfg.overlap = !cli.flag("no-overlap");
   cfg.use_graph = !cli.flag("no-graph");
   cfg.loopback_self = loopback;
@@ -100,7 +103,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   if (backend == "mpi-staged") {
     staged = std::make_unique<MpiStagedHalo<T>>(plan, cart, !cli.flag("pageable"));
   } else {
-    MXS_CHECK(backend == "rccl" || backend == "local", "unknown backend " << backend);
+    MXS_CHECK(backend == "rccl" || backend == "local" || backend == "ipc", "unknown backend " << backend);
     solver = std::make_unique<StencilSolver<T>>(topo, rank, g, a.get(), b.get(), comm.get(), cfg);
   }
 

@@ -62,6 +62,22 @@ inline void mpi_wait_all(std::vector<MPI_Request>& req, const char* what) {
       what, [] {});
 }
 
+// Variable-length allgather of byte strings (control-plane sized), rank order.
+// Usable as the IPC halo backend's HostAllgather bootstrap.
+inline std::vector<std::string> mpi_allgather_bytes(MPI_Comm comm, const std::string& blob) {
+  int n = 0;
+  MXS_MPI_CHECK(MPI_Comm_size(comm, &n));
+  int len = int(blob.size());
+  std::vector<int> lens(static_cast<size_t>(n)), displs(static_cast<size_t>(n), 0);
+  MXS_MPI_CHECK(MPI_Allgather(&len, 1, MPI_INT, lens.data(), 1, MPI_INT, comm));
+  for (int r = 1; r < n; ++r) displs[size_t(r)] = displs[size_t(r - 1)] + lens[size_t(r - 1)];
+  std::string all(size_t(displs[size_t(n - 1)] + lens[size_t(n - 1)]), '\0');
+  MXS_MPI_CHECK(MPI_Allgatherv(blob.data(), len, MPI_BYTE, &all[0], lens.data(), displs.data(), MPI_BYTE, comm));
+  std::vector<std::string> out(static_cast<size_t>(n));
+  for (int r = 0; r < n; ++r) out[size_t(r)] = all.substr(size_t(displs[size_t(r)]), size_t(lens[size_t(r)]));
+  return out;
+}
+
 enum class MpiErrors { Abort, Throw };
 
 class MpiEnv {

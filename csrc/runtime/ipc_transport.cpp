@@ -71,6 +71,9 @@ __device__ bool spin_ge(const u64* p, u64 target, u64 timeout_ticks, u64* status
       atomicCAS(status, 0ull, code);
       return false;
     }
+    // An earlier wait already failed: the exchange sequence is broken, give up
+    // at once instead of letting every queued exchange run into its deadline.
+    if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return false;
     __builtin_amdgcn_s_sleep(1);
   }
   return true;
@@ -189,6 +192,7 @@ struct IpcHaloTransport<T>::Impl {
   int nput = 0, nwait = 0;
   unsigned grid_x = 1;
   u64 timeout_ticks = 0;
+  double timeout_s = 0;
 };
 
 template <typename T>
@@ -204,6 +208,7 @@ IpcHaloTransport<T>::IpcHaloTransport(const HaloPlan& plan, const T* send, T* re
   MXS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&I.ctrl), I.L.words() * sizeof(u64)));
   MXS_HIP_CHECK(hipMemset(I.ctrl, 0, I.L.words() * sizeof(u64)));
   I.timeout_ticks = u64(timeout_s * wall_clock_hz());
+  I.timeout_s = timeout_s;
 
   // Exchange handles + receive tables. A rank with nothing to receive still
   // exports (a dummy 1-element buffer is not needed: recv may be null, then
@@ -337,7 +342,8 @@ void IpcHaloTransport<T>::check() const {
   MXS_CHECK(status == 0, "IPC halo exchange: "
                              << (status == 1 ? "waiting for a peer to free its receive buffer"
                                              : "waiting for a peer's halo")
-                             << " timed out on the device (peer dead or hung)");
+                             << " timed out after " << impl_->timeout_s
+                             << " s on the device: a peer rank is dead or hung (device watchdog)");
 }
 
 template class IpcHaloTransport<float>;
