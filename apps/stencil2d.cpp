@@ -92,7 +92,12 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   SolverConfig cfg;
   cfg.backend = backend == "rccl" ? HaloBackend::Rccl : backend == "ipc" ? HaloBackend::Ipc : HaloBackend::Local;
   if (backend == "ipc") cfg.bootstrap = [](const std::string& b) { return mpi_allgather_bytes(MPI_COMM_WORLD, b); };
-  cfg.overlap = !cli.flag("no-overlap");
+  // Ranks sharing a GPU: their cross-process waits plus the forked interior
+  // branch oversubscribe the GPU's queues and the scheduler time-slices them
+  // (ms-scale stalls, measured: 3-28 vs ~3000 Gcells/s with overlap off), so
+  // co-located ranks default to the serial exchange + update schedule.
+  const bool shared_gpu = env.local_size() > dev.devices_used;
+  cfg.overlap = cli.flag("overlap") || (!cli.flag("no-overlap") && !shared_gpu);
   cfg.use_graph = !cli.flag("no-graph");
   cfg.loopback_self = loopback;
   cfg.coeffs = {cli.get_double("c-center", 0.2), cli.get_double("c-neighbor", 0.2)};
@@ -226,8 +231,8 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
 
 int main(int argc, char** argv) {
   MpiEnv env(&argc, &argv);
-  Cli cli(argc, argv, {"dump", "no-dump", "non-periodic", "strict-square", "no-overlap", "no-graph", "loopback",
-                       "pageable", "checksum"});
+  Cli cli(argc, argv, {"dump", "no-dump", "non-periodic", "strict-square", "no-overlap", "overlap", "no-graph",
+                       "loopback", "pageable", "checksum"});
   comm_timeout() = cli.get_double("comm-timeout", 300.0);
   const DeviceBinding dev = bind_device(env, cli.get("bind", "bunch"));
   const int n = env.size();

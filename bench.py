@@ -88,7 +88,8 @@ def main(argv=None) -> int:
     rows, cols = choose_dims(n, args.dims, prefer="wide")
     gw, gh = (int(v) for v in args.global_.lower().split("x"))
     cfg = StencilConfig(global_width=gw, global_height=gh, dims=f"{rows}x{cols}", dtype=args.dtype,
-                        kind="jacobi5", backend="auto", overlap=not args.no_overlap, graph=not args.no_graph,
+                        kind="jacobi5", backend="auto", overlap=False if args.no_overlap else None,
+                        graph=not args.no_graph,
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup)

@@ -11,9 +11,12 @@
 
 #include <mpi.h>
 
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mxs/core/error.hpp"
@@ -124,7 +127,13 @@ inline MpiEnv::MpiEnv(int* argc, char*** argv, MpiErrors mode) {
 
   if (mode == MpiErrors::Abort) {
     error_config().policy = ErrorPolicy::Abort;
-    error_config().abort_hook = [](int code) { MPI_Abort(MPI_COMM_WORLD, code == 0 ? 1 : code); };
+    error_config().abort_hook = [](int code) {
+      // Let the launcher's stdio forwarding drain the error message before the
+      // abort tears every rank down (otherwise it is often lost).
+      std::fflush(nullptr);
+      std::this_thread::sleep_for(std::chrono::milliseconds(300));
+      MPI_Abort(MPI_COMM_WORLD, code == 0 ? 1 : code);
+    };
   } else {
     error_config().policy = ErrorPolicy::Throw;
   }

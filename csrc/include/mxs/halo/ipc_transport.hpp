@@ -8,9 +8,10 @@
 // Each sender then maps the receivers' buffers and learns where its message
 // lands. One exchange k is three stream-ordered launches:
 //
-//   put     : one workgroup column per outgoing message; waits until the peer
-//             has consumed exchange k-1 (its "free" counter, written into our
-//             control block), copies the packed message straight into the
+//   put     : a one-workgroup kernel waits until every peer has consumed
+//             exchange k-1 (its "free" counter, written into our control
+//             block); then one workgroup column per outgoing message copies
+//             the packed message straight into the
 //             peer's receive buffer over xGMI with system-coherent stores, and
 //             the last workgroup of the message publishes ready[me] = k in the
 //             peer's control block (release, system scope);

@@ -87,7 +87,9 @@ __global__ __launch_bounds__(256) void ipc_put_kernel(const PutDesc<T>* __restri
   if (m >= nmsg) return;
   const PutDesc<T> d = descs[m];
   const u64 k = *epoch + 1;
-  if (threadIdx.x == 0) s_ok = spin_ge(d.local_free, k - 1, timeout_ticks, status, 1) ? 1 : 0;
+  // The "peer consumed k-1" wait ran in ipc_free_wait_kernel (one workgroup),
+  // so the copy workgroups never hold CU slots while spinning.
+  if (threadIdx.x == 0) s_ok = __hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
   __syncthreads();
   if (!s_ok) return;
   const index_t begin = index_t(blockIdx.x) * kChunk;
@@ -103,6 +105,14 @@ __global__ __launch_bounds__(256) void ipc_put_kernel(const PutDesc<T>* __restri
       __hip_atomic_store(d.remote_ready, k, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+}
+
+// One workgroup: every outgoing message's peer has consumed exchange k-1.
+template <typename T>
+__global__ void ipc_free_wait_kernel(const PutDesc<T>* __restrict__ descs, int n, const u64* epoch, u64* status,
+                                     u64 timeout_ticks) {
+  const u64 k = *epoch + 1;
+  if (int(threadIdx.x) < n) spin_ge(descs[threadIdx.x].local_free, k - 1, timeout_ticks, status, 1);
 }
 
 __global__ void ipc_wait_kernel(const WaitDesc* __restrict__ descs, int n, const u64* epoch, u64* status,
@@ -313,6 +323,8 @@ void IpcHaloTransport<T>::put(hipStream_t s) {
   Impl& I = *impl_;
   if (!I.nput) return;
   MXS_TRACE_RANGE("halo.ipc_put");
+  ipc_free_wait_kernel<T><<<1, 64, 0, s>>>(I.put_d.get(), I.nput, I.ctrl + I.L.epoch(), I.ctrl + I.L.status(),
+                                            I.timeout_ticks);
   ipc_put_kernel<T><<<dim3(I.grid_x, unsigned(I.nput)), 256, 0, s>>>(I.put_d.get(), I.nput, I.ctrl + I.L.epoch(),
                                                                       I.ctrl + I.L.status(), I.timeout_ticks);
   MXS_HIP_CHECK_LAUNCH();

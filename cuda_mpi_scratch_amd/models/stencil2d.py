@@ -51,7 +51,7 @@ class StencilConfig:
     c_center: float = 0.2
     c_neighbor: float = 0.2
     backend: str = "auto"            # auto | rccl | ipc | local | torch
-    overlap: bool = True
+    overlap: bool | None = None      # None = auto (on, off for ranks sharing a GPU)
     graph: bool = True
     loopback: bool = False           # single GPU: send self-neighbour halos through RCCL
     variant: str = "auto"            # stencil kernel variant: auto | roll | lds
@@ -100,6 +100,8 @@ class Stencil2D:
         self._init_data()
         self.iteration = 0  # Jacobi iterations applied to the field (checkpoint header)
 
+        local = int(os.environ.get("LOCAL_WORLD_SIZE", self.ctx.world_size))
+        self.shared_gpu = dev.type == "cuda" and local > max(1, torch.cuda.device_count())
         backend = cfg.backend
         if dev.type != "cuda":
             backend = "torch"
@@ -108,8 +110,12 @@ class Stencil2D:
                 backend = "rccl" if cfg.loopback else "local"
             else:
                 # RCCL refuses two ranks on one GPU: ranks sharing GPUs use the IPC backend.
-                local = int(os.environ.get("LOCAL_WORLD_SIZE", self.ctx.world_size))
-                backend = "ipc" if local > max(1, torch.cuda.device_count()) else "rccl"
+                backend = "ipc" if self.shared_gpu else "rccl"
+        # overlap=None (auto): on, except for ranks sharing a GPU, whose
+        # cross-process waits plus the forked interior branch oversubscribe the
+        # GPU queues and get time-sliced (docs/PERF.md): they run the serial
+        # exchange + update schedule.
+        overlap = (not self.shared_gpu) if cfg.overlap is None else bool(cfg.overlap)
         self.backend = backend
         self.comm = None
         self.solver = None
@@ -125,7 +131,7 @@ class Stencil2D:
             weights = [float(w) for w in cfg.box_weights] if cfg.kind == "box" else []
             radius = (int(round(math.sqrt(len(weights)))) - 1) // 2 if weights else 1
             self.solver = H.StencilSolver(d.topo, d.rank, self.geom, self.a.data_ptr(), self.b.data_ptr(), self.comm,
-                                          cfg.dtype, be, cfg.overlap, cfg.graph, cfg.loopback, kind, cfg.c_center,
+                                          cfg.dtype, be, overlap, cfg.graph, cfg.loopback, kind, cfg.c_center,
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
                                           self.time_block, boot)
         else:
@@ -305,7 +311,7 @@ def main(argv=None) -> int:
     else:
         gw, gh = _parse_wh(args.global_ or "8192x8192")
     cfg = StencilConfig(global_width=gw, global_height=gh, dims=f"{rows}x{cols}", dtype=args.dtype,
-                        backend=args.backend, overlap=not args.no_overlap, graph=not args.no_graph,
+                        backend=args.backend, overlap=False if args.no_overlap else None, graph=not args.no_graph,
                         loopback=args.loopback, variant=args.variant, time_block=args.time_block,
                         seed=args.seed)
     st = Stencil2D(cfg, ctx)
