@@ -75,34 +75,64 @@ Variant tb1(const float* in, float* out, const TileGeom& g) {
   return v;
 }
 
-// tmp: scratch tile for the two-pass reference of S > 8 (wrap only: two periodic
-// half-blocks equal one block; without wrap the frozen ghost ring differs).
-template <int S, int PF, bool WRAP = false, bool SKEW = true, bool DPP = true>
+// Reference launcher for S-step variants: the validated LDS kernel (S <= 8), or
+// two periodic half-blocks through `tmp` (wrap only; without wrap the frozen
+// ghost ring differs).
+template <int S, bool WRAP>
+std::function<void(hipStream_t)> ref_for(const float* in, float* out, const TileGeom& g, float* tmp) {
+  if constexpr (S <= 8) {
+    return tb1<S, 128, 32, WRAP>(in, out, g).launch;
+  } else if constexpr (WRAP && S % 2 == 0) {
+    if (!tmp) return {};
+    auto first = tb1<S / 2, 128, 32, true>(in, tmp, g).launch;
+    auto second = tb1<S / 2, 128, 32, true>(tmp, out, g).launch;
+    return [=](hipStream_t s) {
+      first(s);
+      second(s);
+    };
+  } else {
+    return {};
+  }
+}
+
+template <int S, int PF, bool WRAP = false, bool DPP = true>
 Variant stream(const float* in, float* out, const TileGeom& g, int ch, float* tmp = nullptr) {
   char buf[128];
-  std::snprintf(buf, sizeof(buf), "stream_s%d_pf%d_ch%d%s%s%s", S, PF, ch, WRAP ? "_wrap" : "", SKEW ? "" : "_chain",
-                DPP ? "" : "_bperm");
+  std::snprintf(buf, sizeof(buf), "stream_s%d_pf%d_ch%d%s%s", S, PF, ch, WRAP ? "_wrap" : "", DPP ? "" : "_bperm");
   Variant v{buf, [=](hipStream_t s) {
               constexpr int OW = StreamShape<float, S>::OW;
               const index_t strips = (g.width + OW - 1) / OW;
               const dim3 grid(unsigned((strips + 3) / 4), unsigned((g.height + ch - 1) / ch));
-              stencil5_stream_kernel<float, S, PF, WRAP, SKEW, DPP><<<grid, 256, 0, s>>>(
+              stencil5_stream_kernel<float, S, PF, WRAP, DPP><<<grid, 256, 0, s>>>(
                   in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, index_t(ch), 0.2f,
                   0.2f);
             }};
   v.steps = S;
-  if constexpr (S <= 8) {
-    v.ref = tb1<S, 128, 32, WRAP>(in, out, g).launch;
-  } else if constexpr (WRAP && S % 2 == 0) {
-    if (tmp) {
-      auto first = tb1<S / 2, 128, 32, true>(in, tmp, g).launch;
-      auto second = tb1<S / 2, 128, 32, true>(tmp, out, g).launch;
-      v.ref = [=](hipStream_t s) {
-        first(s);
-        second(s);
-      };
-    }
-  }
+  v.ref = ref_for<S, WRAP>(in, out, g, tmp);
+  return v;
+}
+
+// Balanced persistent launch: `per_cu` resident workgroups per CU (0 = occupancy API).
+template <int S, int PF, bool WRAP = false>
+Variant balanced(const float* in, float* out, const TileGeom& g, int per_cu, float* tmp = nullptr) {
+  int blocks_per_cu = per_cu;
+  if (blocks_per_cu <= 0)
+    MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &blocks_per_cu, reinterpret_cast<const void*>(stencil5_stream_balanced_kernel<float, S, PF, WRAP>), 256, 0));
+  int cus = 0;
+  MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const int blocks = std::max(1, blocks_per_cu * cus);
+  char buf[128];
+  std::snprintf(buf, sizeof(buf), "balanced_s%d_pf%d_b%d%s", S, PF, blocks_per_cu, WRAP ? "_wrap" : "");
+  Variant v{buf, [=](hipStream_t s) {
+              constexpr int OW = StreamShape<float, S>::OW;
+              const index_t groups = ((g.width + OW - 1) / OW + 3) / 4;
+              const index_t share = (groups * g.height + blocks - 1) / blocks;
+              stencil5_stream_balanced_kernel<float, S, PF, WRAP><<<blocks, 256, 0, s>>>(
+                  in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, 0.2f, 0.2f);
+            }};
+  v.steps = S;
+  v.ref = ref_for<S, WRAP>(in, out, g, tmp);
   return v;
 }
 
@@ -138,15 +168,17 @@ int main(int argc, char** argv) {
   vs.push_back(tb1<4, 192, 24, false>(in, out, g));
   vs.push_back(tb1<6, 128, 32, false>(in, out, g));
   float* tmp = c.get();
-  for (int ch : {64, 128, 256, 512}) {
-    vs.push_back(stream<8, 3>(in, out, g, ch));
-    vs.push_back(stream<8, 3, false, true, false>(in, out, g, ch));
+  for (int ch : {128, 256, 512}) {
     vs.push_back(stream<12, 3>(in, out, g, ch));
-    vs.push_back(stream<12, 3, false, true, false>(in, out, g, ch));
     vs.push_back(stream<12, 3, true>(in, out, g, ch, tmp));
-    vs.push_back(stream<12, 3, true, true, false>(in, out, g, ch, tmp));
-    vs.push_back(stream<16, 3, true>(in, out, g, ch, tmp));
   }
+  for (int per_cu : {0, 1, 3}) {
+    vs.push_back(balanced<12, 3>(in, out, g, per_cu));
+    vs.push_back(balanced<12, 3, true>(in, out, g, per_cu, tmp));
+  }
+  vs.push_back(balanced<8, 3, true>(in, out, g, 0));
+  vs.push_back(balanced<16, 3, true>(in, out, g, 0, tmp));
+  vs.push_back(balanced<16, 3, true>(in, out, g, 2, tmp));
 
   Stream st;
   Event e0(true), e1(true);

@@ -126,20 +126,47 @@ void launch_tb_tile(const T* in, T* out, const TileGeom& g, index_t x0, index_t 
                                                                  g.height, x0, x1, y0, y1, c0, c1);
 }
 
-// Wave-streaming kernel (stencil_device.hpp). Row chunk CH: the largest of
-// 512..64 that still yields >= 4096 waves (4 per SIMD); a chunk recomputes 2S
-// rows of apron, so tall chunks pay less, short ones fill the chip. Tuned with
-// bench/stencil_tune.hip (profiles/stencil_tuning/tune12-13): 32768^2 -> 512,
-// 8192 x 16384 -> 128, 8192^2 -> 64.
+// Workgroups of the balanced stream kernel resident at once on this device:
+// occupancy x CUs, at least 2 per CU (at S = 16, 1 fits; two rounds of
+// half-size shares still beat one round: profiles/stencil_tuning/tune16).
+template <typename T, int S, bool WRAP>
+int balanced_blocks() {
+  static int blocks = 0;
+  if (blocks == 0) {
+    int occ = 0, cus = 0, dev = 0;
+    MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, reinterpret_cast<const void*>(stencil5_stream_balanced_kernel<T, S, 3, WRAP>), kBlock, 0));
+    MXS_HIP_CHECK(hipGetDevice(&dev));
+    MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    blocks = std::max(occ, 2) * std::max(cus, 1);
+  }
+  return blocks;
+}
+
+// Wave-streaming kernels (stencil_device.hpp). Bulk rectangles: the balanced
+// persistent launch — as many workgroups as are resident, each streaming an
+// equal share of (4-strip group) x rows (profiles/stencil_tuning/tune16: +12-17%
+// over the grid form on 8192^2 and on the 8-GPU tile 8192 x 16384, equal on
+// 32768^2). Rectangles too small to give every workgroup >= 64 rows use the
+// grid form, whose row chunk CH is the largest of 512..64 that still yields
+// >= 4096 waves.
 template <typename T, int S, bool WRAP>
 void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
                    hipStream_t s) {
   constexpr int OW = StreamShape<T, S>::OW;
   const index_t strips = (x1 - x0 + OW - 1) / OW;
   const index_t rows = y1 - y0;
+  const index_t groups = (strips + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int blocks = balanced_blocks<T, S, WRAP>();
+  if (groups * rows >= index_t(blocks) * 64) {
+    const index_t share = (groups * rows + blocks - 1) / blocks;
+    stencil5_stream_balanced_kernel<T, S, 3, WRAP><<<blocks, kBlock, 0, s>>>(
+        in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
+    return;
+  }
   index_t ch = 512;
   while (ch > 64 && strips * ((rows + ch - 1) / ch) < 4096) ch /= 2;
-  const dim3 grid(unsigned((strips + kWavesPerBlock - 1) / kWavesPerBlock), unsigned((rows + ch - 1) / ch));
+  const dim3 grid(unsigned(groups), unsigned((rows + ch - 1) / ch));
   stencil5_stream_kernel<T, S, 3, WRAP><<<grid, kBlock, 0, s>>>(in, out, g.pitch, g.core_offset(), g.width, g.height,
                                                                 x0, x1, y0, y1, ch, c0, c1);
 }

@@ -612,23 +612,26 @@ struct StreamShape {
   static constexpr int OW = kWaveSize * N - 2 * SA;     // output columns per wave
 };
 
-// Workgroup = 4 waves on 4 adjacent strips of the same row chunk. PF = input
-// rows in flight per wave (a register ring, statically indexed; multiple of 3).
-template <typename T, int S, int PF, bool WRAP, bool SKEW = true, bool DPP = true>
-__global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __restrict__ in, T* __restrict__ out,
-                                                                 index_t pitch, index_t core_off, index_t W, index_t H,
-                                                                 index_t x_begin, index_t x_end, index_t y_begin,
-                                                                 index_t y_end, index_t CH, T c0, T c1) {
+// One wave streams output rows [ys, ye) of the column strip whose first output
+// column is xw. PF = input rows in flight (a register ring, statically indexed;
+// a multiple of 3, the window's slot period).
+//
+// Skewed schedule: in iteration j level l works on the row level l-1 made in
+// iteration j-1, so the S levels of one iteration are independent (S-way ILP
+// instead of an S-long dependent chain of cross-lane move -> VALU). Slots per
+// level rotate with the phase p = j % 3: up = win[p], mid = win[p+1],
+// dn = win[p+2]; level l writes its output into win[p][l+1], the slot that is
+// level l+1's dn next iteration, after level l+1 has read it as up (so levels
+// run top-down). Level S-1 outputs row y_first + j - 2S + 1.
+template <typename T, int S, int PF, bool WRAP, bool DPP>
+__device__ __forceinline__ void stream_chunk(const T* __restrict__ in, T* __restrict__ out, index_t pitch,
+                                             index_t core_off, index_t W, index_t H, index_t xw, index_t x_end,
+                                             index_t ys, index_t ye, T c0, T c1) {
   static_assert(PF % 3 == 0, "the window rotates through 3 slots: PF must be a multiple of 3");
   using Sh = StreamShape<T, S>;
-  constexpr int N = Sh::N, SA = Sh::SA, OW = Sh::OW, AL = SA / N;
+  constexpr int N = Sh::N, SA = Sh::SA, AL = SA / N;
   using V = typename Vec16<T>::type;
   const int lane = threadIdx.x & (kWaveSize - 1);
-  const int wave = threadIdx.x / kWaveSize;
-  const index_t xw = x_begin + (index_t(blockIdx.x) * kWavesPerBlock + wave) * OW;
-  if (xw >= x_end) return;  // wave-uniform
-  const index_t ys = y_begin + index_t(blockIdx.y) * CH;
-  const index_t ye = ys + CH < y_end ? ys + CH : y_end;
   const index_t gx = xw - SA + index_t(lane) * N;
 
   index_t lx = gx;
@@ -656,7 +659,7 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __rest
     if constexpr (WRAP) next = next == H ? 0 : next;
     return v;
   };
-  T* __restrict__ pout = out + core_off + gx + ys * pitch;  // row of the first output (input j = 2S)
+  T* __restrict__ pout = out + core_off + gx + ys * pitch;  // first output row
 
   V win[3][S];
 #pragma unroll
@@ -665,83 +668,86 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __rest
     for (int l = 0; l < S; ++l) win[q][l] = V(T(0));
 
   const index_t n_in = (ye - ys) + 2 * S;
+  const index_t n_it = (ye - ys) + 3 * S - 1;
   V pf[PF];
 #pragma unroll
   for (int k = 0; k < PF; ++k) pf[k] = k < n_in ? fetch() : V(T(0));
-
-  if constexpr (SKEW) {
-    // Skewed schedule: in iteration j level l works on the row level l-1 made in
-    // iteration j-1, so the S levels of one iteration are independent (S-way
-    // ILP instead of an S-long dependent chain of bpermute -> VALU). Slots per
-    // level rotate with the phase p = j % 3: up = win[p], mid = win[p+1],
-    // dn = win[p+2]; level l writes its output into win[p][l+1], the slot that
-    // is level l+1's dn next iteration, after level l+1 has read it as up (so
-    // levels run top-down). Level S-1 outputs row y_first + j - 2S + 1.
-    const index_t n_it = (ye - ys) + 3 * S - 1;
 #pragma unroll 1
-    for (index_t i = 0; i < n_it; i += PF) {
-#pragma unroll
-      for (int k = 0; k < PF; ++k) {
-        const index_t j = i + k;
-        if (j < n_it) {
-          const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;  // static after the unroll
-          win[p2][0] = pf[k];
-          if (j + PF < n_in) pf[k] = fetch();
-          V top = V(T(0));
-#pragma unroll
-          for (int l = S - 1; l >= 0; --l) {
-            const V m = win[p1][l];
-            const T left = DPP ? lane_shift<T, kDppWaveShr1>(m[N - 1]) : lane_fetch<T>(m[N - 1], addr_l);
-            const T right = DPP ? lane_shift<T, kDppWaveShl1>(m[0]) : lane_fetch<T>(m[0], addr_r);
-            const V o = jac_row<T, V>(win[p0][l], m, win[p2][l], left, right, c0, c1);
-            if (l == S - 1) top = o;
-            else win[p0][l + 1] = o;
-          }
-          if (j >= 3 * S - 1 && store_lane) {  // row ys + (j - 3S + 1)
-            T* p = pout + (j - (3 * S - 1)) * pitch;
-            if (full_vec) {
-              __builtin_nontemporal_store(top, reinterpret_cast<V*>(p));
-            } else {
-#pragma unroll
-              for (int q = 0; q < N; ++q)
-                if (gx + q < x_end) p[q] = top[q];
-            }
-          }
-        }
-      }
-    }
-    return;
-  }
-#pragma unroll 1
-  for (index_t i = 0; i < n_in; i += PF) {
+  for (index_t i = 0; i < n_it; i += PF) {
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
       const index_t j = i + k;
-      if (j < n_in) {
-        V nw = pf[k];
-        if (j + PF < n_in) pf[k] = fetch();
+      if (j < n_it) {
         const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;  // static after the unroll
+        win[p2][0] = pf[k];
+        if (j + PF < n_in) pf[k] = fetch();
+        V top = V(T(0));
 #pragma unroll
-        for (int l = 0; l < S; ++l) {
+        for (int l = S - 1; l >= 0; --l) {
           const V m = win[p1][l];
-          const T left = lane_fetch<T>(m[N - 1], addr_l);
-          const T right = lane_fetch<T>(m[0], addr_r);
-          const V o = jac_row<T, V>(win[p0][l], m, nw, left, right, c0, c1);
-          win[p2][l] = nw;
-          nw = o;
+          const T left = DPP ? lane_shift<T, kDppWaveShr1>(m[N - 1]) : lane_fetch<T>(m[N - 1], addr_l);
+          const T right = DPP ? lane_shift<T, kDppWaveShl1>(m[0]) : lane_fetch<T>(m[0], addr_r);
+          const V o = jac_row<T, V>(win[p0][l], m, win[p2][l], left, right, c0, c1);
+          if (l == S - 1) top = o;
+          else win[p0][l + 1] = o;
         }
-        if (j >= 2 * S && store_lane) {  // level-S row ys + (j - 2S)
-          T* p = pout + (j - 2 * S) * pitch;
+        if (j >= 3 * S - 1 && store_lane) {  // row ys + (j - 3S + 1)
+          T* p = pout + (j - (3 * S - 1)) * pitch;
           if (full_vec) {
-            __builtin_nontemporal_store(nw, reinterpret_cast<V*>(p));
+            __builtin_nontemporal_store(top, reinterpret_cast<V*>(p));
           } else {
 #pragma unroll
             for (int q = 0; q < N; ++q)
-              if (gx + q < x_end) p[q] = nw[q];
+              if (gx + q < x_end) p[q] = top[q];
           }
         }
       }
     }
+  }
+}
+
+// Grid form: workgroup = 4 waves on 4 adjacent strips of the same CH-row chunk.
+template <typename T, int S, int PF, bool WRAP, bool DPP = true>
+__global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                                 index_t pitch, index_t core_off, index_t W, index_t H,
+                                                                 index_t x_begin, index_t x_end, index_t y_begin,
+                                                                 index_t y_end, index_t CH, T c0, T c1) {
+  constexpr int OW = StreamShape<T, S>::OW;
+  const index_t xw = x_begin + (index_t(blockIdx.x) * kWavesPerBlock + threadIdx.x / kWaveSize) * OW;
+  if (xw >= x_end) return;  // wave-uniform
+  const index_t ys = y_begin + index_t(blockIdx.y) * CH;
+  const index_t ye = ys + CH < y_end ? ys + CH : y_end;
+  stream_chunk<T, S, PF, WRAP, DPP>(in, out, pitch, core_off, W, H, xw, x_end, ys, ye, c0, c1);
+}
+
+// Balanced persistent form: exactly as many workgroups as fit on the chip at
+// once. The work is (group of 4 adjacent strips) x rows, split into equal
+// shares of rows per workgroup (group-major); a workgroup's 4 waves stream the
+// 4 strips of its group over the same rows side by side — as in the grid form,
+// so the apron columns two neighbouring waves both read are L2 hits — and a
+// share that crosses a group boundary restarts there. No tail round, and
+// (3S-1)/share redundant rows instead of (3S-1)/CH per chunk.
+template <typename T, int S, int PF, bool WRAP, bool DPP = true>
+__global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
+    const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
+    index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
+  constexpr int OW = StreamShape<T, S>::OW;
+  const index_t rows = y_end - y_begin;
+  const index_t strips = (x_end - x_begin + OW - 1) / OW;
+  const index_t groups = (strips + kWavesPerBlock - 1) / kWavesPerBlock;
+  const index_t total = groups * rows;
+  const int wave = threadIdx.x / kWaveSize;
+  index_t a = index_t(blockIdx.x) * share;
+  const index_t b = a + share < total ? a + share : total;
+#pragma unroll 1
+  while (a < b) {  // workgroup-uniform
+    const index_t grp = a / rows, r0 = a - grp * rows;
+    const index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
+    const index_t xw = x_begin + (grp * kWavesPerBlock + wave) * OW;
+    if (xw < x_end)
+      stream_chunk<T, S, PF, WRAP, DPP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0,
+                                        c1);
+    a += r1 - r0;
   }
 }
 
