@@ -4,26 +4,28 @@
 //
 // Time blocking (`time_block` = S, Jacobi5): every super-step exchanges an
 // S-deep halo (same bytes per iteration as S 1-deep exchanges, S x fewer
-// latency-bound messages) and then advances S iterations in one LDS-tiled launch
-// (kernels::stencil5_tb: ~S x less HBM traffic per iteration). S = 1 is the
-// classic one-exchange-per-iteration loop. Results are bitwise identical for any S.
+// latency-bound messages) and then advances S iterations in one pass over HBM
+// (kernels::stencil5_tb: the wave-streaming kernel, ~S x less HBM traffic per
+// iteration). S = 1 is the classic one-exchange-per-iteration loop. Results are
+// bitwise identical for any S. A remainder (iters mod S) runs as one shorter block.
 //
-// Per super-step (cur -> nxt), with `overlap` on:
+// Per super-step (cur -> nxt), with `overlap` on and S > 1:
 //
-//   main stream : record(fork) -> pack(cur) -> RCCL send/recv -> unpack(cur) -> wait(interior)
-//                 -> boundary rows [0, S) and [H-S, H), boundary columns [0, S) and [W-S, W)
-//   side stream : wait(fork) -> interior rows [S, H-S) of nxt -> record(interior)
+//   main stream : record(fork) -> pack(cur) -> wire (RCCL send/recv or IPC put/wait)
+//                 -> unpack(cur) -> boundary rows [0, S), [H-S, H) and columns
+//                 [0, S'), [W-S', W) (S' = S rounded to the vector width)
+//                 -> wait(interior)
+//   side stream : wait(fork) -> interior rows [S, H-S) x columns [S', W-S') of nxt
+//                 -> record(interior)
 //
-// (RCCL must run on the capture-origin stream, so the exchange chain stays on
-// the main stream and the long interior sweep is the forked branch.)
-//
-// The interior launch covers full rows, so its first/last S columns read ghost
-// columns that the unpack may be writing concurrently; those output columns are
-// recomputed by the boundary launch after the halo has landed, so the race is
-// benign by construction (it only ever produces values that are overwritten).
-// Without `overlap` (or with nothing to hide) the super-step is exchange + one
-// full launch on the main stream. A 1x1 periodic grid fuses the self-exchange
-// into the kernel's wrap-around addressing (`fuse_periodic_self`).
+// Interior and boundary write disjoint cells, so the boundary strips start as
+// soon as the halo has landed, concurrently with the interior. (RCCL must run on
+// the capture-origin stream, so the exchange chain stays on the main stream and
+// the long interior sweep is the forked branch.) S = 1 keeps the full-row
+// interior and redoes the edge columns after the join. Without `overlap` the
+// super-step is exchange + one full launch on the main stream. A 1x1 periodic
+// grid fuses the self-exchange into the kernel's wrap-around addressing
+// (`fuse_periodic_self`).
 //
 // `use_graph`: the super-step is captured once per buffer orientation into a
 // hipGraph and replayed (launch-bound inner loops, Guideline 9). If capture fails

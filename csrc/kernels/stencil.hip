@@ -3,10 +3,13 @@
 //
 // Regime: a 5-point Jacobi sweep moves 2 x sizeof(T) bytes of compulsory HBM
 // traffic per cell (read u, write u') for ~6 flops: HBM-bound by two orders of
-// magnitude. The design goal is therefore "every input byte crosses HBM once,
-// with enough bytes in flight per CU", not arithmetic.
+// magnitude. One sweep per iteration therefore tops out at the copy roofline
+// (~0.7 T cells/s fp32); the framework's default path is temporal blocking
+// (stencil5_tb below: the wave-streaming kernels of stencil_device.hpp advance
+// S iterations per pass over HBM, ~6 T cells/s at S = 12). The single-sweep
+// kernels remain for S = 1, remainders and box stencils:
 //
-// Variant RegisterRoll (default):
+// Variant RegisterRoll (single sweep, default):
 //   * a wave owns a 64 x VEC column segment (VEC = 16 B / sizeof(T): 256 fp32
 //     or 128 fp64 columns) and a strip of ROWS rows;
 //   * each lane issues one 16-byte load per row (global_load_dwordx4, a whole
