@@ -18,7 +18,7 @@
 //
 // Positional arguments keep the reference contract: [local width (= height) [stencil width]].
 // More options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
-// --iters N, --warmup N, --time-block S (default 12 on timed runs), --no-overlap, --no-graph,
+// --iters N, --warmup N, --time-block S (default: measured per tile size, 12 or 16), --no-overlap, --no-graph,
 // --loopback, --bind bunch|rrobin,
 // --dump / --no-dump, --checksum, --non-periodic, --seed S, --json FILE,
 // --checkpoint FILE / --resume FILE (collective MPI-IO global grid file, any
@@ -79,7 +79,9 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   // Temporal blocking (timed runs on the solver backends): S Jacobi steps per
   // launch on an S-deep ghost ring exchanged once per S steps.
   const int time_block =
-      backend == "mpi-staged" ? 1 : int(cli.get_int("time-block", iters > 0 && lw >= 64 && lh >= 64 ? 12 : 1));
+      backend == "mpi-staged"
+          ? 1
+          : int(cli.get_int("time-block", iters > 0 && lw >= 64 && lh >= 64 ? kernels::auto_time_block(lw, lh) : 1));
   const TileGeom g = TileGeom::aligned(lw, lh, std::max(sw / 2, time_block), std::max(sh / 2, time_block),
                                        int(sizeof(T)));
   std::unique_ptr<RcclComm> comm;
@@ -92,12 +94,14 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   SolverConfig cfg;
   cfg.backend = backend == "rccl" ? HaloBackend::Rccl : backend == "ipc" ? HaloBackend::Ipc : HaloBackend::Local;
   if (backend == "ipc") cfg.bootstrap = [](const std::string& b) { return mpi_allgather_bytes(MPI_COMM_WORLD, b); };
-  // Ranks sharing a GPU: their cross-process waits plus the forked interior
-  // branch oversubscribe the GPU's queues and the scheduler time-slices them
-  // (ms-scale stalls, measured: 3-28 vs ~3000 Gcells/s with overlap off), so
-  // co-located ranks default to the serial exchange + update schedule.
+  // Overlap (interior on a forked stream while the halo moves) defaults on only
+  // for one-exchange-per-iteration runs: with temporal blocking the exchange is
+  // ~5-8% of a super-step and the concurrent thin boundary strips cost more than
+  // they hide (docs/PERF.md). Ranks sharing a GPU never overlap by default: their
+  // cross-process waits plus the forked branch oversubscribe the GPU's queues and
+  // get time-sliced (measured: 3-28 vs ~3000 Gcells/s).
   const bool shared_gpu = env.local_size() > dev.devices_used;
-  cfg.overlap = cli.flag("overlap") || (!cli.flag("no-overlap") && !shared_gpu);
+  cfg.overlap = cli.flag("overlap") || (!cli.flag("no-overlap") && !shared_gpu && time_block == 1);
   cfg.use_graph = !cli.flag("no-graph");
   cfg.loopback_self = loopback;
   cfg.coeffs = {cli.get_double("c-center", 0.2), cli.get_double("c-neighbor", 0.2)};

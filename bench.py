@@ -5,12 +5,15 @@ BASELINE.json metric: "2D stencil Gcells/sec at 1/2/4/8 GPUs; GPU-GPU pingpong
 GB/s + µs latency". Config: the BASELINE 8-GPU problem — a 32768 x 32768 fp32
 periodic grid, 5-point Jacobi, decomposed over a Cartesian process grid (2x4 on
 8 GPUs; 1x1, 1x2, 2x2 below), halo exchange by native RCCL point-to-point over
-xGMI overlapped with the interior update. The global grid is fixed as N grows
+xGMI (pack -> per-peer send/recv -> unpack, captured in a hipGraph with the
+update; `--overlap` forks the interior onto a second stream, the default only
+when --time-block 1). The global grid is fixed as N grows
 (strong scaling). Random-init synthetic data (deterministic per global cell).
 
 One step = one full Jacobi iteration of the global grid: every core cell is
 updated every step. Halos are exchanged communication-avoiding style: an
-S-deep ghost ring (S = --time-block, default 12) is exchanged once per S steps
+S-deep ghost ring (S = --time-block; default 16 for tiles of >= 2^27 cells,
+12 below, as measured) is exchanged once per S steps
 (pack -> RCCL send/recv per peer -> unpack) and the wave-streaming kernel runs
 the S steps in one pass over HBM; the result is bitwise identical to one 1-deep
 exchange + one sweep per step (tests/test_gpu_solver.py). W untimed warm-up
@@ -69,8 +72,10 @@ def main(argv=None) -> int:
     p.add_argument("--dims", default=None, help="process grid RxC (default: 1x1, 1x2, 2x2, 2x4)")
     p.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     p.add_argument("--variant", default="auto", choices=["auto", "roll", "lds"])
-    p.add_argument("--time-block", type=int, default=12, help="Jacobi steps per halo exchange / kernel pass")
+    p.add_argument("--time-block", type=int, default=0,
+                   help="Jacobi steps per halo exchange / kernel pass (0 = measured default per tile: 12 or 16)")
     p.add_argument("--no-overlap", action="store_true")
+    p.add_argument("--overlap", action="store_true", help="force the interior/exchange overlap schedule")
     p.add_argument("--loopback", action="store_true",
                    help="1 GPU: route the self-neighbour halos through RCCL (exercises the multi-GPU schedule)")
     p.add_argument("--no-graph", action="store_true")
@@ -88,7 +93,8 @@ def main(argv=None) -> int:
     rows, cols = choose_dims(n, args.dims, prefer="wide")
     gw, gh = (int(v) for v in args.global_.lower().split("x"))
     cfg = StencilConfig(global_width=gw, global_height=gh, dims=f"{rows}x{cols}", dtype=args.dtype,
-                        kind="jacobi5", backend="auto", overlap=False if args.no_overlap else None,
+                        kind="jacobi5", backend="auto",
+                        overlap=False if args.no_overlap else (True if args.overlap else None),
                         graph=not args.no_graph,
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback)
     st = Stencil2D(cfg, ctx)

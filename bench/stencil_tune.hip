@@ -168,17 +168,27 @@ int main(int argc, char** argv) {
   vs.push_back(tb1<4, 192, 24, false>(in, out, g));
   vs.push_back(tb1<6, 128, 32, false>(in, out, g));
   float* tmp = c.get();
-  for (int ch : {128, 256, 512}) {
-    vs.push_back(stream<12, 3>(in, out, g, ch));
-    vs.push_back(stream<12, 3, true>(in, out, g, ch, tmp));
+  const char* focus = std::getenv("TUNE_FOCUS");
+  if (focus && std::string(focus) == "s") {  // S choice for the balanced launch
+    vs.push_back(balanced<12, 3>(in, out, g, 0));
+    vs.push_back(balanced<12, 3, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<16, 3>(in, out, g, 2));
+    vs.push_back(balanced<16, 3, true>(in, out, g, 2, tmp));
+    vs.push_back(balanced<14, 3, true>(in, out, g, 2, tmp));
+    vs.push_back(balanced<10, 3, true>(in, out, g, 0, tmp));
+  } else {
+    for (int ch : {128, 256, 512}) {
+      vs.push_back(stream<12, 3>(in, out, g, ch));
+      vs.push_back(stream<12, 3, true>(in, out, g, ch, tmp));
+    }
+    for (int per_cu : {0, 1, 3}) {
+      vs.push_back(balanced<12, 3>(in, out, g, per_cu));
+      vs.push_back(balanced<12, 3, true>(in, out, g, per_cu, tmp));
+    }
+    vs.push_back(balanced<8, 3, true>(in, out, g, 0));
+    vs.push_back(balanced<16, 3, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<16, 3, true>(in, out, g, 2, tmp));
   }
-  for (int per_cu : {0, 1, 3}) {
-    vs.push_back(balanced<12, 3>(in, out, g, per_cu));
-    vs.push_back(balanced<12, 3, true>(in, out, g, per_cu, tmp));
-  }
-  vs.push_back(balanced<8, 3, true>(in, out, g, 0));
-  vs.push_back(balanced<16, 3, true>(in, out, g, 0, tmp));
-  vs.push_back(balanced<16, 3, true>(in, out, g, 2, tmp));
 
   Stream st;
   Event e0(true), e1(true);

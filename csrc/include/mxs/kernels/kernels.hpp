@@ -74,6 +74,11 @@ bool stencil5_periodic_supported(const TileGeom& g);
 //                iterates in LDS; S <= 8 for the bulk tile);
 //   RegisterRoll same as Auto.
 constexpr int kMaxTimeBlock = 16;
+// Measured default S for a w x h tile (profiles/stencil_tuning/tunes_*): the
+// wave-streaming pass is VALU-bound beyond S ~ 8, so a deeper block only pays
+// where the chunk/strip aprons are small against the tile: S = 16 from 2^27
+// cells (8192 x 16384: tie, 16384^2 and up: +8-12%), S = 12 below (8192^2: +5%).
+inline int auto_time_block(index_t w, index_t h) { return w * h >= (index_t(1) << 27) ? 16 : 12; }
 template <typename T>
 void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0, index_t y1,
                  Stencil5Coeffs c, bool wrap, hipStream_t s, StencilVariant v = StencilVariant::Auto);

@@ -157,6 +157,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("row_begin"), py::arg("row_end"),
       py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2, py::arg("dtype") = "f32", py::arg("stream") = 0,
       py::arg("variant") = "auto");
+  m.def("auto_time_block", &kernels::auto_time_block, py::arg("width"), py::arg("height"),
+        "measured default Jacobi steps per pass / halo exchange for a tile");
   m.def(
       "stencil5_tb",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0,

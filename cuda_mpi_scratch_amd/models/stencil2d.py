@@ -51,15 +51,16 @@ class StencilConfig:
     c_center: float = 0.2
     c_neighbor: float = 0.2
     backend: str = "auto"            # auto | rccl | ipc | local | torch
-    overlap: bool | None = None      # None = auto (on, off for ranks sharing a GPU)
+    overlap: bool | None = None      # None = auto (on only for time_block 1 on unshared GPUs)
     graph: bool = True
     loopback: bool = False           # single GPU: send self-neighbour halos through RCCL
     variant: str = "auto"            # stencil kernel variant: auto | roll | lds
     fuse_periodic: bool = True       # 1x1 periodic: fuse the self-exchange into the kernel addressing
-    # Jacobi iterations per halo exchange and per temporally blocked launch on GPU
+    # Jacobi iterations per halo exchange and per temporally blocked pass on GPU
     # (wave-streaming kernel); the ghost ring is made this deep. 1 = one exchange
-    # per iteration. 12 is the measured optimum on MI355X (docs/PERF.md).
-    time_block: int = 12
+    # per iteration; 0 = the measured optimum for the tile (12, or 16 from 2^27
+    # cells: kernels::auto_time_block, docs/PERF.md).
+    time_block: int = 0
     seed: int = 1234
     init: str = "random"             # random | rank
 
@@ -86,7 +87,10 @@ class Stencil2D:
         # Temporal blocking only for the GPU Jacobi solver and not for the reference's
         # exchange-only run (its dumps show a stencil_width/2 ghost ring).
         # A ghost ring deeper than a neighbour's tile would need cells two tiles away.
-        self.time_block = (max(1, min(cfg.time_block, d.width, d.height))
+        tb = cfg.time_block
+        if tb <= 0 and dev.type == "cuda":
+            tb = hip().auto_time_block(d.width, d.height)
+        self.time_block = (max(1, min(tb, d.width, d.height))
                            if (dev.type == "cuda" and cfg.kind == "jacobi5" and cfg.init != "rank") else 1)
         h = max(h, self.time_block)
         C = core()
@@ -111,11 +115,13 @@ class Stencil2D:
             else:
                 # RCCL refuses two ranks on one GPU: ranks sharing GPUs use the IPC backend.
                 backend = "ipc" if self.shared_gpu else "rccl"
-        # overlap=None (auto): on, except for ranks sharing a GPU, whose
-        # cross-process waits plus the forked interior branch oversubscribe the
-        # GPU queues and get time-sliced (docs/PERF.md): they run the serial
-        # exchange + update schedule.
-        overlap = (not self.shared_gpu) if cfg.overlap is None else bool(cfg.overlap)
+        # overlap=None (auto): only for one-exchange-per-iteration runs (S = 1).
+        # With temporal blocking the exchange is ~5-8% of a super-step and the
+        # concurrent thin boundary strips cost more than they hide (docs/PERF.md,
+        # "Multi-GPU schedule"); ranks sharing a GPU never overlap (their
+        # cross-process waits + a forked branch oversubscribe the GPU queues).
+        auto_overlap = self.time_block == 1 and not self.shared_gpu
+        overlap = auto_overlap if cfg.overlap is None else bool(cfg.overlap)
         self.backend = backend
         self.comm = None
         self.solver = None

@@ -10,6 +10,7 @@ run() {
 }
 run fused     --global 8192x16384
 run loop      --global 8192x16384 --loopback
-run loop_noov --global 8192x16384 --loopback --no-overlap
+run loop_ov   --global 8192x16384 --loopback --overlap
 run loop_tb1  --global 8192x16384 --loopback --time-block 1
 run loop_tb4  --global 8192x16384 --loopback --time-block 4
+run loop_tb12 --global 8192x16384 --loopback --time-block 12
