@@ -98,6 +98,18 @@ def task_gpu_solver(args):
     return out
 
 
+def task_pingpong(args):
+    """PingPong between ranks 0 and 1 (GPU transports: rccl / ipc)."""
+    from cuda_mpi_scratch_amd.models.pingpong import PingPong
+
+    ctx = init(backend=args.get("pg_backend", "gloo"), device="cuda")
+    pp = PingPong(ctx, args["transport"], max(args["sizes"]))
+    recs = [pp.run(n, args.get("mode", "async"), 2, 10) for n in args["sizes"]]
+    ctx.barrier()
+    ctx.destroy()
+    return {"rank": ctx.rank, "device": str(ctx.device), "records": recs}
+
+
 def task_halo_property(args):
     """Non-square tiles and grids: after one exchange every ghost cell holds the
     owning neighbour's core value (cell value = global linear index)."""

@@ -1,0 +1,39 @@
+"""Multi-GPU tests: one process per GPU, RCCL over xGMI and
+HIP IPC between GPUs. They need >= 2 GPUs and skip on the 1-GPU box, where the
+same plans and schedules are covered by the IPC backend with ranks sharing the
+GPU (tests/test_gpu_multirank.py) and by RCCL loopback (tests/test_gpu_solver.py)."""
+import pytest
+import torch
+
+from cuda_mpi_scratch_amd.ops import jacobi_reference_global, random_values
+from tests.mp_util import run_ranks
+
+NGPU = torch.cuda.device_count() if torch.cuda.is_available() else 0
+pytestmark = [pytest.mark.gpu, pytest.mark.multigpu,
+              pytest.mark.skipif(NGPU < 2, reason="needs >= 2 GPUs")]
+
+GRIDS = [(2, "1x2"), (2, "2x1"), (4, "2x2"), (8, "2x4")]
+
+
+@pytest.mark.parametrize("n,dims", [g for g in GRIDS if g[0] <= NGPU])
+@pytest.mark.parametrize("backend", ["rccl", "ipc"])
+@pytest.mark.parametrize("time_block,overlap", [(16, False), (12, True), (1, True)])
+def test_solver_one_rank_per_gpu(gpu, n, dims, backend, time_block, overlap):
+    w, h, iters, seed = 520, 392, 37, 11
+    res = run_ranks("gpu_solver", n, {"w": w, "h": h, "dims": dims, "iters": iters, "seed": seed,
+                                      "backend": backend, "time_block": time_block, "overlap": overlap},
+                    gpu=True, timeout=600)
+    assert all(r["native"] and r["backend"] == backend for r in res)
+    got = torch.tensor(res[0]["grid"], dtype=torch.float64)
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), iters).double()
+    assert (got - ref).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("transport", ["rccl", "ipc"])
+def test_pingpong_two_gpus(gpu, transport):
+    res = run_ranks("pingpong", 2, {"transport": transport, "sizes": [8, 4099, 1 << 20, 64 << 20]}, gpu=True,
+                    timeout=600)
+    assert res[0]["device"] != res[1]["device"]
+    for rec in res[0]["records"]:
+        assert rec["passed"], rec
+        assert rec["latency_us"] > 0
