@@ -26,6 +26,16 @@ inline void append_json(const std::string& path, const std::string& line) {
   f << line << '\n';
 }
 
+#ifndef MXS_GIT_SHA
+#define MXS_GIT_SHA "unknown"
+#endif
+
+// `, "git": "<sha>", "device": "<desc>"` for the JSON records.
+// HIP apps pass mxs::device_description(dev); the host-only app passes "cpu".
+inline std::string meta_json(const std::string& device_desc) {
+  return std::string(", \"git\": \"") + MXS_GIT_SHA + "\", \"device\": \"" + device_desc + "\"";
+}
+
 inline std::string fmt(double v) {
   char b[64];
   std::snprintf(b, sizeof(b), "%.6g", v);

@@ -49,6 +49,7 @@ int run(MpiEnv& env, const Cli& cli, index_t n_global) {
   const auto mode = parse_reduce(cli.get("reduce", "single-pass"));
   std::vector<T> hx(size_t(n), T(1)), hy(size_t(n), T(1));  // reference: v1 = v2 = 1
   double best = 1e300, result = 0, partial = 0;
+  int device_used = -1;
   if (!gpu) {
     for (int r = 0; r < reps; ++r) {
       env.barrier();
@@ -61,6 +62,7 @@ int run(MpiEnv& env, const Cli& cli, index_t n_global) {
     }
   } else {
     const DeviceBinding dev = bind_device(env, cli.get("bind", "bunch"));
+    device_used = dev.device;
     if (!quiet) {
       std::ostringstream os;
       os << env.processor_name() << " - rank: " << rank << "\tGPU: " << dev.device << '\n';
@@ -128,7 +130,8 @@ int run(MpiEnv& env, const Cli& cli, index_t n_global) {
        << "\", \"reduce\": \"" << cli.get("reduce", "single-pass") << "\", \"ranks\": " << size
        << ", \"device\": \"" << (gpu ? "gpu" : "cpu") << "\", \"result\": " << app::fmt(result)
        << ", \"seconds\": " << app::fmt(best)
-       << ", \"gbytes_per_s\": " << app::fmt(2.0 * double(n_global) * sizeof(T) / best / 1e9) << "}";
+       << ", \"gbytes_per_s\": " << app::fmt(2.0 * double(n_global) * sizeof(T) / best / 1e9)
+       << app::meta_json(gpu ? device_description(device_used) : std::string("cpu")) << "}";
     if (!quiet) std::cout << js.str() << std::endl;
     app::append_json(cli.get("json"), js.str());
   }

@@ -220,7 +220,7 @@ int main(int argc, char** argv) {
     if (mode == "overlap")
       js << ", \"compute_alone_us\": " << app::fmt(st.compute_alone_us) << ", \"comm_alone_us\": "
          << app::fmt(st.comm_alone_us) << ", \"overlapped_us\": " << app::fmt(st.overlapped_us);
-    js << "}";
+    js << app::meta_json(device_description(dev.device)) << "}";
     if (pos.empty() && !cli.flag("quiet")) std::cout << js.str() << std::endl;
     app::append_json(cli.get("json"), js.str());
   }

@@ -218,7 +218,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
          << "\", \"graph\": \"" << (solver ? solver->graph_status() : std::string("n/a"))
          << "\", \"time_block\": " << time_block << ", \"iters\": " << iters;
       if (want_sum) js << ", \"checksum\": " << app::fmt(checksum);
-      js << "}";
+      js << app::meta_json(device_description(dev.device)) << "}";
       std::cout << "Gcells/s: " << app::fmt(gcells) << '\n';
       if (want_sum) std::cout << "checksum: " << app::fmt(checksum) << '\n';
       std::cout << js.str() << std::endl;

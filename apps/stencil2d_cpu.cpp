@@ -105,7 +105,8 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, index_t lw, index
       js << "{\"app\": \"stencil2d_cpu\", \"metric\": \"gcells_per_s\", \"value\": " << app::fmt(gcells)
          << ", \"ranks\": " << env.size() << ", \"dims\": \"" << topo.rows << "x" << topo.cols << "\", \"global\": \""
          << gw << "x" << gh << "\", \"dtype\": \"" << (sizeof(T) == 4 ? "f32" : "f64") << "\", \"iters\": " << timed
-         << ", \"seconds\": " << app::fmt(dt) << ", \"checksum\": " << app::fmt(checksum) << "}";
+         << ", \"seconds\": " << app::fmt(dt) << ", \"checksum\": " << app::fmt(checksum)
+         << app::meta_json("cpu") << "}";
       std::cout << "Gcells/s: " << app::fmt(gcells) << "\nchecksum: " << app::fmt(checksum) << "\n" << js.str()
                 << std::endl;
       app::append_json(cli.get("json"), js.str());

@@ -5,6 +5,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <string>
 #include <utility>
 
 #include "mxs/core/config.hpp"
@@ -151,6 +152,13 @@ inline int current_device() {
   int d = -1;
   MXS_HIP_CHECK(hipGetDevice(&d));
   return d;
+}
+
+// "<marketing name> (<gcnArchName>)" of a HIP device, for result records.
+inline std::string device_description(int device) {
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, device) != hipSuccess) return "unknown";
+  return std::string(p.name) + " (" + p.gcnArchName + ")";
 }
 
 }  // namespace mxs
