@@ -27,8 +27,9 @@
 // grid fuses the self-exchange into the kernel's wrap-around addressing
 // (`fuse_periodic_self`).
 //
-// `use_graph`: the super-step is captured once per buffer orientation into a
-// hipGraph and replayed (launch-bound inner loops, Guideline 9). If capture fails
+// `use_graph`: `graph_supersteps` consecutive super-steps (auto: ~1 ms of work)
+// are captured once per buffer orientation into a hipGraph and replayed
+// (launch-bound inner loops, Guideline 9). If capture fails
 // (e.g. an RCCL build without graph support) the solver falls back to eager launches.
 #pragma once
 
@@ -62,6 +63,8 @@ struct SolverConfig {
   kernels::StencilVariant variant = kernels::StencilVariant::Auto;
   // HaloBackend::Ipc: host allgather used once at construction (collective).
   HostAllgather bootstrap;
+  // Super-steps captured per hipGraph (0 = auto: ~1 ms of work per launch).
+  int graph_supersteps = 0;
 };
 
 template <typename T>
@@ -88,6 +91,7 @@ class StencilSolver {
   bool fused_periodic() const { return fused_; }
   bool overlapped() const { return cfg_.overlap; }
   int time_block() const { return block_; }
+  int graph_supersteps() const { return chain_; }
   index_t cells_per_iteration() const { return tile_.width * tile_.height; }
 
  private:
@@ -109,6 +113,7 @@ class StencilSolver {
   Event fork_, interior_;
   GraphExec graphs_[2];  // one super-step per buffer orientation (as captured)
   int parity_ = 0;
+  int chain_ = 1;  // super-steps per graph launch
   bool graph_tried_ = false;
   bool fused_ = false;
   std::string graph_status_ = "not captured";

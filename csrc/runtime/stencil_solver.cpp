@@ -1,6 +1,7 @@
 #include "mxs/runtime/stencil_solver.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <utility>
 
 #include "mxs/core/fault.hpp"
@@ -32,6 +33,14 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   boot.timeout_s = comm_timeout() > 0 ? comm_timeout() : 60.0;
   ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm, &boot);
   cfg_.bootstrap = nullptr;  // setup only; drop it (it may hold a Python callable)
+  // Super-steps per graph launch: enough for ~1 ms of work per launch (the
+  // launch gap is ~10 us), estimated at 5 T cell-iterations/s; at most 8.
+  if (cfg_.graph_supersteps > 0) {
+    chain_ = cfg_.graph_supersteps;
+  } else {
+    const double est_us = double(tile_.width) * double(tile_.height) * block_ / 5e6;
+    chain_ = std::max(1, std::min(8, int(std::ceil(1000.0 / std::max(est_us, 1.0)))));
+  }
   // Overlap only pays when there is a wire transfer to hide and an interior.
   if (plan.sends.empty() || tile_.height <= 2 * depth || tile_.width <= 2 * depth) cfg_.overlap = false;
   const bool all_self = plan.sends.empty() && int(plan.self_copies.size()) == (corners ? kNumDirs : 4);
@@ -143,7 +152,10 @@ bool StencilSolver<T>::try_capture() {
     }
     bool ok = true;
     try {
-      enqueue_block(a, b, block_);
+      for (int c = 0; c < chain_; ++c) {  // chain_ consecutive super-steps per graph
+        enqueue_block(a, b, block_);
+        std::swap(a, b);
+      }
     } catch (const std::exception& e) {
       graph_status_ = std::string("capture failed: ") + e.what();
       ok = false;
@@ -171,16 +183,22 @@ template <typename T>
 void StencilSolver<T>::run(int iters) {
   MXS_TRACE_RANGE("stencil.run");
   const int supers = iters / block_, rem = iters % block_;
-  for (int i = 0; i < supers; ++i) {
-    if (cfg_.use_graph && !graph_tried_) try_capture();
-    if (graphs_[0].valid()) {
+  if (supers > 0 && cfg_.use_graph && !graph_tried_) try_capture();
+  int i = 0;
+  if (graphs_[0].valid()) {
+    for (; i + chain_ <= supers; i += chain_) {
       MXS_TRACE_RANGE("stencil.graph_launch");
       graphs_[parity_].launch(main_.get());
-      parity_ ^= 1;
-    } else {
-      enqueue_block(cur_, nxt_, block_);
+      if (chain_ % 2) {  // an odd chain ends on the other buffer
+        parity_ ^= 1;
+        std::swap(cur_, nxt_);
+      }
     }
+  }
+  for (; i < supers; ++i) {  // no graph, or fewer than chain_ super-steps left
+    enqueue_block(cur_, nxt_, block_);
     std::swap(cur_, nxt_);
+    parity_ ^= 1;
   }
   // Remainder: one shorter super-step (S = rem <= block_ fits the ghost ring),
   // run eagerly; a lone step takes the single-iteration path.

@@ -63,6 +63,7 @@ class StencilConfig:
     time_block: int = 0
     seed: int = 1234
     init: str = "random"             # random | rank
+    graph_supersteps: int = 0        # super-steps per hipGraph launch (0 = auto, ~1 ms of work)
 
     @property
     def halo(self) -> int:
@@ -139,7 +140,7 @@ class Stencil2D:
             self.solver = H.StencilSolver(d.topo, d.rank, self.geom, self.a.data_ptr(), self.b.data_ptr(), self.comm,
                                           cfg.dtype, be, overlap, cfg.graph, cfg.loopback, kind, cfg.c_center,
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
-                                          self.time_block, boot)
+                                          self.time_block, boot, cfg.graph_supersteps)
         else:
             self.plan = make_plan(d, self.geom, corners=True)
             self.halo = TorchHalo(self.plan, self.ctx)

@@ -185,3 +185,23 @@ def test_stencil5_tb_wrap_matches_periodic_steps(gpu, dtype, steps, shape):
     ref = jacobi_reference_global(u, steps)
     tol = 2e-6 if dtype == torch.float32 else 1e-14
     assert (got.double() - ref.double()).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize("backend,loopback", [("local", False), ("rccl", True)])
+@pytest.mark.parametrize("chain", [1, 2, 3, 0])
+def test_solver_multi_superstep_graphs(gpu, backend, loopback, chain):
+    """Several super-steps per graph launch (odd and even chains flip the buffer
+    orientation differently), plus eager leftovers and a remainder block."""
+    w, h, S = 200, 96, 4
+    iters = 7 * S + 3
+    cfg = StencilConfig(global_width=w, global_height=h, dims="1x1", dtype="f32", backend=backend,
+                        loopback=loopback, seed=8, time_block=S, graph_supersteps=chain)
+    st = Stencil2D(cfg)
+    st.run(iters)
+    st.run(S * 3)  # a second call reuses the captured graphs from the current orientation
+    st.synchronize()
+    assert st.graph_status() == "captured"
+    if chain:
+        assert st.solver.graph_supersteps() == chain
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, 8), iters + 3 * S)
+    assert (st.core_view().cpu() - ref).abs().max().item() < 1e-5
