@@ -95,15 +95,16 @@ std::function<void(hipStream_t)> ref_for(const float* in, float* out, const Tile
   }
 }
 
-template <int S, int PF, bool WRAP = false, bool DPP = true>
+template <int S, int PF, bool WRAP = false, bool DPP = true, bool ROT = false>
 Variant stream(const float* in, float* out, const TileGeom& g, int ch, float* tmp = nullptr) {
   char buf[128];
-  std::snprintf(buf, sizeof(buf), "stream_s%d_pf%d_ch%d%s%s", S, PF, ch, WRAP ? "_wrap" : "", DPP ? "" : "_bperm");
+  std::snprintf(buf, sizeof(buf), "stream_s%d_pf%d_ch%d%s%s%s", S, PF, ch, WRAP ? "_wrap" : "", DPP ? "" : "_bperm",
+                ROT ? "_rot" : "");
   Variant v{buf, [=](hipStream_t s) {
               constexpr int OW = StreamShape<float, S>::OW;
               const index_t strips = (g.width + OW - 1) / OW;
               const dim3 grid(unsigned((strips + 3) / 4), unsigned((g.height + ch - 1) / ch));
-              stencil5_stream_kernel<float, S, PF, WRAP, DPP><<<grid, 256, 0, s>>>(
+              stencil5_stream_kernel<float, S, PF, WRAP, DPP, ROT><<<grid, 256, 0, s>>>(
                   in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, index_t(ch), 0.2f,
                   0.2f);
             }};
@@ -113,22 +114,24 @@ Variant stream(const float* in, float* out, const TileGeom& g, int ch, float* tm
 }
 
 // Balanced persistent launch: `per_cu` resident workgroups per CU (0 = occupancy API).
-template <int S, int PF, bool WRAP = false>
+template <int S, int PF, bool WRAP = false, bool ROT = false>
 Variant balanced(const float* in, float* out, const TileGeom& g, int per_cu, float* tmp = nullptr) {
   int blocks_per_cu = per_cu;
   if (blocks_per_cu <= 0)
     MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &blocks_per_cu, reinterpret_cast<const void*>(stencil5_stream_balanced_kernel<float, S, PF, WRAP>), 256, 0));
+        &blocks_per_cu, reinterpret_cast<const void*>(stencil5_stream_balanced_kernel<float, S, PF, WRAP, true, ROT>),
+        256, 0));
   int cus = 0;
   MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const int blocks = std::max(1, blocks_per_cu * cus);
   char buf[128];
-  std::snprintf(buf, sizeof(buf), "balanced_s%d_pf%d_b%d%s", S, PF, blocks_per_cu, WRAP ? "_wrap" : "");
+  std::snprintf(buf, sizeof(buf), "balanced_s%d_pf%d_b%d%s%s", S, PF, blocks_per_cu, WRAP ? "_wrap" : "",
+                ROT ? "_rot" : "");
   Variant v{buf, [=](hipStream_t s) {
               constexpr int OW = StreamShape<float, S>::OW;
               const index_t groups = ((g.width + OW - 1) / OW + 3) / 4;
               const index_t share = (groups * g.height + blocks - 1) / blocks;
-              stencil5_stream_balanced_kernel<float, S, PF, WRAP><<<blocks, 256, 0, s>>>(
+              stencil5_stream_balanced_kernel<float, S, PF, WRAP, true, ROT><<<blocks, 256, 0, s>>>(
                   in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, 0.2f, 0.2f);
             }};
   v.steps = S;
@@ -169,7 +172,18 @@ int main(int argc, char** argv) {
   vs.push_back(tb1<6, 128, 32, false>(in, out, g));
   float* tmp = c.get();
   const char* focus = std::getenv("TUNE_FOCUS");
-  if (focus && std::string(focus) == "s") {  // S choice for the balanced launch
+  if (focus && std::string(focus) == "rot") {  // rotated-pair fp32 layout vs natural, per S
+    vs.push_back(balanced<16, 3, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<16, 3, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<16, 3, false>(in, out, g, 0));
+    vs.push_back(balanced<16, 3, false, true>(in, out, g, 0));
+    vs.push_back(balanced<12, 3, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<12, 3, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<8, 3, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<14, 3, true, true>(in, out, g, 0, tmp));
+    vs.push_back(stream<12, 3, true, true, true>(in, out, g, 128, tmp));
+    vs.push_back(stream<16, 3, true, true, true>(in, out, g, 128, tmp));
+  } else if (focus && std::string(focus) == "s") {  // S choice for the balanced launch
     vs.push_back(balanced<12, 3>(in, out, g, 0));
     vs.push_back(balanced<12, 3, true>(in, out, g, 0, tmp));
     vs.push_back(balanced<16, 3>(in, out, g, 2));

@@ -138,7 +138,8 @@ int balanced_blocks() {
   if (blocks == 0) {
     int occ = 0, cus = 0, dev = 0;
     MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, reinterpret_cast<const void*>(stencil5_stream_balanced_kernel<T, S, 3, WRAP>), kBlock, 0));
+        &occ, reinterpret_cast<const void*>(stencil5_stream_balanced_kernel<T, S, 3, WRAP, true, sizeof(T) == 4>),
+        kBlock, 0));
     MXS_HIP_CHECK(hipGetDevice(&dev));
     MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     blocks = std::max(occ, 2) * std::max(cus, 1);
@@ -153,25 +154,42 @@ int balanced_blocks() {
 // 32768^2). Rectangles too small to give every workgroup >= 64 rows use the
 // grid form, whose row chunk CH is the largest of 512..64 that still yields
 // >= 4096 waves.
+// The fp32 rotated-pair form (stream_chunk_rot: 11 VALU per level-row instead
+// of ~15, DPP shifts folded into the adds) stores through a buffer descriptor
+// over one chunk's rows: it needs whole output vectors and a chunk under 2 GiB.
+template <typename T>
+bool rot_ok(const TileGeom& g, index_t x1, index_t chunk_rows) {
+  return sizeof(T) == 4 && x1 % 4 == 0 && chunk_rows * g.pitch * index_t(sizeof(T)) < (index_t(1) << 31);
+}
+
 template <typename T, int S, bool WRAP>
 void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
                    hipStream_t s) {
   constexpr int OW = StreamShape<T, S>::OW;
+  constexpr bool kF32 = sizeof(T) == 4;
   const index_t strips = (x1 - x0 + OW - 1) / OW;
   const index_t rows = y1 - y0;
   const index_t groups = (strips + kWavesPerBlock - 1) / kWavesPerBlock;
   const int blocks = balanced_blocks<T, S, WRAP>();
   if (groups * rows >= index_t(blocks) * 64) {
     const index_t share = (groups * rows + blocks - 1) / blocks;
-    stencil5_stream_balanced_kernel<T, S, 3, WRAP><<<blocks, kBlock, 0, s>>>(
-        in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
+    if (kF32 && rot_ok<T>(g, x1, std::min(share, rows)))
+      stencil5_stream_balanced_kernel<T, S, 3, WRAP, true, kF32><<<blocks, kBlock, 0, s>>>(
+          in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
+    else
+      stencil5_stream_balanced_kernel<T, S, 3, WRAP><<<blocks, kBlock, 0, s>>>(
+          in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
     return;
   }
   index_t ch = 512;
   while (ch > 64 && strips * ((rows + ch - 1) / ch) < 4096) ch /= 2;
   const dim3 grid(unsigned(groups), unsigned((rows + ch - 1) / ch));
-  stencil5_stream_kernel<T, S, 3, WRAP><<<grid, kBlock, 0, s>>>(in, out, g.pitch, g.core_offset(), g.width, g.height,
-                                                                x0, x1, y0, y1, ch, c0, c1);
+  if (kF32 && rot_ok<T>(g, x1, std::min(ch, rows)))
+    stencil5_stream_kernel<T, S, 3, WRAP, true, kF32><<<grid, kBlock, 0, s>>>(
+        in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, ch, c0, c1);
+  else
+    stencil5_stream_kernel<T, S, 3, WRAP><<<grid, kBlock, 0, s>>>(in, out, g.pitch, g.core_offset(), g.width,
+                                                                  g.height, x0, x1, y0, y1, ch, c0, c1);
 }
 
 // Dispatch by shape. Bulk rectangles take the wave-streaming kernel (Auto) or

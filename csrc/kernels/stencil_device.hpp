@@ -605,6 +605,39 @@ __device__ __forceinline__ double lane_shift<double, kDppWaveShl1>(double v) {
   return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
 
+// ------------------------------------------------ rotated-pair fp32 layout
+// Measured on the S = 16 stream kernel (scripts/isa_mix.py): with the natural
+// register layout (c0 c1 | c2 c3) the horizontal sums (c[i-1] + c[i+1]) straddle
+// the 64-bit pairs the packed VALU works on, so the backend builds pairs with 4
+// v_mov_b32 and keeps 2 v_mov_b32_dpp: 18 VALU issue slots per level-row, ~75
+// cycles at one wave per SIMD. Holding every intermediate row ROTATED as
+// A = (c1, c2), B = (c3, c0) makes the in-lane pair (c0 + c2, c3 + c1) one
+// v_pk_add_f32 with swapped halves (op_sel), and the two lane-crossing sums
+// c2 + c0[lane+1], c1 + c3[lane-1] two v_add_f32 with a DPP wave shift folded
+// into the source, written straight into the pair (we3, we0) that lines up with
+// B. Per level-row: 9 packed + 2 DPP adds, no moves. Same operations, same
+// operand order per cell as jac() (IEEE add is commutative): bitwise identical.
+// Only the input rows (natural order from HBM) and the stored top level are
+// rotated, once per row each.
+__device__ __forceinline__ f32x4 rot_in(const f32x4& n) { return __builtin_shufflevector(n, n, 1, 2, 3, 0); }
+__device__ __forceinline__ f32x4 rot_out(const f32x4& r) { return __builtin_shufflevector(r, r, 3, 0, 1, 2); }
+
+__device__ __forceinline__ f32x4 jac_rot4f(const f32x4& up, const f32x4& mid, const f32x4& dn, float c0, float c1) {
+  const f32x2 am = mid.xy, bm = mid.zw;  // (c1, c2), (c3, c0)
+  const f32x2 ns_a = up.xy + dn.xy, ns_b = up.zw + dn.zw;
+  const f32x2 we_a = bm.yx + am.yx;  // (c0 + c2, c3 + c1)
+  f32x2 we_b;
+  we_b.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bm.y), kDppWaveShl1, 0xf, 0xf, true)) + am.y;
+  we_b.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bm.x), kDppWaveShr1, 0xf, 0xf, true)) + am.x;
+  const f32x2 c0v = f32x2(c0), c1v = f32x2(c1);
+  const f32x2 oa = __builtin_elementwise_fma(c1v, ns_a + we_a, c0v * am);
+  const f32x2 ob = __builtin_elementwise_fma(c1v, ns_b + we_b, c0v * bm);
+  f32x4 o;
+  o.xy = oa;
+  o.zw = ob;
+  return o;
+}
+
 template <typename T, int S>
 struct StreamShape {
   static constexpr int N = Vec16<T>::N;
@@ -706,8 +739,109 @@ __device__ __forceinline__ void stream_chunk(const T* __restrict__ in, T* __rest
   }
 }
 
+// fp32 form of stream_chunk on the rotated-pair layout (jac_rot4f) with a
+// branch-free row loop, so the whole unrolled PF-row body is ONE basic block:
+// any branch inside it (a guarded fetch, an exec-masked store) lets the backend
+// hoist the DPP shifts of the next row above it, and a v_mov_b32_dpp that is
+// not in its consumer's block cannot fold into the add (measured: 96 separate
+// v_mov_b32_dpp per 48 level-rows otherwise). Hence:
+//   * fetches always load: the row index saturates at the last input row (or
+//     wraps, WRAP) and lanes past the row padding read its last vector —
+//     values that cannot reach a stored cell within S levels (a stored cell at
+//     x < x_end <= W depends on inputs in [x - S, x + S] only, SA >= S);
+//   * stores go through a buffer descriptor over this chunk's output rows, and
+//     a lane/row that must not store gets an out-of-range offset, which the
+//     buffer range check drops (no exec mask, no branch);
+//   * the row count is rounded up to PF; the extra iterations store nothing.
+// Needs x_end % 4 == 0 (whole vectors) and (ye - ys) * pitch * 4 < 2^31 bytes
+// (checked by the launcher, which falls back to stream_chunk otherwise).
+template <int S, int PF, bool WRAP>
+__device__ __forceinline__ void stream_chunk_rot(const float* __restrict__ in, float* __restrict__ out, index_t pitch,
+                                                 index_t core_off, index_t W, index_t H, index_t xw, index_t x_end,
+                                                 index_t ys, index_t ye, float c0, float c1) {
+  static_assert(PF % 3 == 0, "the window rotates through 3 slots: PF must be a multiple of 3");
+  using Sh = StreamShape<float, S>;
+  constexpr int N = Sh::N, SA = Sh::SA, AL = SA / N;
+  const int lane = threadIdx.x & (kWaveSize - 1);
+  const index_t gx = xw - SA + index_t(lane) * N;
+
+  index_t lx;
+  if constexpr (WRAP) {
+    if (W >= kWaveSize * N) lx = gx < 0 ? gx + W : (gx >= W ? gx - W : gx);
+    else lx = ((gx % W) + W) % W;
+  } else {
+    const index_t last_col = (W + N - 1) / N * N + SA - N;  // last vector of the row padding
+    lx = gx < last_col ? gx : last_col;
+  }
+  const float* __restrict__ pin = in + core_off + lx;
+
+  // Output descriptor: rows [ys, ye) from column xw - SA (wave-uniform base).
+  const index_t rows = ye - ys;
+  const float* obase = out + core_off + (xw - SA) + ys * pitch;
+  const unsigned long long ob = reinterpret_cast<unsigned long long>(obase);
+  const unsigned ob_lo = __builtin_amdgcn_readfirstlane(unsigned(ob)), ob_hi = __builtin_amdgcn_readfirstlane(unsigned(ob >> 32));
+  float* obase_u = reinterpret_cast<float*>((static_cast<unsigned long long>(ob_hi) << 32) | ob_lo);
+  const int nbytes = __builtin_amdgcn_readfirstlane(int(rows * pitch * index_t(sizeof(float))));
+  const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(obase_u, 0, nbytes, 0x00020000);
+  const bool store_lane = lane >= AL && lane < kWaveSize - AL && gx < x_end;
+  const unsigned lane_off = unsigned(lane) * unsigned(N * sizeof(float));
+  const unsigned row_bytes = unsigned(pitch) * unsigned(sizeof(float));
+  constexpr unsigned kDrop = 0x80000000u;  // >= nbytes: dropped by the range check
+
+  const index_t y_first = ys - S;
+  const index_t last_row = ye + S - 1;
+  index_t next = y_first;
+  if constexpr (WRAP) next = next < 0 ? next + H : next;
+  auto fetch = [&]() -> f32x4 {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(pin + next * pitch);
+    if constexpr (WRAP) {
+      ++next;
+      next = next == H ? 0 : next;
+    } else {
+      next = next < last_row ? next + 1 : next;
+    }
+    return v;
+  };
+
+  f32x4 win[3][S];
+#pragma unroll
+  for (int q = 0; q < 3; ++q)
+#pragma unroll
+    for (int l = 0; l < S; ++l) win[q][l] = f32x4(0.f);
+
+  const index_t n_it = rows + 3 * S - 1;
+  f32x4 pf[PF];
+#pragma unroll
+  for (int k = 0; k < PF; ++k) pf[k] = fetch();
+#pragma unroll 1
+  for (index_t i = 0; i < n_it; i += PF) {
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      const index_t j = i + k;
+      const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;  // static after the unroll
+      if (j >= n_it) break;  // wave-uniform (scalar branch); without it the allocator spills to AGPRs
+      win[p2][0] = rot_in(pf[k]);
+      pf[k] = fetch();
+      f32x4 top;
+#pragma unroll
+      for (int l = S - 1; l >= 0; --l) {
+        const f32x4 o = jac_rot4f(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+        if (l == S - 1) top = o;
+        else win[p0][l + 1] = o;
+      }
+      const index_t r = j - (3 * S - 1);  // output row (relative to ys) of this iteration
+      const bool ok = store_lane && r >= 0 && r < rows;
+      const unsigned off = ok ? lane_off + unsigned(r) * row_bytes : kDrop;
+      const f32x4 nat = rot_out(top);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, nat),
+                                             orsrc, int(off), 0, 2 /* nt */);
+    }
+  }
+}
+
 // Grid form: workgroup = 4 waves on 4 adjacent strips of the same CH-row chunk.
-template <typename T, int S, int PF, bool WRAP, bool DPP = true>
+// ROT: stream_chunk_rot (fp32, DPP; launcher checks its preconditions).
+template <typename T, int S, int PF, bool WRAP, bool DPP = true, bool ROT = false>
 __global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                  index_t pitch, index_t core_off, index_t W, index_t H,
                                                                  index_t x_begin, index_t x_end, index_t y_begin,
@@ -717,7 +851,8 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __rest
   if (xw >= x_end) return;  // wave-uniform
   const index_t ys = y_begin + index_t(blockIdx.y) * CH;
   const index_t ye = ys + CH < y_end ? ys + CH : y_end;
-  stream_chunk<T, S, PF, WRAP, DPP>(in, out, pitch, core_off, W, H, xw, x_end, ys, ye, c0, c1);
+  if constexpr (ROT) stream_chunk_rot<S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, ys, ye, c0, c1);
+  else stream_chunk<T, S, PF, WRAP, DPP>(in, out, pitch, core_off, W, H, xw, x_end, ys, ye, c0, c1);
 }
 
 // Balanced persistent form: exactly as many workgroups as fit on the chip at
@@ -727,7 +862,7 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __rest
 // so the apron columns two neighbouring waves both read are L2 hits — and a
 // share that crosses a group boundary restarts there. No tail round, and
 // (3S-1)/share redundant rows instead of (3S-1)/CH per chunk.
-template <typename T, int S, int PF, bool WRAP, bool DPP = true>
+template <typename T, int S, int PF, bool WRAP, bool DPP = true, bool ROT = false>
 __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
@@ -744,9 +879,13 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
     const index_t grp = a / rows, r0 = a - grp * rows;
     const index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
     const index_t xw = x_begin + (grp * kWavesPerBlock + wave) * OW;
-    if (xw < x_end)
-      stream_chunk<T, S, PF, WRAP, DPP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0,
-                                        c1);
+    if (xw < x_end) {
+      if constexpr (ROT)
+        stream_chunk_rot<S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1);
+      else
+        stream_chunk<T, S, PF, WRAP, DPP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0,
+                                          c1);
+    }
     a += r1 - r0;
   }
 }
