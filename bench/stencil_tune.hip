@@ -26,6 +26,45 @@ __global__ __launch_bounds__(256) void copy4(const float4* __restrict__ a, float
   for (index_t i = index_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) b[i] = a[i];
 }
 
+// Balanced rotated kernel with per-wave timestamps (s_memrealtime, 100 MHz, and
+// s_memtime, shader clock) at start and end: measures the wave lifetime against
+// the dispatch, i.e. tail / imbalance vs clock (TUNE_FOCUS=stamp).
+template <int S, bool WRAP, bool PRIO>
+__global__ __launch_bounds__(256) void balanced_stamped(const float* __restrict__ in, float* __restrict__ out,
+                                                        index_t pitch, index_t core_off, index_t W, index_t H,
+                                                        index_t x_begin, index_t x_end, index_t y_begin,
+                                                        index_t y_end, index_t share, float c0, float c1,
+                                                        unsigned long long* stamps) {
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime(), t0 = __builtin_amdgcn_s_memtime();
+  constexpr int OW = StreamShape<float, S>::OW;
+  const index_t rows = y_end - y_begin;
+  const index_t strips = (x_end - x_begin + OW - 1) / OW;
+  const index_t groups = (strips + kWavesPerBlock - 1) / kWavesPerBlock;
+  const index_t total = groups * rows;
+  const int wave = threadIdx.x / kWaveSize;
+  index_t a = index_t(blockIdx.x) * share;
+  const index_t a0 = a;
+  const index_t b = a + share < total ? a + share : total;
+  WavePrio wp;
+  if (PRIO && b > a) wp.quarters = 4.f / float(b - a);
+  while (a < b) {
+    const index_t grp = a / rows, q0 = a - grp * rows;
+    const index_t q1 = rows < q0 + (b - a) ? rows : q0 + (b - a);
+    const index_t xw = x_begin + (grp * kWavesPerBlock + wave) * OW;
+    wp.done = a - a0;
+    if (xw < x_end)
+      stream_chunk_rot<S, 3, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + q0, y_begin + q1, c0, c1, &wp);
+    a += q1 - q0;
+  }
+  const unsigned long long r1 = __builtin_amdgcn_s_memrealtime(), t1 = __builtin_amdgcn_s_memtime();
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long* p = stamps + (size_t(blockIdx.x) * 4 + wave) * 6;
+    p[0] = r0; p[1] = r1; p[2] = t0; p[3] = t1;
+    p[4] = __builtin_amdgcn_s_getreg(4 | (31 << 11));   // HW_REG_HW_ID
+    p[5] = __builtin_amdgcn_s_getreg(20 | (31 << 11));  // HW_REG_XCC_ID
+  }
+}
+
 struct Variant {
   std::string name;
   std::function<void(hipStream_t)> launch;
@@ -172,7 +211,48 @@ int main(int argc, char** argv) {
   vs.push_back(tb1<6, 128, 32, false>(in, out, g));
   float* tmp = c.get();
   const char* focus = std::getenv("TUNE_FOCUS");
-  if (focus && std::string(focus) == "rot") {  // rotated-pair fp32 layout vs natural, per S
+  if (focus && std::string(focus) == "stamp") {  // per-wave lifetimes of the default S = 16 rotated kernel
+    int occ = 0, cus = 0;
+    MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, reinterpret_cast<const void*>(balanced_stamped<16, true, true>), 256, 0));
+    MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const int blocks = std::max(occ, 1) * cus;
+    constexpr int OW = StreamShape<float, 16>::OW;
+    const index_t groups = ((W + OW - 1) / OW + 3) / 4;
+    const index_t share = (groups * H + blocks - 1) / blocks;
+    DeviceBuffer<unsigned long long> st(size_t(blocks) * 24);
+    Stream ss;
+    for (int rep = 0; rep < 4; ++rep) {
+      if (std::getenv("STAMP_NOPRIO"))
+        balanced_stamped<16, true, false><<<blocks, 256, 0, ss.get()>>>(in, out, g.pitch, g.core_offset(), W, H, 0, W,
+                                                                        0, H, share, 0.2f, 0.2f, st.get());
+      else
+        balanced_stamped<16, true, true><<<blocks, 256, 0, ss.get()>>>(in, out, g.pitch, g.core_offset(), W, H, 0, W,
+                                                                       0, H, share, 0.2f, 0.2f, st.get());
+      MXS_HIP_CHECK(hipGetLastError());
+      ss.sync();
+    }
+    std::vector<unsigned long long> h(size_t(blocks) * 24);
+    MXS_HIP_CHECK(hipMemcpy(h.data(), st.get(), h.size() * 8, hipMemcpyDeviceToHost));
+    unsigned long long rmin = ~0ull, rmax = 0;
+    for (int w = 0; w < blocks * 4; ++w) {
+      rmin = std::min(rmin, h[size_t(w) * 6]);
+      rmax = std::max(rmax, h[size_t(w) * 6 + 1]);
+    }
+    // One line per wave: block wave xcc se cu simd start_us end_us clock_ghz
+    for (int w = 0; w < blocks * 4; ++w) {
+      const unsigned long long* p = &h[size_t(w) * 6];
+      const unsigned hw = unsigned(p[4]);
+      const double clk = double(p[3] - p[2]) / double(std::max<unsigned long long>(p[1] - p[0], 1)) * 100e6 / 1e9;
+      std::printf("W %d %d %u %u %u %u %.1f %.1f %.3f\n", w / 4, w % 4, unsigned(p[5]) & 0xf, (hw >> 13) & 0x7,
+                  (hw >> 8) & 0xf, (hw >> 4) & 0x3, (p[0] - rmin) / 100.0, (p[1] - rmin) / 100.0, clk);
+    }
+    std::printf("{\"stamp_blocks\": %d, \"span_us\": %.1f}\n", blocks, (rmax - rmin) / 100.0);
+    return 0;
+  } else if (focus && std::string(focus) == "one") {  // counter runs: the default S = 16 kernel, both layouts
+    vs.push_back(balanced<16, 3, true>(in, out, g, 0));
+    vs.push_back(balanced<16, 3, true, true>(in, out, g, 0));
+  } else if (focus && std::string(focus) == "rot") {  // rotated-pair fp32 layout vs natural, per S
     vs.push_back(balanced<16, 3, true>(in, out, g, 0, tmp));
     vs.push_back(balanced<16, 3, true, true>(in, out, g, 0, tmp));
     vs.push_back(balanced<16, 3, false>(in, out, g, 0));

@@ -755,10 +755,36 @@ __device__ __forceinline__ void stream_chunk(const T* __restrict__ in, T* __rest
 //   * the row count is rounded up to PF; the extra iterations store nothing.
 // Needs x_end % 4 == 0 (whole vectors) and (ye - ys) * pitch * 4 < 2^31 bytes
 // (checked by the launcher, which falls back to stream_chunk otherwise).
+// Progress-based wave priority (balanced launch). Two waves share each SIMD and
+// the VALU arbiter prefers the older one, so with equal work the first-launched
+// workgroup of a CU finished at ~62% of the kernel and its partner ran the last
+// ~38% alone at ~70% of the paired issue rate (per-wave s_memrealtime stamps on
+// 32768^2, TUNE_FOCUS=stamp of bench/stencil_tune). Each wave instead sets its
+// priority from the fraction of its share still ahead of it (4 levels), so
+// the laggard gets the issue slots and both finish together.
+struct WavePrio {
+  index_t done = 0;       // rows of the share finished before this chunk
+  float quarters = 0.f;   // 4 / share rows (0: priority left alone)
+  int level = -1;         // current level (s_setprio value)
+};
+__device__ __forceinline__ void wave_prio_update(WavePrio& wp, index_t done) {
+  if (wp.quarters == 0.f) return;
+  const float q = float(done) * wp.quarters;
+  const int level = q >= 3.f ? 0 : (q >= 2.f ? 1 : (q >= 1.f ? 2 : 3));
+  if (level == wp.level) return;
+  wp.level = level;
+  switch (level) {  // s_setprio takes an immediate
+    case 3: __builtin_amdgcn_s_setprio(3); break;
+    case 2: __builtin_amdgcn_s_setprio(2); break;
+    case 1: __builtin_amdgcn_s_setprio(1); break;
+    default: __builtin_amdgcn_s_setprio(0); break;
+  }
+}
+
 template <int S, int PF, bool WRAP>
 __device__ __forceinline__ void stream_chunk_rot(const float* __restrict__ in, float* __restrict__ out, index_t pitch,
                                                  index_t core_off, index_t W, index_t H, index_t xw, index_t x_end,
-                                                 index_t ys, index_t ye, float c0, float c1) {
+                                                 index_t ys, index_t ye, float c0, float c1, WavePrio* wp = nullptr) {
   static_assert(PF % 3 == 0, "the window rotates through 3 slots: PF must be a multiple of 3");
   using Sh = StreamShape<float, S>;
   constexpr int N = Sh::N, SA = Sh::SA, AL = SA / N;
@@ -815,6 +841,7 @@ __device__ __forceinline__ void stream_chunk_rot(const float* __restrict__ in, f
   for (int k = 0; k < PF; ++k) pf[k] = fetch();
 #pragma unroll 1
   for (index_t i = 0; i < n_it; i += PF) {
+    if (wp && (i & 63) == 0) wave_prio_update(*wp, wp->done + i);
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
       const index_t j = i + k;
@@ -873,15 +900,20 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
   const index_t total = groups * rows;
   const int wave = threadIdx.x / kWaveSize;
   index_t a = index_t(blockIdx.x) * share;
+  const index_t a0 = a;
   const index_t b = a + share < total ? a + share : total;
+  WavePrio wp;
+  if (b > a) wp.quarters = 4.f / float(b - a);
 #pragma unroll 1
   while (a < b) {  // workgroup-uniform
     const index_t grp = a / rows, r0 = a - grp * rows;
     const index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
     const index_t xw = x_begin + (grp * kWavesPerBlock + wave) * OW;
     if (xw < x_end) {
+      wp.done = a - a0;
       if constexpr (ROT)
-        stream_chunk_rot<S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1);
+        stream_chunk_rot<S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1,
+                                      &wp);
       else
         stream_chunk<T, S, PF, WRAP, DPP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0,
                                           c1);
