@@ -71,6 +71,11 @@ struct Variant {
   std::vector<float> ms;
   int steps = 1;  // Jacobi iterations per launch
   std::function<void(hipStream_t)> ref;  // validated kernel computing the same thing
+  // The same kernel with input and output swapped: timed launches alternate
+  // launch / launch2 like the solver's ping-pong. Re-reading one never-written
+  // input would let a 256 MiB tile (8192^2) stay in the 256 MB Infinity Cache
+  // and read ~30% faster than any real time step (measured: 129 vs 171 us).
+  std::function<void(hipStream_t)> launch2;
 };
 
 template <int ROWS, int CH, bool NT, int WX, bool NTL, int NW = 4>
@@ -139,14 +144,17 @@ Variant stream(const float* in, float* out, const TileGeom& g, int ch, float* tm
   char buf[128];
   std::snprintf(buf, sizeof(buf), "stream_s%d_pf%d_ch%d%s%s%s", S, PF, ch, WRAP ? "_wrap" : "", DPP ? "" : "_bperm",
                 ROT ? "_rot" : "");
-  Variant v{buf, [=](hipStream_t s) {
-              constexpr int OW = StreamShape<float, S>::OW;
-              const index_t strips = (g.width + OW - 1) / OW;
-              const dim3 grid(unsigned((strips + 3) / 4), unsigned((g.height + ch - 1) / ch));
-              stencil5_stream_kernel<float, S, PF, WRAP, DPP, ROT><<<grid, 256, 0, s>>>(
-                  in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, index_t(ch), 0.2f,
-                  0.2f);
-            }};
+  auto mk = [=](const float* I, float* O) {
+    return [=](hipStream_t s) {
+      constexpr int OW = StreamShape<float, S>::OW;
+      const index_t strips = (g.width + OW - 1) / OW;
+      const dim3 grid(unsigned((strips + 3) / 4), unsigned((g.height + ch - 1) / ch));
+      stencil5_stream_kernel<float, S, PF, WRAP, DPP, ROT><<<grid, 256, 0, s>>>(
+          I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, index_t(ch), 0.2f, 0.2f);
+    };
+  };
+  Variant v{buf, mk(in, out)};
+  v.launch2 = mk(out, const_cast<float*>(in));
   v.steps = S;
   v.ref = ref_for<S, WRAP>(in, out, g, tmp);
   return v;
@@ -166,13 +174,17 @@ Variant balanced(const float* in, float* out, const TileGeom& g, int per_cu, flo
   char buf[128];
   std::snprintf(buf, sizeof(buf), "balanced_s%d_pf%d_b%d%s%s", S, PF, blocks_per_cu, WRAP ? "_wrap" : "",
                 ROT ? "_rot" : "");
-  Variant v{buf, [=](hipStream_t s) {
-              constexpr int OW = StreamShape<float, S>::OW;
-              const index_t groups = ((g.width + OW - 1) / OW + 3) / 4;
-              const index_t share = (groups * g.height + blocks - 1) / blocks;
-              stencil5_stream_balanced_kernel<float, S, PF, WRAP, true, ROT><<<blocks, 256, 0, s>>>(
-                  in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, 0.2f, 0.2f);
-            }};
+  auto mk = [=](const float* I, float* O) {
+    return [=](hipStream_t s) {
+      constexpr int OW = StreamShape<float, S>::OW;
+      const index_t groups = ((g.width + OW - 1) / OW + 3) / 4;
+      const index_t share = (groups * g.height + blocks - 1) / blocks;
+      stencil5_stream_balanced_kernel<float, S, PF, WRAP, true, ROT><<<blocks, 256, 0, s>>>(
+          I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, 0.2f, 0.2f);
+    };
+  };
+  Variant v{buf, mk(in, out)};
+  v.launch2 = mk(out, const_cast<float*>(in));
   v.steps = S;
   v.ref = ref_for<S, WRAP>(in, out, g, tmp);
   return v;
@@ -198,6 +210,9 @@ int main(int argc, char** argv) {
   vs.push_back({"copy_float4", [=](hipStream_t s) {
                   copy4<<<kNumCUs * 8, 256, 0, s>>>(reinterpret_cast<const float4*>(in), reinterpret_cast<float4*>(out), n4);
                 }});
+  vs.back().launch2 = [=](hipStream_t s) {
+    copy4<<<kNumCUs * 8, 256, 0, s>>>(reinterpret_cast<const float4*>(out), reinterpret_cast<float4*>(const_cast<float*>(in)), n4);
+  };
   vs.push_back({"lds_th16", [=](hipStream_t s) {
                   const index_t gx = (W + 255) / 256, gy = (H + 15) / 16;
                   stencil5_lds_kernel<float, 16><<<dim3(gx, gy), 256, (16 + 2) * (256 + 8) * 4, s>>>(
@@ -261,8 +276,10 @@ int main(int argc, char** argv) {
     vs.push_back(balanced<12, 3, true, true>(in, out, g, 0, tmp));
     vs.push_back(balanced<8, 3, true, true>(in, out, g, 0, tmp));
     vs.push_back(balanced<14, 3, true, true>(in, out, g, 0, tmp));
-    vs.push_back(stream<12, 3, true, true, true>(in, out, g, 128, tmp));
-    vs.push_back(stream<16, 3, true, true, true>(in, out, g, 128, tmp));
+    vs.push_back(balanced<16, 6, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<16, 6, false, true>(in, out, g, 0));
+    vs.push_back(balanced<12, 6, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<14, 6, true, true>(in, out, g, 0, tmp));
   } else if (focus && std::string(focus) == "s") {  // S choice for the balanced launch
     vs.push_back(balanced<12, 3>(in, out, g, 0));
     vs.push_back(balanced<12, 3, true>(in, out, g, 0, tmp));
@@ -319,7 +336,10 @@ int main(int argc, char** argv) {
   for (int r = 0; r < rounds; ++r)
     for (auto& v : vs) {
       e0.record(st.get());
-      for (int k = 0; k < 3; ++k) v.launch(st.get());
+      for (int k = 0; k < 3; ++k) {
+        if ((k & 1) && v.launch2) v.launch2(st.get());
+        else v.launch(st.get());
+      }
       e1.record(st.get());
       e1.sync();
       v.ms.push_back(e1.since(e0) / 3);

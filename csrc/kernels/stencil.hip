@@ -132,13 +132,24 @@ void launch_tb_tile(const T* in, T* out, const TileGeom& g, index_t x0, index_t 
 // Workgroups of the balanced stream kernel resident at once on this device:
 // occupancy x CUs, at least 2 per CU (at S = 16, 1 fits; two rounds of
 // half-size shares still beat one round: profiles/stencil_tuning/tune16).
+// Rows in flight per wave (the fetch ring) of the fp32 rotated kernel: 6 up to
+// S = 12, where a 3-row lookahead (~1 us of work) no longer covers HBM latency
+// under load (8192^2, S = 12: +5%); 3 above, where 6 pushes S = 16 to 253
+// VGPRs and measured no better (profiles/stencil_tuning/tunePF_*).
+template <typename T, int S>
+constexpr int stream_pf() {
+  return (sizeof(T) == 4 && S <= 12) ? 6 : 3;
+}
+
 template <typename T, int S, bool WRAP>
 int balanced_blocks() {
   static int blocks = 0;
   if (blocks == 0) {
     int occ = 0, cus = 0, dev = 0;
     MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, reinterpret_cast<const void*>(stencil5_stream_balanced_kernel<T, S, 3, WRAP, true, sizeof(T) == 4>),
+        &occ,
+        reinterpret_cast<const void*>(
+            stencil5_stream_balanced_kernel<T, S, stream_pf<T, S>(), WRAP, true, sizeof(T) == 4>),
         kBlock, 0));
     MXS_HIP_CHECK(hipGetDevice(&dev));
     MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -174,7 +185,7 @@ void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
   if (groups * rows >= index_t(blocks) * 64) {
     const index_t share = (groups * rows + blocks - 1) / blocks;
     if (kF32 && rot_ok<T>(g, x1, std::min(share, rows)))
-      stencil5_stream_balanced_kernel<T, S, 3, WRAP, true, kF32><<<blocks, kBlock, 0, s>>>(
+      stencil5_stream_balanced_kernel<T, S, stream_pf<T, S>(), WRAP, true, kF32><<<blocks, kBlock, 0, s>>>(
           in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
     else
       stencil5_stream_balanced_kernel<T, S, 3, WRAP><<<blocks, kBlock, 0, s>>>(
@@ -185,7 +196,7 @@ void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
   while (ch > 64 && strips * ((rows + ch - 1) / ch) < 4096) ch /= 2;
   const dim3 grid(unsigned(groups), unsigned((rows + ch - 1) / ch));
   if (kF32 && rot_ok<T>(g, x1, std::min(ch, rows)))
-    stencil5_stream_kernel<T, S, 3, WRAP, true, kF32><<<grid, kBlock, 0, s>>>(
+    stencil5_stream_kernel<T, S, stream_pf<T, S>(), WRAP, true, kF32><<<grid, kBlock, 0, s>>>(
         in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, ch, c0, c1);
   else
     stencil5_stream_kernel<T, S, 3, WRAP><<<grid, kBlock, 0, s>>>(in, out, g.pitch, g.core_offset(), g.width,

@@ -842,16 +842,18 @@ __device__ __forceinline__ void stream_chunk_rot(const float* __restrict__ in, f
   // Warm-up: level l first produces a row any stored cell depends on at
   // iteration 3l + 2, so iteration block b (iterations 3b .. 3b+2) only runs
   // levels 0..b; the skipped levels would compute rows outside every stored
-  // cell's dependency cone. Blocks 0..S-2 end at iteration 3S-4, before the
-  // first store (3S-1). Halves the warm-up work: (3S-1) of every chunk's
-  // rows + 3S - 1 iterations, 14% of a 292-row share of the 8-GPU tile.
-  static_assert(PF == 3, "the warm-up blocks are one window period");
+  // cell's dependency cone. The warm-up covers the whole PF-steps below
+  // 3(S-1) (the first store is at 3S-1); it halves the warm-up work of the
+  // (3S-1) extra iterations every chunk pays, 14% of a 292-row share of the
+  // 8-GPU tile.
+  constexpr int kWarm = (3 * (S - 1)) / PF * PF;
   if (wp) wave_prio_update(*wp, wp->done);
 #pragma unroll 1
-  for (int b = 0; b < S - 1; ++b) {
+  for (int ib = 0; ib < kWarm; ib += PF) {
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int p0 = k, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
+    for (int k = 0; k < PF; ++k) {
+      const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
+      const int b = (ib + k) / 3;  // wave-uniform
       win[p2][0] = rot_in(pf[k]);
       pf[k] = fetch();
 #pragma unroll
@@ -861,7 +863,7 @@ __device__ __forceinline__ void stream_chunk_rot(const float* __restrict__ in, f
     }
   }
 #pragma unroll 1
-  for (index_t i = 3 * (S - 1); i < n_it; i += PF) {
+  for (index_t i = kWarm; i < n_it; i += PF) {
     if (wp && (i & 63) == 0) wave_prio_update(*wp, wp->done + i);
 #pragma unroll
     for (int k = 0; k < PF; ++k) {
