@@ -12,7 +12,7 @@ NGPU = torch.cuda.device_count() if torch.cuda.is_available() else 0
 pytestmark = [pytest.mark.gpu, pytest.mark.multigpu,
               pytest.mark.skipif(NGPU < 2, reason="needs >= 2 GPUs")]
 
-GRIDS = [(2, "1x2"), (2, "2x1"), (4, "2x2"), (8, "2x4")]
+GRIDS = [(2, "1x2"), (2, "2x1"), (4, "2x2"), (8, "2x4"), (8, "4x2")]
 
 
 @pytest.mark.parametrize("n,dims", [g for g in GRIDS if g[0] <= NGPU])

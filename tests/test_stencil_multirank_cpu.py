@@ -34,7 +34,7 @@ def test_golden_3x3_gloo():
         assert r["text"] == _golden(name), f"mismatch for {name}"
 
 
-@pytest.mark.parametrize("dims,n", [("1x2", 2), ("2x1", 2), ("2x2", 4), ("2x4", 8), ("1x3", 3)])
+@pytest.mark.parametrize("dims,n", [("1x2", 2), ("2x1", 2), ("2x2", 4), ("2x4", 8), ("4x2", 8), ("1x3", 3)])
 def test_decomposition_invariance_bitwise(dims, n):
     w, h, iters = 40, 24, 6
     res = run_ranks("jacobi", n, {"w": w, "h": h, "dims": dims, "iters": iters, "seed": 5})
