@@ -10,7 +10,8 @@
 // --acc      f64 (default) | f32 (reproduces the reference's float accumulation)
 // --allreduce rccl (device ncclAllReduce) | mpi (host MPI_Reduce, the reference) | auto
 // --device   gpu | cpu,  --bind bunch | rrobin (-DMPI_RROBIN_),  --quiet (-DNO_LOG),
-// --include-alloc-time (time allocation + H2D too, the reference's default), --reps N
+// --include-alloc-time (time allocation + H2D too, the reference's default), --reps N,
+// --grid G (workgroups of the reduction kernel; default from the device CU count)
 #include <mpi.h>
 
 #include <algorithm>
@@ -50,6 +51,7 @@ int run(MpiEnv& env, const Cli& cli, index_t n_global) {
   std::vector<T> hx(size_t(n), T(1)), hy(size_t(n), T(1));  // reference: v1 = v2 = 1
   double best = 1e300, result = 0, partial = 0;
   int device_used = -1;
+  int grid_used = 0;
   if (!gpu) {
     for (int r = 0; r < reps; ++r) {
       env.barrier();
@@ -77,9 +79,14 @@ int run(MpiEnv& env, const Cli& cli, index_t n_global) {
       comm = std::make_unique<RcclComm>(uid, size, rank);
     }
     const bool include_alloc = cli.flag("include-alloc-time");
-    const int grid = kernels::dot_grid_size(n, kernels::kDotBlock);
+    const int grid = cli.has("grid") ? int(cli.get_int("grid", 0)) : kernels::dot_grid_size(n, kernels::kDotBlock);
+    MXS_CHECK(grid > 0, "--grid must be positive");
+    grid_used = grid;
     Stream s;
     DeviceBuffer<T> x, y;
+    // Reduction workspaces: allocated once, outside every timed region.
+    DeviceBuffer<Acc> partials(grid), out(1), total(1);
+    DeviceBuffer<unsigned> counter(4);
     for (int r = 0; r < reps; ++r) {
       env.barrier();
       double t0 = MPI_Wtime();
@@ -90,8 +97,6 @@ int run(MpiEnv& env, const Cli& cli, index_t n_global) {
         MXS_HIP_CHECK(hipMemcpyAsync(y.get(), hy.data(), y.bytes(), hipMemcpyHostToDevice, s.get()));
         s.sync();
       }
-      DeviceBuffer<Acc> partials(grid), out(1), total(1);
-      DeviceBuffer<unsigned> counter(4);
       if (!include_alloc) {  // -DNO_GPU_MALLOC_TIME: time the resident-data reduction only
         env.barrier();
         t0 = MPI_Wtime();
@@ -129,7 +134,7 @@ int run(MpiEnv& env, const Cli& cli, index_t n_global) {
     js << "{\"app\": \"dot\", \"n\": " << n_global << ", \"dtype\": \"" << (sizeof(T) == 4 ? "f32" : "f64")
        << "\", \"reduce\": \"" << cli.get("reduce", "single-pass") << "\", \"ranks\": " << size
        << ", \"device\": \"" << (gpu ? "gpu" : "cpu") << "\", \"result\": " << app::fmt(result)
-       << ", \"seconds\": " << app::fmt(best)
+       << ", \"seconds\": " << app::fmt(best) << ", \"grid\": " << grid_used
        << ", \"gbytes_per_s\": " << app::fmt(2.0 * double(n_global) * sizeof(T) / best / 1e9)
        << app::meta_json(gpu ? device_description(device_used) : std::string("cpu")) << "}";
     if (!quiet) std::cout << js.str() << std::endl;

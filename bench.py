@@ -3,30 +3,40 @@
 
 BASELINE.json metric: "2D stencil Gcells/sec at 1/2/4/8 GPUs; GPU-GPU pingpong
 GB/s + µs latency". Config: the BASELINE 8-GPU problem — a 32768 x 32768 fp32
-periodic grid, 5-point Jacobi, decomposed over a Cartesian process grid (2x4 on
-8 GPUs: 2 ranks along x, 4 along y; 1x1, 1x2, 2x2 below), halo exchange by native RCCL point-to-point over
-xGMI (pack -> per-peer send/recv -> unpack, captured in a hipGraph with the
-update; `--overlap` forks the interior onto a second stream, the default only
-when --time-block 1). The global grid is fixed as N grows
-(strong scaling). Random-init synthetic data (deterministic per global cell).
+periodic grid, 5-point Jacobi, decomposed over a Cartesian process grid
+(MPI_Dims_create order: 1, 2 rows x 1 col, 2 x 2, 4 rows x 2 cols), halo
+exchange by native RCCL point-to-point over xGMI (pack -> per-peer send/recv ->
+unpack, captured in a hipGraph with the update). The global grid is fixed as N
+grows (strong scaling). Random-init synthetic data (deterministic per global
+cell). At N = 1 the only neighbour is the rank itself: the self-exchange is
+fused into the kernel's periodic addressing (no copy at all), and the record
+says so.
 
 One step = one full Jacobi iteration of the global grid: every core cell is
 updated every step. Halos are exchanged communication-avoiding style: an
 S-deep ghost ring (S = --time-block; default 16 for tiles of >= 2^27 cells,
-12 below, as measured) is exchanged once per S steps
-(pack -> RCCL send/recv per peer -> unpack) and the wave-streaming kernel runs
-the S steps in one pass over HBM; the result is bitwise identical to one 1-deep
-exchange + one sweep per step (tests/test_gpu_solver.py). W untimed warm-up
-steps, then K timed steps bracketed by barrier + device synchronisation on both
-sides; the time is the max over ranks. K need not be a multiple of S (the
-remainder runs as one shorter block).
+12 below, as measured) is exchanged once per super-step and the
+wave-streaming kernel runs the super-step's iterations in one pass over HBM;
+the result is bitwise identical to one 1-deep exchange + one sweep per step
+(tests/test_gpu_solver.py). K steps run as ceil(K / S) near-equal super-steps
+(K = 20 -> 10 + 10).
+
+Timing: W untimed warm-up steps, then ``prepare(K)`` (graph capture + upload
+and one launch of every kernel shape the timed window uses, state unchanged),
+then K timed steps bracketed by barrier + device synchronisation on both
+sides; the time is the max over ranks.
 
     python bench.py                       # N=1
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
 
-Extras (not the headline number): on N=1 the BASELINE single-GPU config
-(8192^2 fp32); on N>=2 an RCCL ping-pong between ranks 0 and 1 (latency at 8 B,
-bandwidth at 256 MiB).
+Extras (not the headline number, BASELINE configs 2/3/5):
+  * every N: the parallel dot product, 2^30 fp64 split over the N ranks,
+    single-pass device reduction + RCCL all-reduce of the partial (GB/s read);
+  * N = 1: 8192^2 fp32 and fp64 single-GPU stencil rates;
+  * N >= 2: GPU-GPU ping-pong between ranks 0 and 1, 8 B - 256 MiB, RCCL
+    blocking / async / overlap and device-initiated HIP IPC. Summary
+    (latency at 8 B, GB/s at 1 MiB / 16 MiB / 256 MiB) in extras, the full
+    sweep in gpurun_out/bench_pingpong_n<N>.json.
 """
 from __future__ import annotations
 
@@ -37,6 +47,9 @@ import sys
 import time
 
 import torch
+
+PINGPONG_SIZES = [8 << i for i in range(26)]  # 8 B .. 256 MiB
+SUMMARY_SIZES = {"1MiB": 1 << 20, "16MiB": 16 << 20, "256MiB": 256 << 20}
 
 
 def _ms(x):
@@ -50,17 +63,94 @@ def _sync():
 
 def timed_run(st, ctx, steps: int, warmup: int) -> float:
     st.run(warmup)
+    st.prepare(steps)  # graphs + first launches of the timed shapes, outside the window
     st.synchronize()
     _sync()
     ctx.barrier()
     _sync()
     t0 = time.perf_counter()
     st.run(steps)
-    st.synchronize()
+    st.synchronize()  # polls under the communication watchdog when a peer can hang
     _sync()
     ctx.barrier()
     t1 = time.perf_counter()
     return ctx.allreduce_max(t1 - t0)
+
+
+def stencil_rate(ctx, gw, gh, dtype, steps, warmup, **kw) -> float:
+    from cuda_mpi_scratch_amd.models.stencil2d import Stencil2D, StencilConfig
+
+    st = Stencil2D(StencilConfig(global_width=gw, global_height=gh, dims="1x1", dtype=dtype, **kw), ctx)
+    dt = timed_run(st, ctx, steps, warmup)
+    rate = st.cells_per_step * steps / dt / 1e9
+    del st
+    return rate
+
+
+def dot_extras(ctx, extras: dict, n_global: int) -> None:
+    """BASELINE config 5: 2^30 fp64 over all ranks, device reduction + RCCL all-reduce."""
+    from cuda_mpi_scratch_amd.models.dot import DotProduct
+
+    n = ctx.world_size
+    gpu = torch.cuda.is_available()
+    dp = DotProduct(ctx, n_global, "f64", "single-pass", "rccl" if gpu else "torch")
+    value, dt = dp.timed(reps=20, warmup=3)
+    tag = "dot_2p30_f64" if n_global == 2**30 else f"dot_{n_global}_f64"
+    if ctx.is_root:
+        extras[f"{tag}_us"] = round(dt * 1e6, 2)
+        extras[f"{tag}_gbytes_per_s"] = round(dp.bytes_read / dt / 1e9, 1)
+        extras[f"{tag}_per_gpu_tbytes_per_s"] = round(dp.bytes_read / dt / 1e12 / n, 3)
+        extras[f"{tag}_verified"] = value == float(n_global)
+        extras[f"{tag}_reduce"] = "single-pass" + ((" + RCCL all-reduce" if gpu else " + gloo all-reduce")
+                                                   if n > 1 else "")
+    del dp
+
+
+def pingpong_extras(ctx, extras: dict, max_bytes: int) -> None:
+    """BASELINE metric 2 / config 3: ranks 0 <-> 1, 8 B - 256 MiB."""
+    from cuda_mpi_scratch_amd.models.pingpong import PingPong
+
+    sweep = []
+    plan = ((("rccl", ("blocking", "async", "overlap")), ("ipc", ("device",))) if torch.cuda.is_available()
+            else (("torch", ("blocking",)),))  # CPU rehearsal: gloo send/recv
+    for transport, modes in plan:
+        try:
+            sizes = [b for b in PINGPONG_SIZES if b <= max_bytes]
+            pp = PingPong(ctx, transport, sizes[-1])
+            for mode in modes:
+                for nb in sizes:
+                    reps = 50 if nb <= (1 << 20) else (10 if nb <= (32 << 20) else 5)
+                    rec = pp.run(nb, "async" if mode == "device" else mode, 3, reps)
+                    rec["mode"] = mode
+                    if "rtt_us" in rec:
+                        sweep.append(rec)
+            del pp
+        except Exception as e:  # noqa: BLE001 - reported, never fatal for the headline
+            extras[f"pingpong_{transport}_error"] = str(e)[:200]
+        _sync()
+        ctx.barrier()
+    if not ctx.is_root or not sweep:
+        return
+    for rec in sweep:
+        key = f"pingpong_{rec['transport']}_{rec['mode']}"
+        if rec["bytes"] == 8:
+            extras[f"{key}_8B_latency_us"] = round(rec["latency_us"], 2)
+        for label, nb in SUMMARY_SIZES.items():
+            if rec["bytes"] == nb:
+                extras[f"{key}_{label}_gbps"] = round(rec["gbps"], 2)
+        if rec["mode"] == "overlap" and rec["bytes"] == SUMMARY_SIZES["256MiB"]:
+            alone = rec.get("compute_alone_us", 0.0) + rec.get("comm_alone_us", 0.0)
+            if rec.get("overlapped_us"):
+                extras[f"{key}_256MiB_overlap_speedup"] = round(alone / rec["overlapped_us"], 3)
+    extras["pingpong_verified"] = all(r.get("passed", False) for r in sweep)
+    path = os.path.join("gpurun_out", f"bench_pingpong_n{ctx.world_size}.json")
+    try:
+        os.makedirs("gpurun_out", exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(sweep, f, indent=1)
+        extras["pingpong_sweep_file"] = path
+    except OSError as e:
+        extras["pingpong_sweep_file_error"] = str(e)[:120]
 
 
 def main(argv=None) -> int:
@@ -79,70 +169,82 @@ def main(argv=None) -> int:
     p.add_argument("--overlap", action="store_true", help="force the interior/exchange overlap schedule")
     p.add_argument("--loopback", action="store_true",
                    help="1 GPU: route the self-neighbour halos through RCCL (exercises the multi-GPU schedule)")
+    p.add_argument("--backend", default="auto", choices=["auto", "rccl", "ipc", "local", "torch"])
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-extras", action="store_true")
+    p.add_argument("--dot-n", type=int, default=2**30, help="global dot-product length (extras)")
+    p.add_argument("--pingpong-max", type=int, default=256 << 20, help="largest ping-pong message (extras)")
+    p.add_argument("--comm-timeout", type=float, default=300.0,
+                   help="seconds a halo / all-reduce wait may take before the run fails (0 = forever)")
     args = p.parse_args(argv)
 
-    from cuda_mpi_scratch_amd.models.pingpong import PingPong
     from cuda_mpi_scratch_amd.models.stencil2d import Stencil2D, StencilConfig
     from cuda_mpi_scratch_amd.parallel import choose_dims, init as dist_init
 
-    ctx = dist_init(backend="nccl" if torch.cuda.is_available() else "gloo")
+    gpu = torch.cuda.is_available()
+    ctx = dist_init(backend="nccl" if gpu else "gloo", timeout_s=max(60, int(args.comm_timeout) + 60))
     n = ctx.world_size
     if n != args.gpus and ctx.is_root:
         print(f"warning: --gpus {args.gpus} but world size {n}", file=sys.stderr)
+    if gpu:
+        from cuda_mpi_scratch_amd import hip
+
+        hip().set_comm_timeout(args.comm_timeout)  # RCCL / IPC waits fail instead of hanging
     # Default process grid: MPI_Dims_create order (rows >= cols; 8 -> 4 rows x 2
-    # columns, i.e. the BASELINE "2x4" grid read x-first as the reference's
-    # MPI_Cart_create does). Each rank's tile is then wider than tall
-    # (16384 x 8192 on 8 GPUs): the row-streaming kernel runs 7.5% faster on it
-    # than on 8192 x 16384 and the strided (column) halos are half as long
+    # columns). Each rank's tile is then wider than tall (16384 x 8192 on 8
+    # GPUs): the row-streaming kernel runs 7.5% faster on it than on
+    # 8192 x 16384 and the strided (column) halos are half as long
     # (profiles/r01_rot/tile_orientation.txt).
     rows, cols = choose_dims(n, args.dims, prefer="mpi")
     gw, gh = (int(v) for v in args.global_.lower().split("x"))
     cfg = StencilConfig(global_width=gw, global_height=gh, dims=f"{rows}x{cols}", dtype=args.dtype,
-                        kind="jacobi5", backend="auto",
+                        kind="jacobi5", backend=args.backend,
                         overlap=False if args.no_overlap else (True if args.overlap else None),
                         graph=not args.no_graph,
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup)
     value = st.cells_per_step * args.steps / dt / 1e9
-    extras: dict = {"backend": st.backend, "halo": st.halo_mode(), "graph": st.graph_status(),
+    halo = st.halo_mode()
+    exchange = ("none: 1x1 periodic self-exchange fused into the kernel addressing"
+                if st.solver is not None and st.solver.fused_periodic()
+                else f"{st.backend} point-to-point per neighbour")
+    extras: dict = {"backend": st.backend, "halo": halo, "halo_exchange": exchange, "graph": st.graph_status(),
                     "time_block": st.time_block,
                     "tile": f"{st.decomp.width}x{st.decomp.height}",
                     "process_grid": f"{rows} rows x {cols} cols of ranks"}
+    if gpu:
+        from cuda_mpi_scratch_amd import hip
+
+        extras["stencil_kernel"] = hip().last_stencil_dispatch()
     del st
-    torch.cuda.empty_cache()
+    if gpu:
+        torch.cuda.empty_cache()
 
     if not args.no_extras:
-        if n == 1:
-            cfg1 = StencilConfig(global_width=8192, global_height=8192, dims="1x1", dtype="f32",
-                                 time_block=args.time_block)
-            st1 = Stencil2D(cfg1, ctx)
-            dt1 = timed_run(st1, ctx, 600, 48)
-            extras["stencil_8192sq_f32_1gpu_gcells_per_s"] = round(st1.cells_per_step * 600 / dt1 / 1e9, 2)
-            del st1
+        try:
+            dot_extras(ctx, extras, args.dot_n)
+        except Exception as e:  # noqa: BLE001
+            extras["dot_error"] = str(e)[:200]
+        _sync()
+        ctx.barrier()
+        if gpu:
+            torch.cuda.empty_cache()
+        if n == 1 and gpu:
+            extras["stencil_8192sq_f32_1gpu_gcells_per_s"] = round(
+                stencil_rate(ctx, 8192, 8192, "f32", 600, 48, time_block=args.time_block), 2)
+            extras["stencil_8192sq_f64_1gpu_gcells_per_s"] = round(
+                stencil_rate(ctx, 8192, 8192, "f64", 600, 48, time_block=args.time_block), 2)
         else:
-            # GPU-GPU ping-pong between ranks 0 and 1 (BASELINE's second metric):
-            # RCCL send/recv, and device-initiated HIP IPC. Failures are reported
-            # in extras and never stop the headline line.
-            for transport in ("rccl", "ipc"):
-                try:
-                    pp = PingPong(ctx, transport, 256 << 20)
-                    small = pp.run(8, "async", 20, 200)
-                    big = pp.run(256 << 20, "async", 3, 20)
-                    if ctx.is_root:
-                        extras[f"pingpong_{transport}_8B_latency_us"] = round(small.get("latency_us", 0.0), 2)
-                        extras[f"pingpong_{transport}_256MiB_gbps"] = round(big.get("gbps", 0.0), 2)
-                        extras[f"pingpong_{transport}_verified"] = bool(small.get("passed")) and bool(big.get("passed"))
-                    del pp
-                except Exception as e:  # noqa: BLE001
-                    extras[f"pingpong_{transport}_error"] = str(e)[:200]
-                _sync()
-                ctx.barrier()
+            pingpong_extras(ctx, extras, args.pingpong_max)
         ctx.barrier()
 
     if ctx.is_root:
+        if exchange.startswith("none"):
+            model = f"2D stencil {gw}x{gh} {args.dtype} 5-point Jacobi, periodic, 1 rank (self-halo fused, no exchange)"
+        else:
+            model = (f"2D stencil {gw}x{gh} {args.dtype} 5-point Jacobi, periodic, {rows}x{cols} ranks, "
+                     f"{st_backend_label(extras['backend'])} halo exchange")
         line = {
             "metric": "2D stencil Gcells/sec",
             "value": round(value, 3),
@@ -157,16 +259,20 @@ def main(argv=None) -> int:
             "dtype": "fp32" if args.dtype == "f32" else "fp64",
             "data": "synthetic (deterministic random init per global cell)",
             "config": {
-                "model": f"2D stencil {gw}x{gh} {args.dtype} 5-point Jacobi, periodic, RCCL halo exchange",
+                "model": model,
                 "global_batch": gw * gh,
                 "seq_len": None,
-                "parallelism": f"cart{cols}x{rows}",  # ranks along x by ranks along y
+                "parallelism": f"cart{rows}x{cols} ({rows} rows x {cols} cols of ranks)",
             },
             "extras": extras,
         }
         print(json.dumps(line), flush=True)
     ctx.destroy()
     return 0
+
+
+def st_backend_label(backend: str) -> str:
+    return {"rccl": "RCCL", "ipc": "HIP IPC", "torch": "torch.distributed", "local": "local"}.get(backend, backend)
 
 
 if __name__ == "__main__":

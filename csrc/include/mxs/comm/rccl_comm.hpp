@@ -51,6 +51,7 @@ class RcclComm {
   RcclComm& operator=(const RcclComm&) = delete;
 
   ncclComm_t get() const { return comm_; }
+  bool aborted() const { return comm_ == nullptr; }
   int rank() const { return rank_; }
   int size() const { return nranks_; }
 
@@ -58,7 +59,8 @@ class RcclComm {
   // `msg` when the communicator is in an error state (e.g. a peer died).
   bool healthy(std::string* msg = nullptr) const;
   // Tear the communicator down without waiting for peers (after a failure).
-  void abort();
+  // Later calls on it fail with "communicator aborted"; the destructor skips it.
+  void abort() const;
   // Wait for `stream` under the communication watchdog (mxs/core/fault.hpp):
   // fails on an RCCL async error, or after comm_timeout() seconds (the
   // communicator is aborted first so the error path cannot block on it).
@@ -67,21 +69,26 @@ class RcclComm {
   // Sum-allreduce `count` elements in place or out of place on `stream`.
   template <typename T>
   void allreduce_sum(const T* send, T* recv, size_t count, hipStream_t stream) const {
-    MXS_RCCL_CHECK(ncclAllReduce(send, recv, count, rccl_type<T>(), ncclSum, comm_, stream));
+    MXS_RCCL_CHECK(ncclAllReduce(send, recv, count, rccl_type<T>(), ncclSum, live(), stream));
   }
   template <typename T>
   void send(const T* buf, size_t count, int peer, hipStream_t stream) const {
-    MXS_RCCL_CHECK(ncclSend(buf, count, rccl_type<T>(), peer, comm_, stream));
+    MXS_RCCL_CHECK(ncclSend(buf, count, rccl_type<T>(), peer, live(), stream));
   }
   template <typename T>
   void recv(T* buf, size_t count, int peer, hipStream_t stream) const {
-    MXS_RCCL_CHECK(ncclRecv(buf, count, rccl_type<T>(), peer, comm_, stream));
+    MXS_RCCL_CHECK(ncclRecv(buf, count, rccl_type<T>(), peer, live(), stream));
   }
   void group_start() const { MXS_RCCL_CHECK(ncclGroupStart()); }
   void group_end() const { MXS_RCCL_CHECK(ncclGroupEnd()); }
 
  private:
-  ncclComm_t comm_ = nullptr;
+  ncclComm_t live() const {
+    MXS_CHECK(comm_ != nullptr, "RCCL communicator aborted (an earlier wait timed out or failed)");
+    return comm_;
+  }
+  // Mutable: a watchdog timeout inside a const wait() aborts and clears it.
+  mutable ncclComm_t comm_ = nullptr;
   int rank_ = 0;
   int nranks_ = 1;
 };

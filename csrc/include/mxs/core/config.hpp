@@ -21,7 +21,8 @@ using index_t = std::int64_t;  // 64-bit indexing everywhere.
 
 // gfx950 wavefront width. Hard-coded on purpose (cdna_hip_programming.md §1).
 constexpr int kWaveSize = 64;
-// CUs on one MI355X (8 XCDs x 32 CUs).
+// CUs on one MI355X in SPX mode (8 XCDs x 32 CUs). Only a fallback: grids are
+// sized from the device attribute (runtime/hip_utils.hpp: device_cu_count()).
 constexpr int kNumCUs = 256;
 constexpr int kNumXCDs = 8;
 

@@ -89,6 +89,13 @@ template <typename T>
 void stencil5_rect(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0,
                    index_t y1, Stencil5Coeffs c, hipStream_t s);
 
+// Kernel form chosen by the most recent stencil launcher on this host process:
+// "stream_balanced_rot" (the persistent fp32 rotated-pair kernel the benchmarks
+// time), "stream_balanced", "stream_grid_rot", "stream_grid", "tb_tile",
+// "roll", "roll_wrap", "lds", "rect" or "box". A record of the host-side
+// dispatch decision, for tests and result records; graph replays do not update it.
+const char* last_stencil_dispatch();
+
 // (2R+1)^2 box stencil with arbitrary weights (row-major, (2R+1)^2 entries), R in {1, 2}.
 // Needs a ghost ring of at least R cells. LDS-tiled: each workgroup stages a
 // (64+2R) x (16+2R) input tile once and reads the (2R+1)^2 taps from LDS.

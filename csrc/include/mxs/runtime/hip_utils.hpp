@@ -142,6 +142,11 @@ class GraphExec {
   }
   bool valid() const { return exec_ != nullptr; }
   void launch(hipStream_t s) const { MXS_HIP_CHECK(hipGraphLaunch(exec_, s)); }
+  // Pre-stage the executable graph on the device so its first launch costs
+  // the same as every later one (kept out of timed regions by prepare()).
+  void upload(hipStream_t s) const {
+    if (exec_ && hipGraphUpload(exec_, s) != hipSuccess) (void)hipGetLastError();
+  }
 
  private:
   hipGraph_t graph_ = nullptr;
@@ -152,6 +157,24 @@ inline int current_device() {
   int d = -1;
   MXS_HIP_CHECK(hipGetDevice(&d));
   return d;
+}
+
+// Compute units of the current device, queried once per device. Grid sizing
+// uses this rather than a constant: a partitioned MI355X (CPX / DPX modes)
+// exposes fewer CUs per agent than the 256 of SPX mode.
+inline int device_cu_count() {
+  static int cached[64] = {};
+  const int d = current_device();
+  if (d < 0 || d >= 64) return kNumCUs;
+  if (cached[d] == 0) {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || cus <= 0) {
+      (void)hipGetLastError();
+      cus = kNumCUs;
+    }
+    cached[d] = cus;
+  }
+  return cached[d];
 }
 
 // "<marketing name> (<gcnArchName>)" of a HIP device, for result records.

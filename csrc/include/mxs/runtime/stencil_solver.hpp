@@ -7,7 +7,15 @@
 // latency-bound messages) and then advances S iterations in one pass over HBM
 // (kernels::stencil5_tb: the wave-streaming kernel, ~S x less HBM traffic per
 // iteration). S = 1 is the classic one-exchange-per-iteration loop. Results are
-// bitwise identical for any S. A remainder (iters mod S) runs as one shorter block.
+// bitwise identical for any S. run(K) splits K into ceil(K / S) near-equal
+// super-steps (K = 20, S = 16 -> 10 + 10, not 16 + a short HBM-bound 4), so a
+// short timed window costs the same per iteration as a long one.
+//
+// Physical (non-periodic) edges: the S-step kernels advance the ghost ring as
+// ordinary cells at every intermediate level, which is exactly right for a
+// neighbour's cells but would overwrite fixed boundary values. A topology with
+// any non-periodic dimension therefore runs S = 1 (one exchange per iteration),
+// so every backend agrees with the S = 1 result.
 //
 // Per super-step (cur -> nxt), with `overlap` on and S > 1:
 //
@@ -35,6 +43,7 @@
 
 #include <memory>
 #include <string>
+#include <vector>
 
 #include "mxs/halo/exchange.hpp"
 #include "mxs/kernels/kernels.hpp"
@@ -78,6 +87,12 @@ class StencilSolver {
 
   void step();            // enqueue one iteration
   void run(int iters);    // enqueue `iters` iterations (super-steps of time_block, graph replay)
+  // Make a later run(iters) free of one-off costs: capture (and pre-upload) the
+  // graphs of every super-step size run(iters) uses and launch every kernel
+  // shape once. The warm-up launches write only the scratch buffer and refresh
+  // the ghost ring, so the iteration state is unchanged. Collective (all ranks
+  // call it with the same iters: it runs halo exchanges). Idempotent per size.
+  void prepare(int iters);
   void exchange_only();   // enqueue a halo exchange of the current tile (no update)
   void synchronize();     // wait for everything enqueued so far
 
@@ -85,7 +100,7 @@ class StencilSolver {
   T* other() const { return nxt_; }
   hipStream_t main_stream() const { return main_.get(); }
   hipStream_t side_stream() const { return side_.get(); }
-  bool graph_active() const { return graphs_[0].valid(); }
+  bool graph_active() const;
   const std::string& graph_status() const { return graph_status_; }
   const HaloPlan& plan() const { return ex_->plan(); }
   bool fused_periodic() const { return fused_; }
@@ -96,25 +111,44 @@ class StencilSolver {
 
  private:
   void enqueue_block(T* cur, T* nxt, int S);  // S <= block_ iterations, one exchange
-  void enqueue_single(T* cur, T* nxt);  // 1 iteration (remainders)
   // `steps` iterations over core rows [r0, r1) x cols [c0, c1).
   void update(const T* in, T* out, int steps, index_t c0, index_t c1, index_t r0, index_t r1, hipStream_t s);
-  bool try_capture();
+  // Graphs of `chain` consecutive super-steps of size S, one per buffer
+  // orientation: g[0] starts from buf_a_, g[1] from buf_b_.
+  struct GraphSet {
+    int S = 0;
+    int chain = 1;
+    bool ok = false;
+    GraphExec g[2];
+  };
+  // Graphs for super-step size S, captured on first use with a chain of at
+  // most `count` super-steps (nullptr: graphs off or capture failed).
+  GraphSet* graphs_for(int S, int count);
+  bool capture(GraphSet& gs);
+  int chain_for(int S) const;
+  // (size, count) groups of run(iters): ceil(iters / block_) near-equal blocks.
+  struct Group {
+    int S, count;
+  };
+  void split(int iters, Group out[2]) const;
+  void run_group(int S, int count);
 
   TileGeom tile_;
   SolverConfig cfg_;
   int block_ = 1;
   int radius_ = 1;
+  T* buf_a_;
+  T* buf_b_;
   T* cur_;
   T* nxt_;
   const RcclComm* comm_ = nullptr;  // watchdog waits (synchronize) when set
   std::unique_ptr<HaloExchanger<T>> ex_;
   Stream main_, side_;
   Event fork_, interior_;
-  GraphExec graphs_[2];  // one super-step per buffer orientation (as captured)
-  int parity_ = 0;
-  int chain_ = 1;  // super-steps per graph launch
-  bool graph_tried_ = false;
+  std::vector<std::unique_ptr<GraphSet>> graphs_;  // at most kMaxGraphSets sizes, oldest evicted
+  static constexpr int kMaxGraphSets = 4;
+  std::vector<int> warmed_;  // super-step sizes whose kernels prepare() has launched
+  int chain_ = 1;  // super-steps per graph launch at S = block_
   bool fused_ = false;
   std::string graph_status_ = "not captured";
 };

@@ -25,6 +25,7 @@
 
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
+#include "mxs/runtime/hip_utils.hpp"
 
 namespace mxs {
 namespace kernels {
@@ -32,7 +33,7 @@ namespace {
 
 constexpr int kBlock = kDotBlock;
 constexpr int kWaves = kBlock / kWaveSize;
-constexpr int kUnroll = 4;
+constexpr int kUnroll = 8;
 
 template <typename T>
 struct V16 {
@@ -62,36 +63,55 @@ __device__ __forceinline__ Acc block_sum(Acc v, Acc* lds) {
   return r;
 }
 
+template <typename Acc>
+__device__ __forceinline__ Acc fma_acc(Acc a, Acc b, Acc c) {
+  if constexpr (sizeof(Acc) == 8) return __builtin_fma(a, b, c);
+  else return __builtin_fmaf(a, b, c);
+}
+
+// Per-thread partial over a block-contiguous streaming pattern: each workgroup
+// iteration covers kBlock x kUnroll consecutive 16-byte vectors (16 KiB of x
+// and of y at kUnroll = 4 ... 32 KiB at 8), every wave-instruction a whole
+// 1 KiB, and the grid strides over those chunks. Loads are non-temporal: the
+// vectors are read exactly once, so they should not displace anything in L2 /
+// the Infinity Cache. All kUnroll x 2 loads of a chunk are issued before any
+// arithmetic (kUnroll x 2 KiB in flight per wave).
 template <typename T, typename Acc>
 __device__ __forceinline__ Acc thread_partial(const T* __restrict__ x, const T* __restrict__ y, index_t n) {
   constexpr int N = V16<T>::N;
   using V = typename V16<T>::type;
+  constexpr index_t kChunk = index_t(kBlock) * kUnroll;  // vectors per workgroup iteration
   const index_t nvec = n / N;
   const V* __restrict__ xv = reinterpret_cast<const V*>(x);
   const V* __restrict__ yv = reinterpret_cast<const V*>(y);
-  const index_t tid = index_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  const index_t nthreads = index_t(gridDim.x) * blockDim.x;
+  const index_t stride = index_t(gridDim.x) * kChunk;
   Acc acc[kUnroll] = {};
-  index_t i = tid;
-  for (; i + (kUnroll - 1) * nthreads < nvec; i += kUnroll * nthreads) {
+  index_t base = index_t(blockIdx.x) * kChunk + threadIdx.x;
+  for (; base + (kUnroll - 1) * kBlock < nvec; base += stride) {  // whole chunks: no bounds checks
     V a[kUnroll], b[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      a[u] = xv[i + u * nthreads];
-      b[u] = yv[i + u * nthreads];
+      a[u] = __builtin_nontemporal_load(xv + base + u * kBlock);
+      b[u] = __builtin_nontemporal_load(yv + base + u * kBlock);
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u)
 #pragma unroll
-      for (int k = 0; k < N; ++k) acc[u] += Acc(a[u][k]) * Acc(b[u][k]);
+      for (int k = 0; k < N; ++k) acc[u] = fma_acc<Acc>(Acc(a[u][k]), Acc(b[u][k]), acc[u]);
   }
-  for (; i < nvec; i += nthreads) {
-    const V a = xv[i], b = yv[i];
 #pragma unroll
-    for (int k = 0; k < N; ++k) acc[0] += Acc(a[k]) * Acc(b[k]);
+  for (int u = 0; u < kUnroll; ++u) {  // the one ragged chunk
+    const index_t i = base + u * kBlock;
+    if (i < nvec) {
+      const V a = xv[i], b = yv[i];
+#pragma unroll
+      for (int k = 0; k < N; ++k) acc[u] = fma_acc<Acc>(Acc(a[k]), Acc(b[k]), acc[u]);
+    }
   }
   // Scalar tail (n not a multiple of the vector width).
-  for (index_t j = nvec * N + tid; j < n; j += nthreads) acc[0] += Acc(x[j]) * Acc(y[j]);
+  const index_t tid = index_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const index_t nthreads = index_t(gridDim.x) * blockDim.x;
+  for (index_t j = nvec * N + tid; j < n; j += nthreads) acc[0] = fma_acc<Acc>(Acc(x[j]), Acc(y[j]), acc[0]);
   Acc r = Acc(0);
 #pragma unroll
   for (int u = 0; u < kUnroll; ++u) r += acc[u];
@@ -173,7 +193,7 @@ int dot_grid_size(index_t n, int block) {
   // combine step (single-pass last block, two-pass finisher) is a short tail.
   const index_t per_block = index_t(block) * 16;
   const index_t want = (n + per_block - 1) / per_block;
-  return int(std::max<index_t>(1, std::min<index_t>(want, index_t(kNumCUs) * 4)));
+  return int(std::max<index_t>(1, std::min<index_t>(want, index_t(device_cu_count()) * 4)));
 }
 
 template <typename T, typename Acc>

@@ -7,6 +7,7 @@
 
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
+#include "mxs/runtime/hip_utils.hpp"
 
 namespace mxs {
 namespace kernels {
@@ -16,7 +17,7 @@ constexpr int kBlock = 256;
 
 inline int grid_for(index_t work, int per_thread = 1) {
   const index_t blocks = (work + index_t(kBlock) * per_thread - 1) / (index_t(kBlock) * per_thread);
-  const index_t cap = index_t(kNumCUs) * 8;
+  const index_t cap = index_t(device_cu_count()) * 8;
   return int(blocks < 1 ? 1 : (blocks > cap ? cap : blocks));
 }
 

@@ -35,9 +35,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
+#include "mxs/runtime/hip_utils.hpp"
 
 #include "stencil_device.hpp"
 
@@ -46,6 +48,11 @@ namespace kernels {
 namespace {
 using namespace detail;
 constexpr int kLdsRows = 16;
+
+// Host-side record of the kernel form the last stencil launcher picked (the
+// tests assert that their shapes reach the kernel the benchmarks time).
+std::atomic<const char*> g_last_dispatch{"none"};
+inline void note(const char* k) { g_last_dispatch.store(k, std::memory_order_relaxed); }
 
 // Tuned on MI355X with bench/stencil_tune.hip (profiles/stencil_tuning/*.log):
 // short strips whose ROWS+2 row loads are all issued up front beat long rolling
@@ -87,7 +94,9 @@ void stencil5_rows(const T* in, T* out, const TileGeom& g, index_t row_begin, in
     const size_t lds = size_t(kLdsRows + 2) * (kWaveSize * N + 2 * N) * sizeof(T);
     stencil5_lds_kernel<T, kLdsRows><<<dim3(unsigned(gx), unsigned(gy)), kBlock, lds, s>>>(
         in, out, g.pitch, g.core_offset(), g.width, row_begin, row_end, c0, c1);
+    note("lds");
   } else {
+    note("roll");
     if (g.width * int(sizeof(T)) >= 32768 * 4) launch_roll<T, 4>(in, out, g, row_begin, row_end, c0, c1, s);
     else launch_roll<T, 3>(in, out, g, row_begin, row_end, c0, c1, s);
   }
@@ -116,6 +125,7 @@ void stencil5_periodic(const T* in, T* out, const TileGeom& g, Stencil5Coeffs c,
   };
   if (g.width * int(sizeof(T)) >= 32768 * 4) go(std::integral_constant<int, 4>{});
   else go(std::integral_constant<int, 3>{});
+  note("roll_wrap");
   MXS_HIP_CHECK_LAUNCH();
 }
 
@@ -127,6 +137,7 @@ void launch_tb_tile(const T* in, T* out, const TileGeom& g, index_t x0, index_t 
   const dim3 grid(unsigned((x1 - x0 + TW - 1) / TW), unsigned((y1 - y0 + TH - 1) / TH));
   stencil5_tb1_kernel<T, S, TW, TH, WRAP><<<grid, 256, lds, s>>>(in, out, g.pitch, g.core_offset(), g.width,
                                                                  g.height, x0, x1, y0, y1, c0, c1);
+  note("tb_tile");
 }
 
 // Workgroups of the balanced stream kernel resident at once on this device:
@@ -184,23 +195,29 @@ void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
   const int blocks = balanced_blocks<T, S, WRAP>();
   if (groups * rows >= index_t(blocks) * 64) {
     const index_t share = (groups * rows + blocks - 1) / blocks;
-    if (kF32 && rot_ok<T>(g, x1, std::min(share, rows)))
+    if (kF32 && rot_ok<T>(g, x1, std::min(share, rows))) {
       stencil5_stream_balanced_kernel<T, S, stream_pf<T, S>(), WRAP, true, kF32><<<blocks, kBlock, 0, s>>>(
           in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
-    else
+      note("stream_balanced_rot");
+    } else {
       stencil5_stream_balanced_kernel<T, S, 3, WRAP><<<blocks, kBlock, 0, s>>>(
           in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
+      note("stream_balanced");
+    }
     return;
   }
   index_t ch = 512;
   while (ch > 64 && strips * ((rows + ch - 1) / ch) < 4096) ch /= 2;
   const dim3 grid(unsigned(groups), unsigned((rows + ch - 1) / ch));
-  if (kF32 && rot_ok<T>(g, x1, std::min(ch, rows)))
+  if (kF32 && rot_ok<T>(g, x1, std::min(ch, rows))) {
     stencil5_stream_kernel<T, S, stream_pf<T, S>(), WRAP, true, kF32><<<grid, kBlock, 0, s>>>(
         in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, ch, c0, c1);
-  else
+    note("stream_grid_rot");
+  } else {
     stencil5_stream_kernel<T, S, 3, WRAP><<<grid, kBlock, 0, s>>>(in, out, g.pitch, g.core_offset(), g.width,
                                                                   g.height, x0, x1, y0, y1, ch, c0, c1);
+    note("stream_grid");
+  }
 }
 
 // Dispatch by shape. Bulk rectangles take the wave-streaming kernel (Auto) or
@@ -269,9 +286,10 @@ void stencil5_rect(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
   MXS_CHECK(g.halo_x >= 1 && g.halo_y >= 1, "stencil5 needs a ghost ring of at least 1");
   MXS_CHECK(x0 >= 0 && y0 >= 0 && x1 <= g.width && y1 <= g.height, "rect out of the core");
   const index_t n = (x1 - x0) * (y1 - y0);
-  const index_t blocks = std::min<index_t>((n + kBlock - 1) / kBlock, index_t(kNumCUs) * 8);
+  const index_t blocks = std::min<index_t>((n + kBlock - 1) / kBlock, index_t(device_cu_count()) * 8);
   stencil5_rect_kernel<T><<<unsigned(blocks), kBlock, 0, s>>>(in, out, g.pitch, g.core_offset(), x0, x1 - x0, y0,
                                                               y1 - y0, T(c.center), T(c.neighbor));
+  note("rect");
   MXS_HIP_CHECK_LAUNCH();
 }
 
@@ -286,8 +304,11 @@ void stencil_box(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1,
     stencil_box_kernel<T, 1><<<grid, kBlock, 0, s>>>(in, out, g.pitch, g.core_offset(), x0, x1 - x0, y0, y1 - y0, w);
   else
     stencil_box_kernel<T, 2><<<grid, kBlock, 0, s>>>(in, out, g.pitch, g.core_offset(), x0, x1 - x0, y0, y1 - y0, w);
+  note("box");
   MXS_HIP_CHECK_LAUNCH();
 }
+
+const char* last_stencil_dispatch() { return g_last_dispatch.load(std::memory_order_relaxed); }
 
 #define MXS_INST_STENCIL(T)                                                                                    \
   template void stencil5_rows<T>(const T*, T*, const TileGeom&, index_t, index_t, Stencil5Coeffs, hipStream_t, \

@@ -15,6 +15,7 @@
 #include <string>
 
 #include "mxs/comm/rccl_comm.hpp"
+#include "mxs/core/fault.hpp"
 #include "mxs/halo/exchange.hpp"
 #include "mxs/kernels/kernels.hpp"
 #include "mxs/runtime/ipc.hpp"
@@ -160,6 +161,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
   m.def("auto_time_block", &kernels::auto_time_block, py::arg("width"), py::arg("height"),
         "measured default Jacobi steps per pass / halo exchange for a tile");
   m.def(
+      "last_stencil_dispatch", [] { return std::string(kernels::last_stencil_dispatch()); },
+      "kernel form chosen by the most recent stencil launcher (e.g. 'stream_balanced_rot')");
+  m.def("device_cu_count", &device_cu_count, "compute units of the current HIP device");
+  m.def(
       "stencil5_tb",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0,
          index_t y1, double c0, double c1, bool wrap, const std::string& dt, std::uintptr_t s,
@@ -224,6 +229,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("stream") = 0);
 
   // ------------------------------------------------------------------ RCCL
+  m.def(
+      "set_comm_timeout", [](double s) { comm_timeout() = s; }, py::arg("seconds"),
+      "communication watchdog: waits on RCCL streams / IPC peers fail after this many seconds (0 = forever)");
+  m.def("comm_timeout", [] { return comm_timeout(); });
   py::class_<RcclComm>(m, "RcclComm")
       .def(py::init([](py::bytes uid, int nranks, int rank) {
              return std::make_unique<RcclComm>(std::string(uid), nranks, rank);
@@ -239,6 +248,12 @@ PYBIND11_MODULE(_mxs_hip, m) {
              return py::make_tuple(ok, msg);
            })
       .def("abort", &RcclComm::abort)
+      .def_property_readonly("aborted", &RcclComm::aborted)
+      .def(
+          "wait",
+          [](const RcclComm& c, std::uintptr_t s, const std::string& what) { c.wait(strm(s), what.c_str()); },
+          py::arg("stream") = 0, py::arg("what") = "RCCL stream", py::call_guard<py::gil_scoped_release>(),
+          "wait for `stream` under the communication watchdog (set_comm_timeout)")
       .def(
           "allreduce_sum",
           [](const RcclComm& c, std::uintptr_t send, std::uintptr_t recv, size_t count, const std::string& dt,
@@ -334,6 +349,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def(
           "run", [](SolverHandle& h, int n) { h.visit([n](auto& s) { s.run(n); }); }, py::arg("iters"),
           py::call_guard<py::gil_scoped_release>())
+      .def(
+          "prepare", [](SolverHandle& h, int n) { h.visit([n](auto& s) { s.prepare(n); }); }, py::arg("iters"),
+          py::call_guard<py::gil_scoped_release>(),
+          "capture graphs and launch every kernel shape run(iters) uses, without advancing the state")
       .def("exchange_only", [](SolverHandle& h) { h.visit([](auto& s) { s.exchange_only(); }); })
       .def("synchronize", [](SolverHandle& h) { h.visit([](auto& s) { s.synchronize(); }); },
            py::call_guard<py::gil_scoped_release>())

@@ -27,15 +27,31 @@ void fill_stats(PingPongStats& s, const std::vector<double>& rtts) {
   s.median_rtt_us = median(rtts);
 }
 
-// HBM-streaming triad used as the "compute" side of the overlap mode.
-__global__ __launch_bounds__(256) void triad_kernel(float4* __restrict__ a, const float4* __restrict__ b,
-                                                    const float4* __restrict__ c, index_t n, int repeat) {
-  const index_t stride = index_t(gridDim.x) * blockDim.x;
-  for (int r = 0; r < repeat; ++r)
-    for (index_t i = index_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-      const float4 x = b[i], y = c[i];
-      a[i] = make_float4(x.x + 0.5f * y.x, x.y + 0.5f * y.y, x.z + 0.5f * y.z, x.w + 0.5f * y.w);
-    }
+// Compute side of the overlap mode: an ALU-bound kernel (independent FMA
+// chains in registers, one conditional store per thread), so the overlap figure
+// measures how well the transfer hides behind compute on separate streams, not
+// HBM contention between a streaming kernel and the copy engines / RCCL.
+__global__ __launch_bounds__(256) void fma_burn_kernel(float* __restrict__ sink, int iters) {
+  float a = float(threadIdx.x) * 1e-3f, b = float(blockIdx.x) * 1e-3f, c = 0.5f, d = 0.25f;
+  for (int i = 0; i < iters; ++i) {
+    a = __builtin_fmaf(a, 0.999f, 0.001f);
+    b = __builtin_fmaf(b, 0.998f, 0.002f);
+    c = __builtin_fmaf(c, 0.997f, 0.003f);
+    d = __builtin_fmaf(d, 0.996f, 0.004f);
+  }
+  if (a + b + c + d == -1.0f) sink[0] = a;  // never true: keeps the chains alive
+}
+
+// Per-process overlap scratch, created on first use and kept (never freed: it
+// must outlive every caller, and process exit reclaims it): the compute stream
+// and a 4-byte sink. The old per-call 3 GiB + stream allocation is gone.
+struct OverlapScratch {
+  Stream stream{true, 0};
+  DeviceBuffer<float> sink{1};
+};
+OverlapScratch& overlap_scratch() {
+  static OverlapScratch* s = new OverlapScratch();
+  return *s;
 }
 
 void round_trip(const RcclComm& comm, int peer, void* sendbuf, void* recvbuf, size_t bytes, hipStream_t s) {
@@ -98,34 +114,36 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
       rtts.push_back(double(e1.since(e0)) * 1000.0 / per);
     }
     if (mode == PingPongMode::Overlap) {
-      // Compute alone, comm alone, then both on separate streams.
-      const index_t n4 = index_t(64) << 20;  // 64 Mi float4 = 1 GiB per array
-      DeviceBuffer<float4> a(n4), bb(n4), c(n4);
-      MXS_HIP_CHECK(hipMemsetAsync(bb.get(), 0, bb.bytes(), stream));
-      MXS_HIP_CHECK(hipMemsetAsync(c.get(), 0, c.bytes(), stream));
-      Stream cs(true, 0);
-      auto launch_triad = [&](hipStream_t s) {
-        triad_kernel<<<kNumCUs * 4, 256, 0, s>>>(a.get(), bb.get(), c.get(), n4, 2);
-      };
-      MXS_HIP_CHECK(hipStreamSynchronize(stream));
+      // Comm alone, then compute alone (calibrated to about the same time),
+      // then both on separate streams.
+      OverlapScratch& ov = overlap_scratch();
+      hipStream_t cs = ov.stream.get();
+      const int grid = device_cu_count() * 4;
       Event t0(true), t1(true), t2(true);
-      t0.record(cs.get());
-      launch_triad(cs.get());
-      t1.record(cs.get());
-      t1.sync();
-      st.compute_alone_us = t1.since(t0) * 1000.0;
       t0.record(stream);
       for (int i = 0; i < per; ++i) round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
       t1.record(stream);
       t1.sync();
       st.comm_alone_us = t1.since(t0) * 1000.0;
-      // Both: start the triad, make the comm stream start with it, then join.
-      t0.record(cs.get());
+      const int probe = 4096;
+      t0.record(cs);
+      fma_burn_kernel<<<grid, 256, 0, cs>>>(ov.sink.get(), probe);
+      t1.record(cs);
+      t1.sync();
+      const double probe_us = std::max(1.0, double(t1.since(t0)) * 1000.0);
+      const int iters = int(std::min(1e8, std::max(256.0, probe * st.comm_alone_us / probe_us)));
+      t0.record(cs);
+      fma_burn_kernel<<<grid, 256, 0, cs>>>(ov.sink.get(), iters);
+      t1.record(cs);
+      t1.sync();
+      st.compute_alone_us = t1.since(t0) * 1000.0;
+      // Both: the comm stream starts with the compute launch, then join.
+      t0.record(cs);
       t0.wait_on(stream);
-      launch_triad(cs.get());
+      fma_burn_kernel<<<grid, 256, 0, cs>>>(ov.sink.get(), iters);
       for (int i = 0; i < per; ++i) round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
       t1.record(stream);
-      t2.record(cs.get());
+      t2.record(cs);
       t1.sync();
       t2.sync();
       st.overlapped_us = std::max(t1.since(t0), t2.since(t0)) * 1000.0;

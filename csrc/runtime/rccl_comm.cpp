@@ -45,10 +45,10 @@ void RcclComm::wait(hipStream_t stream, const char* what) const {
         if (!healthy(&msg)) raise_error(std::string(what) + ": RCCL communicator failed: " + msg);
         return false;
       },
-      what, [&] { (void)ncclCommAbort(comm_); });
+      what, [&] { abort(); });
 }
 
-void RcclComm::abort() {
+void RcclComm::abort() const {
   if (comm_) (void)ncclCommAbort(comm_);
   comm_ = nullptr;
 }

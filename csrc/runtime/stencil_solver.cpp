@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cmath>
 #include <utility>
+#include <vector>
 
 #include "mxs/core/fault.hpp"
 #include "mxs/core/trace.hpp"
@@ -12,10 +13,21 @@ namespace mxs {
 template <typename T>
 StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGeom& tile, T* buf_a, T* buf_b,
                                 const RcclComm* comm, const SolverConfig& cfg)
-    : tile_(tile), cfg_(cfg), cur_(buf_a), nxt_(buf_b), comm_(comm), main_(true, -1), side_(true, 0) {
+    : tile_(tile),
+      cfg_(cfg),
+      buf_a_(buf_a),
+      buf_b_(buf_b),
+      cur_(buf_a),
+      nxt_(buf_b),
+      comm_(comm),
+      main_(true, -1),
+      side_(true, 0) {
   // The main stream gets the higher priority (lower number): its short pack /
   // unpack / boundary launches should not queue behind the long interior sweep.
   block_ = cfg_.kind == StencilKind::Jacobi5 ? std::max(1, cfg_.time_block) : 1;
+  // Fixed boundary values on a physical edge must not be advanced as cells:
+  // time blocking is only exact when every edge is a neighbour's (see header).
+  if (!(topo.periodic_rows && topo.periodic_cols)) block_ = 1;
   MXS_CHECK(block_ <= kernels::kMaxTimeBlock, "time_block must be <= " << kernels::kMaxTimeBlock);
   MXS_CHECK(block_ <= tile_.width && block_ <= tile_.height,
             "time_block " << block_ << " exceeds the tile (" << tile_.width << "x" << tile_.height
@@ -35,12 +47,7 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   cfg_.bootstrap = nullptr;  // setup only; drop it (it may hold a Python callable)
   // Super-steps per graph launch: enough for ~1 ms of work per launch (the
   // launch gap is ~10 us), estimated at 5 T cell-iterations/s; at most 8.
-  if (cfg_.graph_supersteps > 0) {
-    chain_ = cfg_.graph_supersteps;
-  } else {
-    const double est_us = double(tile_.width) * double(tile_.height) * block_ / 5e6;
-    chain_ = std::max(1, std::min(8, int(std::ceil(1000.0 / std::max(est_us, 1.0)))));
-  }
+  chain_ = chain_for(block_);
   // Overlap only pays when there is a wire transfer to hide and an interior.
   if (plan.sends.empty() || tile_.height <= 2 * depth || tile_.width <= 2 * depth) cfg_.overlap = false;
   const bool all_self = plan.sends.empty() && int(plan.self_copies.size()) == (corners ? kNumDirs : 4);
@@ -68,17 +75,6 @@ void StencilSolver<T>::update(const T* in, T* out, int steps, index_t c0, index_
   } else {
     kernels::stencil5_rect<T>(in, out, tile_, c0, c1, r0, r1, cfg_.coeffs, s);
   }
-}
-
-template <typename T>
-void StencilSolver<T>::enqueue_single(T* cur, T* nxt) {
-  hipStream_t m = main_.get();
-  if (fused_) {
-    kernels::stencil5_periodic<T>(cur, nxt, tile_, cfg_.coeffs, m);
-    return;
-  }
-  ex_->exchange(cur, m);
-  update(cur, nxt, 1, 0, tile_.width, 0, tile_.height, m);
 }
 
 // Stream roles: the MAIN stream (the capture origin, high priority) carries the
@@ -137,13 +133,25 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
 }
 
 template <typename T>
-bool StencilSolver<T>::try_capture() {
+int StencilSolver<T>::chain_for(int S) const {
+  if (cfg_.graph_supersteps > 0) return cfg_.graph_supersteps;
+  const double est_us = double(tile_.width) * double(tile_.height) * S / 5e6;
+  return std::max(1, std::min(8, int(std::ceil(1000.0 / std::max(est_us, 1.0)))));
+}
+
+template <typename T>
+bool StencilSolver<T>::graph_active() const {
+  for (const auto& gs : graphs_)
+    if (gs->ok) return true;
+  return false;
+}
+
+template <typename T>
+bool StencilSolver<T>::capture(GraphSet& gs) {
   MXS_TRACE_RANGE("stencil.graph_capture");
-  graph_tried_ = true;
-  // One graph per orientation: graphs_[0] = cur->nxt, graphs_[1] = nxt->cur.
   for (int k = 0; k < 2; ++k) {
-    T* a = k == 0 ? cur_ : nxt_;
-    T* b = k == 0 ? nxt_ : cur_;
+    T* a = k == 0 ? buf_a_ : buf_b_;
+    T* b = k == 0 ? buf_b_ : buf_a_;
     hipGraph_t g = nullptr;
     if (hipStreamBeginCapture(main_.get(), hipStreamCaptureModeThreadLocal) != hipSuccess) {
       (void)hipGetLastError();
@@ -152,8 +160,8 @@ bool StencilSolver<T>::try_capture() {
     }
     bool ok = true;
     try {
-      for (int c = 0; c < chain_; ++c) {  // chain_ consecutive super-steps per graph
-        enqueue_block(a, b, block_);
+      for (int c = 0; c < gs.chain; ++c) {  // chain consecutive super-steps per graph
+        enqueue_block(a, b, gs.S);
         std::swap(a, b);
       }
     } catch (const std::exception& e) {
@@ -165,49 +173,88 @@ bool StencilSolver<T>::try_capture() {
       (void)hipGetLastError();
       if (ok) graph_status_ = "hipStreamEndCapture failed";
       if (g) (void)hipGraphDestroy(g);
-      for (auto& x : graphs_) x.reset();
       return false;
     }
-    if (!graphs_[k].adopt(g)) {
+    if (!gs.g[k].adopt(g)) {
       graph_status_ = "hipGraphInstantiate failed";
-      for (auto& x : graphs_) x.reset();
       return false;
     }
+    gs.g[k].upload(main_.get());
   }
   graph_status_ = "captured";
-  parity_ = 0;
   return true;
+}
+
+template <typename T>
+typename StencilSolver<T>::GraphSet* StencilSolver<T>::graphs_for(int S, int count) {
+  if (!cfg_.use_graph) return nullptr;
+  for (auto& gs : graphs_)
+    if (gs->S == S) return gs->ok ? gs.get() : nullptr;
+  if (int(graphs_.size()) >= kMaxGraphSets) graphs_.erase(graphs_.begin());
+  auto gs = std::make_unique<GraphSet>();
+  gs->S = S;
+  gs->chain = std::max(1, std::min(chain_for(S), count));  // a short first run gets a short chain
+  gs->ok = capture(*gs);
+  if (!gs->ok) {
+    gs->g[0].reset();
+    gs->g[1].reset();
+  }
+  graphs_.push_back(std::move(gs));
+  return graphs_.back()->ok ? graphs_.back().get() : nullptr;
+}
+
+template <typename T>
+void StencilSolver<T>::split(int iters, Group out[2]) const {
+  out[0] = out[1] = Group{0, 0};
+  if (iters <= 0) return;
+  const int blocks = (iters + block_ - 1) / block_;
+  const int base = iters / blocks, extra = iters % blocks;  // extra blocks of base + 1
+  out[0] = Group{base + 1, extra};
+  out[1] = Group{base, blocks - extra};
+}
+
+template <typename T>
+void StencilSolver<T>::run_group(int S, int count) {
+  if (count <= 0) return;
+  int i = 0;
+  if (GraphSet* gs = graphs_for(S, count)) {
+    for (; i + gs->chain <= count; i += gs->chain) {
+      MXS_TRACE_RANGE("stencil.graph_launch");
+      gs->g[cur_ == buf_a_ ? 0 : 1].launch(main_.get());
+      if (gs->chain % 2) std::swap(cur_, nxt_);  // an odd chain ends on the other buffer
+    }
+  }
+  for (; i < count; ++i) {  // no graph, or fewer than `chain` super-steps left
+    enqueue_block(cur_, nxt_, S);
+    std::swap(cur_, nxt_);
+  }
 }
 
 template <typename T>
 void StencilSolver<T>::run(int iters) {
   MXS_TRACE_RANGE("stencil.run");
-  const int supers = iters / block_, rem = iters % block_;
-  if (supers > 0 && cfg_.use_graph && !graph_tried_) try_capture();
-  int i = 0;
-  if (graphs_[0].valid()) {
-    for (; i + chain_ <= supers; i += chain_) {
-      MXS_TRACE_RANGE("stencil.graph_launch");
-      graphs_[parity_].launch(main_.get());
-      if (chain_ % 2) {  // an odd chain ends on the other buffer
-        parity_ ^= 1;
-        std::swap(cur_, nxt_);
-      }
-    }
+  Group gr[2];
+  split(iters, gr);
+  for (const Group& g : gr) run_group(g.S, g.count);
+}
+
+template <typename T>
+void StencilSolver<T>::prepare(int iters) {
+  MXS_TRACE_RANGE("stencil.prepare");
+  Group gr[2];
+  split(iters, gr);
+  for (const Group& g : gr) {
+    if (g.count <= 0) continue;
+    (void)graphs_for(g.S, g.count);
+    if (std::find(warmed_.begin(), warmed_.end(), g.S) != warmed_.end()) continue;
+    // One untimed launch of every kernel of this super-step size: cur -> nxt
+    // without swapping (nxt is scratch; the exchange rewrites cur's ghost ring
+    // with the same values a real super-step would).
+    enqueue_block(cur_, nxt_, g.S);
+    warmed_.push_back(g.S);
   }
-  for (; i < supers; ++i) {  // no graph, or fewer than chain_ super-steps left
-    enqueue_block(cur_, nxt_, block_);
-    std::swap(cur_, nxt_);
-    parity_ ^= 1;
-  }
-  // Remainder: one shorter super-step (S = rem <= block_ fits the ghost ring),
-  // run eagerly; a lone step takes the single-iteration path.
-  if (rem > 0) {
-    if (rem == 1) enqueue_single(cur_, nxt_);
-    else enqueue_block(cur_, nxt_, rem);
-    std::swap(cur_, nxt_);
-    parity_ ^= 1;  // keep the graph orientation in sync with the buffers
-  }
+  main_.sync();
+  side_.sync();
 }
 
 template <typename T>

@@ -45,7 +45,7 @@ class DotProduct:
             self.x = torch.rand(self.n, dtype=t, generator=g).to(dev)
             self.y = torch.rand(self.n, dtype=t, generator=g).to(dev)
         self.ws = ops.DotWorkspace(self.n, dev) if dev.type == "cuda" else None
-        self.comm = make_rccl_comm(ctx) if (allreduce == "rccl" and dev.type == "cuda") else None
+        self.comm = ctx.native_comm() if (allreduce == "rccl" and dev.type == "cuda") else None
         self.total = torch.zeros(1, dtype=torch.float64, device=dev)
 
     def local(self) -> torch.Tensor:
@@ -80,6 +80,54 @@ class DotProduct:
         dt = ctx.allreduce_max(time.perf_counter() - t0)
         self.partial = float(part.item())
         return value, dt
+
+
+    def reduce_global(self) -> torch.Tensor:
+        """Enqueue one full dot (local kernel + device all-reduce) on the current
+        stream without synchronising; returns the device tensor holding it."""
+        import torch.distributed as dist
+
+        part = self.local()
+        if self.ctx.world_size > 1:
+            if self.comm is not None:
+                s = torch.cuda.current_stream().cuda_stream
+                self.comm.allreduce_sum(part.data_ptr(), self.total.data_ptr(), 1, "f64", s)
+                return self.total
+            res = part.clone()
+            dist.all_reduce(res)  # torch process group (gloo on CPU)
+            return res
+        return part
+
+    def timed(self, reps: int = 20, warmup: int = 3) -> tuple[float, float]:
+        """Back-to-back dots (kernel + RCCL all-reduce per rep, stream-ordered,
+        one host sync at the end), bracketed by barrier + device sync; returns
+        (global dot, seconds per dot, max over ranks). On CPU the all-reduce is
+        the torch process group's."""
+        cuda = self.x.is_cuda
+
+        def sync():
+            if cuda:
+                torch.cuda.synchronize()
+
+        for _ in range(warmup):
+            self.reduce_global()
+        sync()
+        self.ctx.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            res = self.reduce_global()
+        if self.comm is not None:
+            self.comm.wait(torch.cuda.current_stream().cuda_stream, "dot all-reduce")
+        sync()
+        self.ctx.barrier()
+        dt = self.ctx.allreduce_max((time.perf_counter() - t0) / reps)
+        return float(res.item()), dt
+
+    @property
+    def bytes_read(self) -> int:
+        """HBM bytes one global dot reads (both vectors, all ranks)."""
+        return 2 * self.n_global * self.x.element_size()
 
 
 def main(argv=None) -> int:

@@ -10,7 +10,9 @@ and unidirectional bandwidth (bytes / (RTT/2)).
 Transports:
   ``rccl``   native RCCL send/recv between rank 0 and rank 1 (xGMI), modes
              blocking (host sync per round trip), async (stream-pipelined,
-             hipEvent-timed) and overlap (async beside an HBM-streaming kernel);
+             hipEvent-timed) and overlap (async beside an ALU-bound kernel on a
+             second stream, sized to the transfer time: compute alone, comm
+             alone and both together are reported);
   ``ipc``    device-initiated: HIP IPC mailboxes in each rank's HBM, one
              persistent kernel per rank writes the payload into the peer's
              mailbox over xGMI and spins on a system-scope flag for the echo
@@ -58,7 +60,7 @@ class PingPong:
         self.recv = torch.empty(max_bytes, dtype=torch.uint8, device=dev)
         self.comm = None
         if transport == "rccl" or transport == "loopback":
-            self.comm = make_rccl_comm(ctx)
+            self.comm = ctx.native_comm()
         self.peer = 1 - ctx.rank if ctx.world_size > 1 else ctx.rank
         self.mailbox = self.peer_mailbox = None
         if transport == "ipc":
@@ -80,9 +82,11 @@ class PingPong:
 
     def run(self, nbytes: int, mode: str = "blocking", warmup: int = 5, reps: int = 20) -> dict:
         assert nbytes <= self.max_bytes
+        rec = {"bytes": nbytes, "transport": self.transport, "mode": mode}
+        if self.transport == "torch":
+            return self._run_torch(nbytes, warmup, reps, rec)
         H = hip()
         stream = torch.cuda.current_stream().cuda_stream
-        rec = {"bytes": nbytes, "transport": self.transport, "mode": mode}
         if self.transport in ("rccl", "loopback"):
             if not self.active:
                 return rec
@@ -123,8 +127,9 @@ class PingPong:
         pattern = (torch.arange(nbytes, dtype=torch.int64, device=s.device) * 131 + 7) % 251
         s.copy_(pattern.to(torch.uint8))
         times = []
+        sync = torch.cuda.synchronize if s.is_cuda else (lambda: None)
         for i in range(warmup + reps):
-            torch.cuda.synchronize()
+            sync()
             t0 = time.perf_counter()
             if self.ctx.rank == 0:
                 dist.send(s, 1)
@@ -132,7 +137,7 @@ class PingPong:
             else:
                 dist.recv(r, 0)
                 dist.send(r, 0)
-            torch.cuda.synchronize()
+            sync()
             if i >= warmup:
                 times.append((time.perf_counter() - t0) * 1e6)
         sm = summarize(times)

@@ -91,8 +91,12 @@ class Stencil2D:
         tb = cfg.time_block
         if tb <= 0 and dev.type == "cuda":
             tb = hip().auto_time_block(d.width, d.height)
+        # A physical (non-periodic) edge holds fixed boundary values that the
+        # S-step kernels would advance as cells: time blocking needs every edge
+        # to be a neighbour's (the native solver enforces the same rule).
         self.time_block = (max(1, min(tb, d.width, d.height))
-                           if (dev.type == "cuda" and cfg.kind == "jacobi5" and cfg.init != "rank") else 1)
+                           if (dev.type == "cuda" and cfg.kind == "jacobi5" and cfg.init != "rank"
+                               and cfg.periodic) else 1)
         h = max(h, self.time_block)
         C = core()
         if dev.type == "cuda":
@@ -130,7 +134,7 @@ class Stencil2D:
         if backend in ("rccl", "local", "ipc"):
             H = hip()
             if backend == "rccl":
-                self.comm = make_rccl_comm(self.ctx)
+                self.comm = self.ctx.native_comm()
             torch.cuda.synchronize()
             kind = H.StencilKind.BOX if cfg.kind == "box" else H.StencilKind.JACOBI5
             be = {"rccl": H.HaloBackend.RCCL, "local": H.HaloBackend.LOCAL, "ipc": H.HaloBackend.IPC}[backend]
@@ -171,6 +175,13 @@ class Stencil2D:
             return
         for _ in range(iters):
             self._python_step()
+
+    def prepare(self, iters: int):
+        """Collective: take every one-off cost of a later ``run(iters)`` now
+        (graph capture + upload, first launch of each kernel shape) without
+        advancing the field. Benchmarks call it before their timed window."""
+        if self.solver is not None and iters > 0:
+            self.solver.prepare(iters)
 
     def _python_step(self):
         cfg, g = self.cfg, self.geom
@@ -215,6 +226,7 @@ class Stencil2D:
         """Assemble the global core grid on every rank (tests / validation)."""
         import torch.distributed as dist
 
+        self.synchronize()  # the native solver writes on its own streams
         local = self.core_view().detach().cpu().clone()
         d = self.decomp
         if not self.ctx.is_distributed:
@@ -327,6 +339,7 @@ def main(argv=None) -> int:
         if ctx.is_root:
             print(f"resumed from {args.resume} at iteration {hdr.iteration}", file=sys.stderr)
     st.run(args.warmup)
+    st.prepare(args.iters)
     st.synchronize()
     ctx.barrier()
     t0 = time.perf_counter()

@@ -41,6 +41,16 @@ class DistContext:
     device: torch.device = field(default_factory=_default_device)
     backend: str = "none"
     owns_group: bool = False
+    _native_comm: object = field(default=None, repr=False)
+
+    def native_comm(self):
+        """The process's native RCCL communicator over all ranks, created on
+        first use and shared by every workload (stencil halo, ping-pong, dot).
+        One communicator, created in the same order on every rank right after
+        the torch process group, so the unique-id keys always line up."""
+        if self._native_comm is None:
+            self._native_comm = make_rccl_comm(self)
+        return self._native_comm
 
     @property
     def is_distributed(self) -> bool:
@@ -106,6 +116,7 @@ class DistContext:
         return [bytes(store.get(f"{k}/{r}")) for r in range(self.world_size)]
 
     def destroy(self) -> None:
+        self._native_comm = None  # workloads still holding it keep it alive
         if self.owns_group and dist.is_initialized():
             dist.destroy_process_group()
             self.owns_group = False

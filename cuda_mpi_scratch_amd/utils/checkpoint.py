@@ -71,6 +71,9 @@ def create_grid_file(path: str, header: GridHeader) -> None:
 def save(stencil, path: str) -> GridHeader:
     """Collective: write the core of every rank of `stencil` (a models.Stencil2D)."""
     d, ctx = stencil.decomp, stencil.ctx
+    # The native solver runs on its own non-blocking streams and switches its
+    # current buffer as soon as work is queued: wait for it before reading.
+    stencil.synchronize()
     core = stencil.core_view().detach().cpu().numpy()
     header = GridHeader(core.dtype.itemsize, d.global_width, d.global_height, stencil.iteration, stencil.cfg.seed)
     if ctx.is_root:
@@ -97,7 +100,10 @@ def load(stencil, path: str) -> GridHeader:
         raise ValueError(f"{path}: {header.width}x{header.height} grid, expected "
                          f"{d.global_width}x{d.global_height}")
     block = np.ascontiguousarray(arr[d.y0:d.y0 + d.height, d.x0:d.x0 + d.width])
+    stencil.synchronize()  # no queued solver work may land after the copy
     stencil.core_view().copy_(torch.from_numpy(block))
+    if stencil.device.type == "cuda":
+        torch.cuda.synchronize()  # the copy ran on torch's stream, not the solver's
     stencil.synchronize()
     stencil.iteration = header.iteration
     del arr

@@ -24,9 +24,13 @@ int main(int argc, char** argv) {
   };
   if (env.rank() == 0) {
     send("Hello from rank 0", 1, tag0to1);
-    std::cout << "Task 0:  received message \"" << receive(1, tag1to0) << '"' << std::endl;
+    // Receive first, then print the whole line in one write: the two ranks'
+    // lines must not interleave on a shared stdout.
+    const std::string msg = receive(1, tag1to0);
+    std::cout << "Task 0:  received message \"" + msg + "\"\n" << std::flush;
   } else if (env.rank() == 1) {
-    std::cout << "Task 1:  received message \"" << receive(0, tag0to1) << '"' << std::endl;
+    const std::string msg = receive(0, tag0to1);
+    std::cout << "Task 1:  received message \"" + msg + "\"\n" << std::flush;
     send("Hello from rank 1", 0, tag1to0);
   }
   return 0;

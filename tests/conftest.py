@@ -29,4 +29,6 @@ def gpu():
 
 @pytest.fixture(scope="session")
 def build_dir():
-    return os.path.join(ROOT, "build")
+    # MXS_BUILD_DIR: run the native-binary tests against another build tree
+    # (e.g. the host-sanitizer build of scripts/cpu_sanitize.sh).
+    return os.environ.get("MXS_BUILD_DIR") or os.path.join(ROOT, "build")

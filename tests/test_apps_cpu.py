@@ -9,7 +9,8 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BIN = os.path.join(ROOT, "build", "bin")
+# MXS_BIN_DIR: run the same tests against another build (scripts/cpu_sanitize.sh).
+BIN = os.environ.get("MXS_BIN_DIR") or os.path.join(ROOT, "build", "bin")
 MPIEXEC = shutil.which("mpiexec", path="/opt/conda/bin") or shutil.which("mpiexec")
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "stencil_3x3_16_5")
 

@@ -20,13 +20,40 @@ def _check(line, n, steps, warmup):
 
 def test_bench_single_rank_cpu():
     r = run_ranks("bench", 1, {"argv": ["--global", "128x96", "--steps", "6", "--warmup", "2", "--no-extras"]})
-    _check(r[0]["line"], 1, 6, 2)
+    d = _check(r[0]["line"], 1, 6, 2)
+    assert d["config"]["parallelism"].startswith("cart1x1")
 
 
-def test_bench_two_ranks_cpu_extras_survive():
-    r = run_ranks("bench", 2, {"argv": ["--gpus", "2", "--global", "128x96", "--steps", "5", "--warmup", "1"]})
+def test_bench_single_rank_cpu_dot_extras():
+    r = run_ranks("bench", 1, {"argv": ["--global", "128x96", "--steps", "4", "--warmup", "1", "--dot-n", "4096"]})
+    ex = _check(r[0]["line"], 1, 4, 1)["extras"]
+    assert ex["dot_4096_f64_verified"] is True and ex["dot_4096_f64_gbytes_per_s"] > 0
+
+
+def test_bench_two_ranks_cpu_extras():
+    r = run_ranks("bench", 2, {"argv": ["--gpus", "2", "--global", "128x96", "--steps", "5", "--warmup", "1",
+                                        "--dot-n", "8192", "--pingpong-max", "4096"]})
     assert r[1]["line"] is None and r[0]["rc"] == 0 and r[1]["rc"] == 0
     d = _check(r[0]["line"], 2, 5, 1)
-    assert d["config"]["parallelism"] == "cart1x2"
+    # MPI_Dims_create order: 2 ranks -> 2 rows x 1 col, printed rows first.
+    assert d["config"]["parallelism"] == "cart2x1 (2 rows x 1 cols of ranks)"
+    assert "2x1 ranks" in d["config"]["model"]
     ex = d["extras"]
-    assert any(k.startswith("pingpong_rccl") for k in ex) and any(k.startswith("pingpong_ipc") for k in ex)
+    assert ex["process_grid"] == "2 rows x 1 cols of ranks"
+    assert ex["dot_8192_f64_verified"] is True
+    # CPU rehearsal of the ping-pong sweep: gloo send/recv, 8 B .. 4 KiB.
+    assert ex["pingpong_torch_blocking_8B_latency_us"] > 0 and ex["pingpong_verified"] is True
+    assert ex["pingpong_sweep_file"].endswith("bench_pingpong_n2.json")
+
+
+def test_bench_eight_ranks_cpu_walks_the_8gpu_path():
+    """The N = 8 code path end to end (4 rows x 2 cols, torch halo backend on gloo):
+    the same grid choice, exchange plan and extras the 8-GPU node runs."""
+    r = run_ranks("bench", 8, {"argv": ["--gpus", "8", "--global", "256x128", "--steps", "3", "--warmup", "1",
+                                        "--dot-n", "65536", "--pingpong-max", "64"]}, timeout=240)
+    assert all(x["rc"] == 0 for x in r) and all(x["line"] is None for x in r[1:])
+    d = _check(r[0]["line"], 8, 3, 1)
+    assert d["config"]["parallelism"] == "cart4x2 (4 rows x 2 cols of ranks)"
+    ex = d["extras"]
+    assert ex["tile"] == "128x32" and ex["backend"] == "torch"
+    assert ex["dot_65536_f64_verified"] is True and ex["pingpong_verified"] is True

@@ -1,0 +1,162 @@
+"""The kernel the benchmarks time, under test.
+
+bench.py's headline (32768^2 fp32) and the BASELINE single-GPU / 8-GPU-tile
+configs dispatch the persistent balanced wave-streaming kernel
+(``stencil5_stream_balanced_kernel``, rotated-pair fp32 form) — chosen only
+for rectangles of >= ~32k (strip group x row) work items, so the small-shape
+tests elsewhere never reach it. These tests run shapes that do, assert the
+dispatch, and compare against a float64-emulated reference on the GPU
+(torch ops, the same rounding as the kernels' fma sequence) or bitwise against
+single-step runs.
+"""
+import time
+
+import pytest
+import torch
+
+from cuda_mpi_scratch_amd import core, hip
+from cuda_mpi_scratch_amd.models.stencil2d import Stencil2D, StencilConfig
+from cuda_mpi_scratch_amd.ops import jacobi_reference_global
+from cuda_mpi_scratch_amd.ops.stencil import dtype_name
+
+pytestmark = pytest.mark.gpu
+
+
+def _core(buf, g, w, h):
+    return buf.view(g.total_height(), g.pitch)[g.halo_y:g.halo_y + h, g.x_origin + g.halo_x:g.x_origin + g.halo_x + w]
+
+
+def _frozen_edge_reference(full, steps, c0=0.2, c1=0.2):
+    """S Jacobi steps on core + ghost ring (float64-emulated fma for fp32); the
+    border stays frozen, so everything >= S cells inside it is exact."""
+    u = full.clone()
+    f32 = u.dtype == torch.float32
+    for _ in range(steps):
+        n, s, w, e, c = u[:-2, 1:-1], u[2:, 1:-1], u[1:-1, :-2], u[1:-1, 2:], u[1:-1, 1:-1]
+        sums = (n + s) + (w + e)
+        new = u.clone()
+        if f32:
+            new[1:-1, 1:-1] = (float(torch.tensor(c1, dtype=torch.float32)) * sums.double()
+                               + (torch.tensor(c0, dtype=torch.float32, device=u.device) * c).double()).float()
+        else:
+            new[1:-1, 1:-1] = c1 * sums + c0 * c
+        u = new
+    return u
+
+
+@pytest.mark.parametrize("w,h,steps,dtype,kernel", [
+    (8192, 8192, 12, torch.float32, "stream_balanced_rot"),   # BASELINE config 2 (1 GPU), auto S
+    (4096, 8192, 16, torch.float32, "stream_balanced_rot"),
+    (16384, 4096, 16, torch.float32, "stream_balanced_rot"),  # wide tile, deepest block
+    (4096, 4096, 12, torch.float64, "stream_balanced"),       # fp64 balanced path
+    (8192, 8192, 8, torch.float64, "stream_balanced"),
+])
+def test_balanced_wrap_matches_periodic_reference(gpu, w, h, steps, dtype, kernel):
+    g = core().TileGeom.aligned(w, h, 1, 1, torch.tensor([], dtype=dtype).element_size())
+    gen = torch.Generator(device=gpu).manual_seed(w + h + steps)
+    u = torch.rand(h, w, generator=gen, device=gpu, dtype=torch.float64).to(dtype)
+    src = torch.zeros(g.alloc_elems(), dtype=dtype, device=gpu)
+    _core(src, g, w, h).copy_(u)
+    dst = torch.zeros_like(src)
+    hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, 0, w, 0, h, 0.2, 0.2, True, dtype_name(src),
+                      torch.cuda.current_stream().cuda_stream, "auto")
+    assert hip().last_stencil_dispatch() == kernel
+    torch.cuda.synchronize()
+    ref = jacobi_reference_global(u, steps)
+    tol = 2e-6 if dtype == torch.float32 else 1e-14
+    assert (_core(dst, g, w, h).double() - ref.double()).abs().max().item() <= tol
+
+
+@pytest.mark.parametrize("w,h,steps,rect,dtype,kernel", [
+    # The 8-GPU tile of the 32768^2 problem (4 rows x 2 cols -> 16384 x 8192),
+    # halved in both directions to keep the test quick: non-wrap, 16-deep ring.
+    (8192, 4096, 16, None, torch.float32, "stream_balanced_rot"),
+    # Ragged right edge (x_end % 4 != 0): the non-rotated balanced form.
+    (8190, 4096, 16, None, torch.float32, "stream_balanced"),
+    # Interior rectangle of the overlap schedule (vector-aligned columns).
+    (8192, 4096, 12, (16, 8176, 12, 4084), torch.float32, "stream_balanced_rot"),
+    (4096, 4096, 12, None, torch.float64, "stream_balanced"),
+])
+def test_balanced_ghost_ring_matches_reference(gpu, w, h, steps, rect, dtype, kernel):
+    esz = torch.tensor([], dtype=dtype).element_size()
+    g = core().TileGeom.aligned(w, h, steps, steps, esz)
+    gen = torch.Generator(device=gpu).manual_seed(steps * 7 + w)
+    full = torch.rand(g.total_height(), g.total_width(), generator=gen, device=gpu, dtype=torch.float64).to(dtype)
+    src = torch.zeros(g.alloc_elems(), dtype=dtype, device=gpu)
+    src.view(g.total_height(), g.pitch)[:, g.x_origin:g.x_origin + g.total_width()] = full
+    dst = torch.full_like(src, -3.0)
+    x0, x1, y0, y1 = rect or (0, w, 0, h)
+    hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, x0, x1, y0, y1, 0.2, 0.2, False, dtype_name(src),
+                      torch.cuda.current_stream().cuda_stream, "auto")
+    assert hip().last_stencil_dispatch() == kernel
+    torch.cuda.synchronize()
+    got = _core(dst, g, w, h)
+    ref = _frozen_edge_reference(full, steps)[steps:steps + h, steps:steps + w]
+    tol = 2e-6 if dtype == torch.float32 else 1e-14
+    assert (got[y0:y1, x0:x1].double() - ref[y0:y1, x0:x1].double()).abs().max().item() <= tol
+    mask = torch.ones(h, w, dtype=torch.bool, device=gpu)
+    mask[y0:y1, x0:x1] = False
+    assert bool((got[mask] == -3.0).all()), "the kernel wrote outside its rectangle"
+
+
+@pytest.mark.parametrize("dtype", ["f32", "f64"])
+def test_solver_blocked_run_bitwise_equals_single_steps(gpu, dtype):
+    """run(20) at the auto time block (8192^2: S = 12 -> two super-steps of 10)
+    equals 20 one-step iterations bit for bit, and prepare() changes nothing."""
+    kw = dict(global_width=8192, global_height=8192, dims="1x1", dtype=dtype, seed=99)
+    blocked = Stencil2D(StencilConfig(**kw))
+    assert blocked.time_block == 12
+    blocked.prepare(20)
+    blocked.prepare(20)  # idempotent
+    blocked.run(20)
+    blocked.synchronize()
+    single = Stencil2D(StencilConfig(time_block=1, **kw))
+    single.run(20)
+    single.synchronize()
+    assert blocked.graph_status() == "captured"
+    assert torch.equal(blocked.core_view(), single.core_view())
+
+
+def test_solver_odd_splits_bitwise(gpu):
+    """Near-equal splits of awkward counts (17 = 9 + 8, 33 = 11 + 11 + 11 at S = 12)
+    and a graph reused across calls stay exact."""
+    kw = dict(global_width=2048, global_height=1024, dims="1x1", dtype="f32", seed=5)
+    a = Stencil2D(StencilConfig(**kw))
+    for n in (17, 33, 1, 12):
+        a.run(n)
+    a.synchronize()
+    b = Stencil2D(StencilConfig(time_block=1, **kw))
+    b.run(17 + 33 + 1 + 12)
+    b.synchronize()
+    assert torch.equal(a.core_view(), b.core_view())
+
+
+def test_non_periodic_runs_single_step_and_keeps_boundary(gpu):
+    """Physical edges hold fixed values: the solver must not time-block them
+    (S-step kernels advanced the ghost ring as cells)."""
+    w, h, iters = 640, 200, 14
+    st = Stencil2D(StencilConfig(global_width=w, global_height=h, dims="1x1", dtype="f32", periodic=False,
+                                 time_block=12, seed=3))
+    assert st.time_block == 1 and st.solver.time_block() == 1
+    full0 = st.full_view().clone()
+    st.run(iters)
+    st.synchronize()
+    hx, hy = st.geom.halo_x, st.geom.halo_y
+    ref = _frozen_edge_reference(full0, iters)[hy:hy + h, hx:hx + w]
+    assert (st.core_view().double() - ref.double()).abs().max().item() <= 2e-6
+    assert torch.equal(st.full_view()[0], full0[0]), "a physical boundary row changed"
+
+
+def test_headline_rate_floor(gpu):
+    """Regression floor near the measured rate: 32768^2 fp32, a 20-step window
+    after prepare() (the driver's --steps 20 --warmup 5). Measured ~7 T cells/s."""
+    st = Stencil2D(StencilConfig(global_width=32768, global_height=32768, dims="1x1", dtype="f32"))
+    st.run(5)
+    st.prepare(20)
+    st.synchronize()
+    t0 = time.perf_counter()
+    st.run(20)
+    st.synchronize()
+    rate = st.cells_per_step * 20 / (time.perf_counter() - t0) / 1e9
+    assert hip().last_stencil_dispatch() == "stream_balanced_rot"
+    assert rate > 5000, f"{rate:.0f} Gcells/s"
