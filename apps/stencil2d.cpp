@@ -84,7 +84,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   const int time_block =
       (backend == "mpi-staged" || !all_periodic)
           ? 1
-          : int(cli.get_int("time-block", iters > 0 && lw >= 64 && lh >= 64 ? kernels::auto_time_block(lw, lh) : 1));
+          : int(cli.get_int("time-block", iters > 0 && lw >= 64 && lh >= 64 ? kernels::auto_time_block(lw, lh, int(sizeof(T))) : 1));
   const TileGeom g = TileGeom::aligned(lw, lh, std::max(sw / 2, time_block), std::max(sh / 2, time_block),
                                        int(sizeof(T)));
   std::unique_ptr<RcclComm> comm;

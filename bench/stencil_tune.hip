@@ -190,6 +190,32 @@ Variant balanced(const float* in, float* out, const TileGeom& g, int per_cu, flo
   return v;
 }
 
+// Two-stage wave pipeline (S = S0 + S1 levels; 512-thread workgroups).
+template <int S0, int S1, int PF, bool WRAP = true>
+Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullptr) {
+  int per_cu = 0, cus = 0;
+  MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu, reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP>), 512, 0));
+  MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const int blocks = std::max(1, per_cu * cus);
+  char buf[128];
+  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "");
+  auto mk = [=](const float* I, float* O) {
+    return [=](hipStream_t s) {
+      constexpr int OW = StreamShape<float, S0 + S1>::OW;
+      const index_t groups = ((g.width + OW - 1) / OW + 3) / 4;
+      const index_t share = (groups * g.height + blocks - 1) / blocks;
+      stencil5_stream_pipe_kernel<S0, S1, PF, WRAP><<<blocks, 512, 0, s>>>(
+          I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, 0.2f, 0.2f);
+    };
+  };
+  Variant v{buf, mk(in, out)};
+  v.launch2 = mk(out, const_cast<float*>(in));
+  v.steps = S0 + S1;
+  v.ref = ref_for<S0 + S1, WRAP>(in, out, g, tmp);
+  return v;
+}
+
 int main(int argc, char** argv) {
   const index_t W = argc > 1 ? atol(argv[1]) : 32768;
   const index_t H = argc > 2 ? atol(argv[2]) : 32768;
@@ -280,6 +306,23 @@ int main(int argc, char** argv) {
     vs.push_back(balanced<16, 6, false, true>(in, out, g, 0));
     vs.push_back(balanced<12, 6, true, true>(in, out, g, 0, tmp));
     vs.push_back(balanced<14, 6, true, true>(in, out, g, 0, tmp));
+  } else if (focus && std::string(focus) == "pipe") {  // two-stage wave pipeline vs the single-wave kernel
+    vs.push_back(balanced<16, 3, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<10, 6, true, true>(in, out, g, 0, tmp));
+    vs.push_back(pipe<8, 8, 3>(in, out, g, tmp));
+    vs.push_back(pipe<10, 10, 3>(in, out, g, tmp));
+    vs.push_back(pipe<10, 10, 6>(in, out, g, tmp));
+    vs.push_back(pipe<12, 12, 3>(in, out, g, tmp));
+    vs.push_back(pipe<12, 12, 6>(in, out, g, tmp));
+    vs.push_back(pipe<16, 16, 3>(in, out, g, tmp));
+  } else if (focus && std::string(focus) == "deep") {  // time blocks past 16 (AGPR-backed window, 1 wave/SIMD)
+    vs.push_back(balanced<16, 3, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<10, 6, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<18, 3, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<20, 3, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<20, 6, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<24, 3, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<20, 3, true, true>(in, out, g, 2, tmp));
   } else if (focus && std::string(focus) == "s") {  // S choice for the balanced launch
     vs.push_back(balanced<12, 3>(in, out, g, 0));
     vs.push_back(balanced<12, 3, true>(in, out, g, 0, tmp));

@@ -74,11 +74,27 @@ bool stencil5_periodic_supported(const TileGeom& g);
 //                iterates in LDS; S <= 8 for the bulk tile);
 //   RegisterRoll same as Auto.
 constexpr int kMaxTimeBlock = 16;
-// Measured default S for a w x h tile (profiles/stencil_tuning/tunes_*): the
-// wave-streaming pass is VALU-bound beyond S ~ 8, so a deeper block only pays
-// where the chunk/strip aprons are small against the tile: S = 16 from 2^27
-// cells (8192 x 16384: tie, 16384^2 and up: +8-12%), S = 12 below (8192^2: +5%).
-inline int auto_time_block(index_t w, index_t h) { return w * h >= (index_t(1) << 27) ? 16 : 12; }
+// fp32 blocks of 17..32 steps run on the two-stage wave pipeline
+// (stencil5_stream_pipe_kernel: two waves per column strip, levels split
+// between them and handed over through LDS). Needs fp32, x0 and x1 multiples
+// of 4 (whole vectors); see stencil5_deep_supported().
+constexpr int kMaxTimeBlockDeep = 32;
+// Measured default S for a w x h tile of `elem_bytes`-byte cells
+// (profiles/stencil_tuning/tunes_*, profiles/r02_deep/pipe_*): fp32 takes the
+// two-stage pipeline at S = 24 (32768^2: 8.0 vs 7.85 T cells/s at S = 16;
+// 8192^2: 6.3 vs 5.7); fp64 and the single-wave kernels: S = 16 from 2^27
+// cells, S = 12 below (the pass is VALU-bound beyond S ~ 8, so a deeper block
+// only pays where the chunk / strip aprons are small against the tile).
+inline int auto_time_block(index_t w, index_t h, int elem_bytes = 4) {
+  if (elem_bytes == 4 && w >= 1024 && h >= 1024) return 24;
+  return w * h >= (index_t(1) << 27) ? 16 : 12;
+}
+// Whether a `steps`-step stencil5_tb launch over [x0, x1) can run: every
+// steps <= kMaxTimeBlock; deeper blocks only for fp32 on whole vectors.
+template <typename T>
+constexpr bool stencil5_deep_supported(int steps, index_t x0, index_t x1) {
+  return steps <= kMaxTimeBlock || (steps <= kMaxTimeBlockDeep && sizeof(T) == 4 && x0 % 4 == 0 && x1 % 4 == 0);
+}
 template <typename T>
 void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0, index_t y1,
                  Stencil5Coeffs c, bool wrap, hipStream_t s, StencilVariant v = StencilVariant::Auto);
@@ -90,8 +106,9 @@ void stencil5_rect(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
                    index_t y1, Stencil5Coeffs c, hipStream_t s);
 
 // Kernel form chosen by the most recent stencil launcher on this host process:
-// "stream_balanced_rot" (the persistent fp32 rotated-pair kernel the benchmarks
-// time), "stream_balanced", "stream_grid_rot", "stream_grid", "tb_tile",
+// "stream_pipe" (the two-stage fp32 pipeline of blocks > 16 steps, the one the
+// benchmarks time), "stream_balanced_rot" (persistent single-wave fp32
+// rotated-pair kernel), "stream_balanced", "stream_grid_rot", "stream_grid", "tb_tile",
 // "roll", "roll_wrap", "lds", "rect" or "box". A record of the host-side
 // dispatch decision, for tests and result records; graph replays do not update it.
 const char* last_stencil_dispatch();

@@ -63,8 +63,9 @@ struct SolverConfig {
   // wrap-around addressing (ghost cells untouched; exchange_only() still performs
   // an explicit exchange for dumps).
   bool fuse_periodic_self = true;
-  // Jacobi iterations per halo exchange / per launch (1..kernels::kMaxTimeBlock);
-  // the tile's ghost ring must be at least this deep.
+  // Jacobi iterations per halo exchange / per launch (1..kernels::kMaxTimeBlock,
+  // up to kMaxTimeBlockDeep for fp32 without overlap: the two-stage pipeline;
+  // larger requests are capped); the tile's ghost ring must be at least this deep.
   int time_block = 1;
   StencilKind kind = StencilKind::Jacobi5;
   kernels::Stencil5Coeffs coeffs;
@@ -93,6 +94,12 @@ class StencilSolver {
   // the ghost ring, so the iteration state is unchanged. Collective (all ranks
   // call it with the same iters: it runs halo exchanges). Idempotent per size.
   void prepare(int iters);
+  // `passes` more untimed launches of run(iters)'s super-step shapes, with the
+  // same state-preserving rule as prepare() (scratch output, ghost refresh):
+  // brings the device to its sustained clocks before a short timed window
+  // (a cold 20-step window at 32768^2 runs ~20% slower than a warm one,
+  // profiles/r02_deep/clock_ramp.txt). Collective: same passes on all ranks.
+  void warm(int iters, int passes);
   void exchange_only();   // enqueue a halo exchange of the current tile (no update)
   void synchronize();     // wait for everything enqueued so far
 

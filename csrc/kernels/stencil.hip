@@ -243,14 +243,56 @@ void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, i
   launch_stream<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
 }
 
+// Two-stage pipeline (S = 17..32, fp32): levels split S0 = S/2, S1 = S - S0;
+// 6 input rows in flight up to S = 28 (the fetch ring fits beside the
+// windows at 2 waves/SIMD), 3 above. One 512-thread workgroup per CU: the
+// occupancy API decides, as for the single-wave balanced kernel.
+template <int S>
+constexpr int pipe_pf() {
+  return S <= 28 ? 6 : 3;
+}
+
+template <int S, bool WRAP>
+int pipe_blocks() {
+  static int blocks = 0;
+  if (blocks == 0) {
+    int occ = 0;
+    MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S / 2, S - S / 2, pipe_pf<S>(), WRAP>),
+        2 * kBlock, 0));
+    blocks = std::max(occ, 1) * device_cu_count();
+  }
+  return blocks;
+}
+
+template <int S, bool WRAP>
+void launch_pipe(const float* in, float* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
+                 float c0, float c1, hipStream_t s) {
+  constexpr int OW = StreamShape<float, S>::OW;
+  const index_t strips = (x1 - x0 + OW - 1) / OW;
+  const index_t rows = y1 - y0;
+  const index_t groups = (strips + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int blocks = pipe_blocks<S, WRAP>();
+  const index_t share = (groups * rows + blocks - 1) / blocks;
+  MXS_CHECK(std::min(share, rows) * g.pitch * index_t(sizeof(float)) < (index_t(1) << 31),
+            "stencil5_tb: a pipeline chunk must stay under 2 GiB (buffer-descriptor stores)");
+  stencil5_stream_pipe_kernel<S / 2, S - S / 2, pipe_pf<S>(), WRAP><<<blocks, 2 * kBlock, 0, s>>>(
+      in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
+  note("stream_pipe");
+}
+
 template <typename T, bool WRAP, int S = 1>
 void dispatch_tb(int steps, const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
                  T c0, T c1, StencilVariant v, hipStream_t s) {
   if constexpr (S <= kMaxTimeBlock) {
     if (steps == S) return launch_tb<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, v, s);
     return dispatch_tb<T, WRAP, S + 1>(steps, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+  } else if constexpr (S <= kMaxTimeBlockDeep && sizeof(T) == 4) {
+    if (steps == S) return launch_pipe<S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
+    return dispatch_tb<T, WRAP, S + 1>(steps, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   } else {
-    MXS_CHECK(false, "stencil5_tb: steps must be in [1, " << kMaxTimeBlock << "], got " << steps);
+    MXS_CHECK(false, "stencil5_tb: steps must be in [1, " << (sizeof(T) == 4 ? kMaxTimeBlockDeep : kMaxTimeBlock)
+                                                          << "], got " << steps);
   }
 }
 }  // namespace
@@ -261,6 +303,9 @@ void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, 
   if (x1 <= x0 || y1 <= y0) return;
   constexpr int N = Vec16<T>::N;
   MXS_CHECK(x0 >= 0 && y0 >= 0 && x1 <= g.width && y1 <= g.height, "stencil5_tb: rect out of the core");
+  MXS_CHECK(stencil5_deep_supported<T>(steps, x0, x1),
+            "stencil5_tb: " << steps << "-step blocks need fp32 and a column range of whole vectors (got "
+                            << sizeof(T) * 8 << "-bit, [" << x0 << ", " << x1 << "))");
   MXS_CHECK(x0 % N == 0, "stencil5_tb: x0 must be a multiple of the vector width");
   MXS_CHECK((g.pitch % N) == 0 && ((g.x_origin + g.halo_x) % N) == 0, "stencil5_tb needs a TileGeom::aligned layout");
   const int sa = ((steps + N - 1) / N) * N;

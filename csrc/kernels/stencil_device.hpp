@@ -945,6 +945,223 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
   }
 }
 
+// ------------------------------------------------- two-stage wave pipeline
+// Deeper time blocks without more registers per wave. A single wave holds a
+// three-slot window per level (12 VGPRs per level at fp32), so S = 16 already
+// needs ~237 VGPRs; S = 20 in one wave drops to 1 wave per SIMD and spills to
+// AGPRs, measured 35-45% slower per iteration (profiles/r02_deep). Here a
+// column strip is streamed by TWO waves of the workgroup: stage 0 runs levels
+// 1..S0 on rows fetched from HBM and hands each level-S0 row to stage 1
+// through an LDS ring (one ds_write_b128 / ds_read_b128 per lane and row);
+// stage 1 runs levels S0+1..S0+S1 and stores. Each wave keeps only its own
+// levels' windows, so S = S0 + S1 reaches 20-32 at 2 waves per SIMD, and HBM
+// sees one read + one write per cell per S iterations.
+//
+// Lock-step: all 8 waves of the workgroup (4 strips x 2 stages) advance in
+// blocks of PF iterations with one barrier per block. Stage 0 emits its k-th
+// output row at its iteration 3*S0 - 1 + k; stage 1 starts T1 blocks later and
+// consumes row k at its iteration k, so every row it reads was written at
+// least one barrier earlier; a ring of 3*PF rows per strip is never
+// overwritten before it is read (see the derivation in docs/PERF.md). Both
+// stages run the same number of blocks (their extra iterations read / write
+// rows outside every stored cell's dependency cone). The apron is that of a
+// single S-level wave (the strip's edge contamination spreads one column per
+// level through both stages): OW = 256 - 2 * SA(S) output columns per strip.
+template <int S0, int S1, int PF>
+struct PipeShape {
+  static constexpr int S = S0 + S1;
+  static constexpr int RING = 3 * PF;                      // rows per strip in the LDS ring
+  static constexpr int T1 = (3 * S0 + PF - 1 + PF - 1) / PF;  // stage-1 start block: ceil((3*S0 + PF - 1) / PF)
+};
+
+template <int S0, int S1, int PF, bool WRAP>
+__device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* __restrict__ out, index_t pitch,
+                                           index_t core_off, index_t W, index_t H, index_t xw, index_t x_end,
+                                           index_t ys, index_t ye, float c0, float c1, f32x4* __restrict__ ring,
+                                           int stage) {
+  static_assert(PF % 3 == 0, "the window rotates through 3 slots: PF must be a multiple of 3");
+  using P = PipeShape<S0, S1, PF>;
+  constexpr int S = P::S, RING = P::RING, T1 = P::T1;
+  using Sh = StreamShape<float, S>;
+  constexpr int N = Sh::N, SA = Sh::SA, AL = SA / N;
+  const int lane = threadIdx.x & (kWaveSize - 1);
+  const index_t gx = xw - SA + index_t(lane) * N;
+  const index_t rows = ye - ys;
+  const index_t n_it0 = rows + 2 * S1 + 3 * S0 - 1;  // stage 0: level-S0 rows [ys - S1, ye + S1)
+  const index_t n_it1 = rows + 3 * S1 - 1;           // stage 1: output rows [ys, ye)
+  const index_t blocks0 = (n_it0 + PF - 1) / PF, blocks1 = T1 + (n_it1 + PF - 1) / PF;
+  const index_t blocks = blocks0 > blocks1 ? blocks0 : blocks1;
+  f32x4* __restrict__ my = ring + lane;
+
+  if (stage == 0) {  // wave-uniform
+    index_t lx;
+    if (xw >= x_end) {
+      lx = 0;  // idle strip past the rectangle: any valid address, nothing it makes is stored
+    } else if constexpr (WRAP) {
+      if (W >= kWaveSize * N) lx = gx < 0 ? gx + W : (gx >= W ? gx - W : gx);
+      else lx = ((gx % W) + W) % W;
+    } else {
+      const index_t last_col = (W + N - 1) / N * N + SA - N;
+      lx = gx < last_col ? gx : last_col;
+    }
+    const float* __restrict__ pin = in + core_off + lx;
+    const index_t last_row = ye + S - 1;
+    index_t next = ys - S;
+    if constexpr (WRAP) next = next < 0 ? next + H : next;
+    auto fetch = [&]() -> f32x4 {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(pin + next * pitch);
+      if constexpr (WRAP) {
+        ++next;
+        next = next == H ? 0 : next;
+      } else {
+        next = next < last_row ? next + 1 : next;
+      }
+      return v;
+    };
+    f32x4 win[3][S0];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int l = 0; l < S0; ++l) win[q][l] = f32x4(0.f);
+    f32x4 pf[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) pf[k] = fetch();
+    constexpr int kWarm = (3 * (S0 - 1)) / PF * PF;  // see stream_chunk_rot: level l matters from iteration 3l + 2
+#pragma unroll 1
+    for (int ib = 0; ib < kWarm; ib += PF) {
+#pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
+        const int b = (ib + k) / 3;
+        win[p2][0] = rot_in(pf[k]);
+        pf[k] = fetch();
+#pragma unroll
+        for (int l = S0 - 2; l >= 0; --l)
+          if (l <= b) win[p0][l + 1] = jac_rot4f(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+      }
+      __syncthreads();
+    }
+#pragma unroll 1
+    for (index_t i = kWarm; i < blocks * PF; i += PF) {
+      // Ring slot of this block's first row k = i - (3*S0 - 1) (wave-uniform, once per block).
+      const int base = int((i - (3 * S0 - 1) + index_t(RING) * (3 * S0)) % RING);
+#pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
+        win[p2][0] = rot_in(pf[k]);
+        pf[k] = fetch();
+        f32x4 top;
+#pragma unroll
+        for (int l = S0 - 1; l >= 0; --l) {
+          const f32x4 o = jac_rot4f(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+          if (l == S0 - 1) top = o;
+          else win[p0][l + 1] = o;
+        }
+        // Row k = j - (3*S0 - 1) of stage 1's input (rotated layout); writes
+        // for k < 0 land in slots no reader touches before they are rewritten.
+        const int slot = base + k < RING ? base + k : base + k - RING;
+        my[slot * kWaveSize] = top;
+      }
+      __syncthreads();
+    }
+  } else {
+    // Output descriptor over rows [ys, ye) (see stream_chunk_rot).
+    const float* obase = out + core_off + (xw - SA) + ys * pitch;
+    const unsigned long long ob = reinterpret_cast<unsigned long long>(obase);
+    const unsigned ob_lo = __builtin_amdgcn_readfirstlane(unsigned(ob)),
+                   ob_hi = __builtin_amdgcn_readfirstlane(unsigned(ob >> 32));
+    float* obase_u = reinterpret_cast<float*>((static_cast<unsigned long long>(ob_hi) << 32) | ob_lo);
+    const int nbytes = __builtin_amdgcn_readfirstlane(int(rows * pitch * index_t(sizeof(float))));
+    const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(obase_u, 0, nbytes, 0x00020000);
+    const bool store_lane = lane >= AL && lane < kWaveSize - AL && gx < x_end && xw < x_end;
+    const unsigned lane_off = unsigned(lane) * unsigned(N * sizeof(float));
+    const unsigned row_bytes = unsigned(pitch) * unsigned(sizeof(float));
+    constexpr unsigned kDrop = 0x80000000u;
+    f32x4 win[3][S1];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int l = 0; l < S1; ++l) win[q][l] = f32x4(0.f);
+#pragma unroll 1
+    for (int t = 0; t < T1; ++t) __syncthreads();  // stage 0 fills the ring
+    constexpr int kWarm = (3 * (S1 - 1)) / PF * PF;
+#pragma unroll 1
+    for (int ib = 0; ib < kWarm; ib += PF) {
+      f32x4 inrow[PF];
+      const int base = (ib / PF) % 3 * PF;  // RING = 3 * PF and ib is a multiple of PF
+#pragma unroll
+      for (int k = 0; k < PF; ++k) inrow[k] = my[(base + k) * kWaveSize];
+#pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
+        const int b = (ib + k) / 3;
+        win[p2][0] = inrow[k];
+#pragma unroll
+        for (int l = S1 - 2; l >= 0; --l)
+          if (l <= b) win[p0][l + 1] = jac_rot4f(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+      }
+      __syncthreads();
+    }
+#pragma unroll 1
+    for (index_t i = kWarm; i < (blocks - T1) * PF; i += PF) {
+      f32x4 inrow[PF];
+      const int base = int((i / PF) % 3) * PF;
+#pragma unroll
+      for (int k = 0; k < PF; ++k) inrow[k] = my[(base + k) * kWaveSize];
+#pragma unroll
+      for (int k = 0; k < PF; ++k) {
+        const index_t j = i + k;
+        const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
+        win[p2][0] = inrow[k];
+        f32x4 top;
+#pragma unroll
+        for (int l = S1 - 1; l >= 0; --l) {
+          const f32x4 o = jac_rot4f(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+          if (l == S1 - 1) top = o;
+          else win[p0][l + 1] = o;
+        }
+        const index_t r = j - (3 * S1 - 1);
+        const bool ok = store_lane && r >= 0 && r < rows;
+        const unsigned off = ok ? lane_off + unsigned(r) * row_bytes : kDrop;
+        const f32x4 nat = rot_out(top);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, nat),
+                                               orsrc, int(off), 0, 2 /* nt */);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Balanced persistent launch of the two-stage pipeline: 512-thread workgroups
+// (4 strips x 2 stages), equal shares of (4-strip group) x rows as in
+// stencil5_stream_balanced_kernel. fp32 only (rotated-pair layout); needs
+// x_end % 4 == 0 and a chunk under 2 GiB (the output buffer descriptor).
+template <int S0, int S1, int PF, bool WRAP>
+__global__ __launch_bounds__(2 * kBlock) void stencil5_stream_pipe_kernel(
+    const float* __restrict__ in, float* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
+    index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, float c0, float c1) {
+  using P = PipeShape<S0, S1, PF>;
+  constexpr int OW = StreamShape<float, P::S>::OW;
+  __shared__ f32x4 ring[kWavesPerBlock * P::RING * kWaveSize];
+  const index_t rows = y_end - y_begin;
+  const index_t strips = (x_end - x_begin + OW - 1) / OW;
+  const index_t groups = (strips + kWavesPerBlock - 1) / kWavesPerBlock;
+  const index_t total = groups * rows;
+  const int wave = threadIdx.x / kWaveSize;
+  const int strip = wave % kWavesPerBlock, stage = wave / kWavesPerBlock;
+  index_t a = index_t(blockIdx.x) * share;
+  const index_t b = a + share < total ? a + share : total;
+#pragma unroll 1
+  while (a < b) {  // workgroup-uniform: all 8 waves take every chunk (barriers inside)
+    const index_t grp = a / rows, r0 = a - grp * rows;
+    const index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
+    const index_t xw = x_begin + (grp * kWavesPerBlock + strip) * OW;
+    pipe_chunk<S0, S1, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1,
+                                 ring + strip * P::RING * kWaveSize, stage);
+    a += r1 - r0;
+  }
+}
+
 }  // namespace detail
 }  // namespace kernels
 }  // namespace mxs

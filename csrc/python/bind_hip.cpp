@@ -158,8 +158,15 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("row_begin"), py::arg("row_end"),
       py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2, py::arg("dtype") = "f32", py::arg("stream") = 0,
       py::arg("variant") = "auto");
-  m.def("auto_time_block", &kernels::auto_time_block, py::arg("width"), py::arg("height"),
-        "measured default Jacobi steps per pass / halo exchange for a tile");
+  m.def(
+      "auto_time_block",
+      [](index_t w, index_t h, const std::string& dt) {
+        return kernels::auto_time_block(w, h, parse_dtype(dt) == DType::F32 ? 4 : 8);
+      },
+      py::arg("width"), py::arg("height"), py::arg("dtype") = "f32",
+      "measured default Jacobi steps per pass / halo exchange for a tile");
+  m.attr("MAX_TIME_BLOCK") = kernels::kMaxTimeBlock;
+  m.attr("MAX_TIME_BLOCK_DEEP") = kernels::kMaxTimeBlockDeep;
   m.def(
       "last_stencil_dispatch", [] { return std::string(kernels::last_stencil_dispatch()); },
       "kernel form chosen by the most recent stencil launcher (e.g. 'stream_balanced_rot')");
@@ -353,6 +360,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
           "prepare", [](SolverHandle& h, int n) { h.visit([n](auto& s) { s.prepare(n); }); }, py::arg("iters"),
           py::call_guard<py::gil_scoped_release>(),
           "capture graphs and launch every kernel shape run(iters) uses, without advancing the state")
+      .def(
+          "warm", [](SolverHandle& h, int n, int passes) { h.visit([n, passes](auto& s) { s.warm(n, passes); }); },
+          py::arg("iters"), py::arg("passes"), py::call_guard<py::gil_scoped_release>(),
+          "untimed state-preserving passes of run(iters)'s shapes (sustained clocks before a short window)")
       .def("exchange_only", [](SolverHandle& h) { h.visit([](auto& s) { s.exchange_only(); }); })
       .def("synchronize", [](SolverHandle& h) { h.visit([](auto& s) { s.synchronize(); }); },
            py::call_guard<py::gil_scoped_release>())

@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -28,7 +29,13 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   // Fixed boundary values on a physical edge must not be advanced as cells:
   // time blocking is only exact when every edge is a neighbour's (see header).
   if (!(topo.periodic_rows && topo.periodic_cols)) block_ = 1;
-  MXS_CHECK(block_ <= kernels::kMaxTimeBlock, "time_block must be <= " << kernels::kMaxTimeBlock);
+  // Blocks past kMaxTimeBlock run on the fp32 two-stage pipeline, which takes
+  // whole-vector column ranges only: not the overlap schedule's thin strips,
+  // not fp64, not a ragged width. Elsewhere the block is capped at 16.
+  if (block_ > kernels::kMaxTimeBlock &&
+      !(std::is_same_v<T, float> && !cfg_.overlap && tile_.width % 4 == 0))
+    block_ = kernels::kMaxTimeBlock;
+  MXS_CHECK(block_ <= kernels::kMaxTimeBlockDeep, "time_block must be <= " << kernels::kMaxTimeBlockDeep);
   MXS_CHECK(block_ <= tile_.width && block_ <= tile_.height,
             "time_block " << block_ << " exceeds the tile (" << tile_.width << "x" << tile_.height
                           << "): its ghost ring would reach past the neighbouring tiles");
@@ -253,6 +260,18 @@ void StencilSolver<T>::prepare(int iters) {
     enqueue_block(cur_, nxt_, g.S);
     warmed_.push_back(g.S);
   }
+  main_.sync();
+  side_.sync();
+}
+
+template <typename T>
+void StencilSolver<T>::warm(int iters, int passes) {
+  MXS_TRACE_RANGE("stencil.warm");
+  Group gr[2];
+  split(iters, gr);
+  for (int p = 0; p < passes; ++p)
+    for (const Group& g : gr)
+      if (g.count > 0) enqueue_block(cur_, nxt_, g.S);  // cur -> nxt, no swap: state unchanged
   main_.sync();
   side_.sync();
 }

@@ -57,9 +57,10 @@ class StencilConfig:
     variant: str = "auto"            # stencil kernel variant: auto | roll | lds
     fuse_periodic: bool = True       # 1x1 periodic: fuse the self-exchange into the kernel addressing
     # Jacobi iterations per halo exchange and per temporally blocked pass on GPU
-    # (wave-streaming kernel); the ghost ring is made this deep. 1 = one exchange
-    # per iteration; 0 = the measured optimum for the tile (12, or 16 from 2^27
-    # cells: kernels::auto_time_block, docs/PERF.md).
+    # (wave-streaming kernels); the ghost ring is made this deep. 1 = one
+    # exchange per iteration; 0 = the measured optimum for the tile
+    # (kernels::auto_time_block: fp32 24 on the two-stage pipeline, fp64 12/16,
+    # docs/PERF.md). Up to 32 for fp32 without overlap, else capped at 16.
     time_block: int = 0
     seed: int = 1234
     init: str = "random"             # random | rank
@@ -90,7 +91,7 @@ class Stencil2D:
         # A ghost ring deeper than a neighbour's tile would need cells two tiles away.
         tb = cfg.time_block
         if tb <= 0 and dev.type == "cuda":
-            tb = hip().auto_time_block(d.width, d.height)
+            tb = hip().auto_time_block(d.width, d.height, cfg.dtype)
         # A physical (non-periodic) edge holds fixed boundary values that the
         # S-step kernels would advance as cells: time blocking needs every edge
         # to be a neighbour's (the native solver enforces the same rule).
@@ -145,6 +146,9 @@ class Stencil2D:
                                           cfg.dtype, be, overlap, cfg.graph, cfg.loopback, kind, cfg.c_center,
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
                                           self.time_block, boot, cfg.graph_supersteps)
+            # The solver may cap the request (blocks > 16 need the fp32 pipeline's
+            # preconditions); the ghost ring was sized for the request.
+            self.time_block = self.solver.time_block()
         else:
             self.plan = make_plan(d, self.geom, corners=True)
             self.halo = TorchHalo(self.plan, self.ctx)
@@ -182,6 +186,22 @@ class Stencil2D:
         advancing the field. Benchmarks call it before their timed window."""
         if self.solver is not None and iters > 0:
             self.solver.prepare(iters)
+
+    def warm(self, iters: int, seconds: float) -> int:
+        """Collective: about ``seconds`` of untimed, state-preserving passes of
+        ``run(iters)``'s kernel shapes, so a short timed window that follows runs
+        at the device's sustained clocks instead of paying the DVFS ramp (a cold
+        20-step window at 32768^2 is ~20% slower than a warm one). The pass count
+        is agreed across ranks (max of the per-rank estimates). Returns it."""
+        if self.solver is None or iters <= 0 or seconds <= 0:
+            return 0
+        self.solver.synchronize()
+        t0 = time.perf_counter()
+        self.solver.warm(iters, 1)
+        one = max(time.perf_counter() - t0, 1e-5)
+        passes = int(self.ctx.allreduce_max(min(1000.0, math.ceil(seconds / one))))
+        self.solver.warm(iters, passes)
+        return passes + 1
 
     def _python_step(self):
         cfg, g = self.cfg, self.geom

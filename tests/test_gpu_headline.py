@@ -45,7 +45,12 @@ def _frozen_edge_reference(full, steps, c0=0.2, c1=0.2):
 
 
 @pytest.mark.parametrize("w,h,steps,dtype,kernel", [
-    (8192, 8192, 12, torch.float32, "stream_balanced_rot"),   # BASELINE config 2 (1 GPU), auto S
+    (8192, 8192, 24, torch.float32, "stream_pipe"),           # BASELINE config 2 (1 GPU), auto S: two-stage pipeline
+    (8192, 8192, 20, torch.float32, "stream_pipe"),           # the driver's 20-step window in one pass
+    (4096, 2048, 17, torch.float32, "stream_pipe"),           # odd split 8 + 9
+    (2048, 1024, 32, torch.float32, "stream_pipe"),           # deepest block, PF = 3
+    (300, 200, 24, torch.float32, "stream_pipe"),             # narrower than one strip group: modulo wrap
+    (8192, 8192, 12, torch.float32, "stream_balanced_rot"),
     (4096, 8192, 16, torch.float32, "stream_balanced_rot"),
     (16384, 4096, 16, torch.float32, "stream_balanced_rot"),  # wide tile, deepest block
     (4096, 4096, 12, torch.float64, "stream_balanced"),       # fp64 balanced path
@@ -71,6 +76,9 @@ def test_balanced_wrap_matches_periodic_reference(gpu, w, h, steps, dtype, kerne
     # The 8-GPU tile of the 32768^2 problem (4 rows x 2 cols -> 16384 x 8192),
     # halved in both directions to keep the test quick: non-wrap, 16-deep ring.
     (8192, 4096, 16, None, torch.float32, "stream_balanced_rot"),
+    # Same tile at the fp32 default block (24-deep ring): two-stage pipeline.
+    (8192, 4096, 24, None, torch.float32, "stream_pipe"),
+    (4096, 2048, 20, (8, 4088, 20, 2040), torch.float32, "stream_pipe"),
     # Ragged right edge (x_end % 4 != 0): the non-rotated balanced form.
     (8190, 4096, 16, None, torch.float32, "stream_balanced"),
     # Interior rectangle of the overlap schedule (vector-aligned columns).
@@ -99,13 +107,32 @@ def test_balanced_ghost_ring_matches_reference(gpu, w, h, steps, rect, dtype, ke
     assert bool((got[mask] == -3.0).all()), "the kernel wrote outside its rectangle"
 
 
-@pytest.mark.parametrize("dtype", ["f32", "f64"])
-def test_solver_blocked_run_bitwise_equals_single_steps(gpu, dtype):
-    """run(20) at the auto time block (8192^2: S = 12 -> two super-steps of 10)
-    equals 20 one-step iterations bit for bit, and prepare() changes nothing."""
+def test_deep_blocks_reject_what_the_pipeline_cannot_run(gpu):
+    """Blocks > 16 exist only for fp32 whole-vector column ranges: anything else
+    fails loudly instead of silently running a different schedule."""
+    for dtype, x1 in ((torch.float64, 512), (torch.float32, 510)):
+        g = core().TileGeom.aligned(512, 256, 20, 20, torch.tensor([], dtype=dtype).element_size())
+        buf = torch.zeros(g.alloc_elems(), dtype=dtype, device=gpu)
+        with pytest.raises(Exception, match="whole vectors"):
+            hip().stencil5_tb(buf.data_ptr(), buf.data_ptr(), g, 20, 0, x1, 0, 256, 0.2, 0.2, False,
+                              dtype_name(buf), torch.cuda.current_stream().cuda_stream, "auto")
+
+
+def test_solver_caps_deep_blocks_where_the_pipeline_cannot_run(gpu):
+    kw = dict(global_width=1024, global_height=512, dims="1x1", seed=2, time_block=24)
+    assert Stencil2D(StencilConfig(dtype="f32", **kw)).time_block == 24
+    assert Stencil2D(StencilConfig(dtype="f64", **kw)).time_block == 16
+    assert Stencil2D(StencilConfig(dtype="f32", overlap=True, backend="rccl", loopback=True, **kw)).time_block == 16
+
+
+@pytest.mark.parametrize("dtype,block", [("f32", 24), ("f64", 12)])
+def test_solver_blocked_run_bitwise_equals_single_steps(gpu, dtype, block):
+    """run(20) at the auto time block (8192^2: fp32 S = 24 -> one 20-step
+    pipeline pass; fp64 S = 12 -> two super-steps of 10) equals 20 one-step
+    iterations bit for bit, and prepare() changes nothing."""
     kw = dict(global_width=8192, global_height=8192, dims="1x1", dtype=dtype, seed=99)
     blocked = Stencil2D(StencilConfig(**kw))
-    assert blocked.time_block == 12
+    assert blocked.time_block == block
     blocked.prepare(20)
     blocked.prepare(20)  # idempotent
     blocked.run(20)
@@ -118,8 +145,9 @@ def test_solver_blocked_run_bitwise_equals_single_steps(gpu, dtype):
 
 
 def test_solver_odd_splits_bitwise(gpu):
-    """Near-equal splits of awkward counts (17 = 9 + 8, 33 = 11 + 11 + 11 at S = 12)
-    and a graph reused across calls stay exact."""
+    """Near-equal splits of awkward counts at the fp32 default S = 24 (17 in one
+    pipeline pass, 33 = 17 + 16: pipeline + single-wave kernel, then 1 and 12)
+    and graphs reused across calls stay exact."""
     kw = dict(global_width=2048, global_height=1024, dims="1x1", dtype="f32", seed=5)
     a = Stencil2D(StencilConfig(**kw))
     for n in (17, 33, 1, 12):
@@ -149,7 +177,8 @@ def test_non_periodic_runs_single_step_and_keeps_boundary(gpu):
 
 def test_headline_rate_floor(gpu):
     """Regression floor near the measured rate: 32768^2 fp32, a 20-step window
-    after prepare() (the driver's --steps 20 --warmup 5). Measured ~7 T cells/s."""
+    after prepare() (the driver's --steps 20 --warmup 5): one 20-step pipeline
+    pass. Tuner: 7.9 T cells/s."""
     st = Stencil2D(StencilConfig(global_width=32768, global_height=32768, dims="1x1", dtype="f32"))
     st.run(5)
     st.prepare(20)
@@ -158,5 +187,24 @@ def test_headline_rate_floor(gpu):
     st.run(20)
     st.synchronize()
     rate = st.cells_per_step * 20 / (time.perf_counter() - t0) / 1e9
-    assert hip().last_stencil_dispatch() == "stream_balanced_rot"
-    assert rate > 5000, f"{rate:.0f} Gcells/s"
+    assert hip().last_stencil_dispatch() == "stream_pipe"
+    assert rate > 6000, f"{rate:.0f} Gcells/s"
+
+
+@pytest.mark.parametrize("backend,loopback", [("local", False), ("rccl", True)])
+def test_warm_and_prepare_leave_the_state_alone(gpu, backend, loopback):
+    """bench.py's untimed clock warm-up and prepare() launch real passes
+    (exchange included on the RCCL path) but must not advance the field."""
+    kw = dict(global_width=1024, global_height=768, dims="1x1", dtype="f32", seed=17, backend=backend,
+              loopback=loopback)
+    a = Stencil2D(StencilConfig(**kw))
+    a.run(5)
+    a.prepare(20)
+    assert a.warm(20, 0.01) >= 2
+    a.run(20)
+    a.synchronize()
+    b = Stencil2D(StencilConfig(**kw))
+    b.run(5)
+    b.run(20)
+    b.synchronize()
+    assert torch.equal(a.core_view(), b.core_view())
