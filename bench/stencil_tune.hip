@@ -191,21 +191,22 @@ Variant balanced(const float* in, float* out, const TileGeom& g, int per_cu, flo
 }
 
 // Two-stage wave pipeline (S = S0 + S1 levels; 512-thread workgroups).
-template <int S0, int S1, int PF, bool WRAP = true>
+template <int S0, int S1, int PF, bool WRAP = true, int PRIO = 0>
 Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullptr) {
   int per_cu = 0, cus = 0;
   MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu, reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP>), 512, 0));
+      &per_cu, reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO>), 512, 0));
   MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const int blocks = std::max(1, per_cu * cus);
   char buf[128];
-  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "");
+  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
+                PRIO == 1 ? "_prio0" : (PRIO == 2 ? "_prio1" : ""));
   auto mk = [=](const float* I, float* O) {
     return [=](hipStream_t s) {
       constexpr int OW = StreamShape<float, S0 + S1>::OW;
       const index_t groups = ((g.width + OW - 1) / OW + 3) / 4;
       const index_t share = (groups * g.height + blocks - 1) / blocks;
-      stencil5_stream_pipe_kernel<S0, S1, PF, WRAP><<<blocks, 512, 0, s>>>(
+      stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO><<<blocks, 512, 0, s>>>(
           I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, 0.2f, 0.2f);
     };
   };
@@ -220,7 +221,7 @@ int main(int argc, char** argv) {
   const index_t W = argc > 1 ? atol(argv[1]) : 32768;
   const index_t H = argc > 2 ? atol(argv[2]) : 32768;
   const int rounds = argc > 3 ? atoi(argv[3]) : 5;
-  const TileGeom g = TileGeom::aligned(W, H, 16, 16, 4);  // 16-deep ghost ring: non-wrap variants up to S = 16
+  const TileGeom g = TileGeom::aligned(W, H, 32, 32, 4);  // 32-deep ghost ring: non-wrap variants up to S = 32
   DeviceBuffer<float> a(g.alloc_elems()), b(g.alloc_elems()), c(g.alloc_elems());
   // Random data: zero-filled operands raise the clock under load and inflate
   // the numbers (cdna_hip_programming.md §5.4 rule 25).
@@ -315,6 +316,34 @@ int main(int argc, char** argv) {
     vs.push_back(pipe<12, 12, 3>(in, out, g, tmp));
     vs.push_back(pipe<12, 12, 6>(in, out, g, tmp));
     vs.push_back(pipe<16, 16, 3>(in, out, g, tmp));
+  } else if (focus && std::string(focus) == "pipe2") {  // pipeline splits, depth, priority; wrap and ghost-ring forms
+    vs.push_back(balanced<16, 3, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<16, 3, false, true>(in, out, g, 0));
+    vs.push_back(pipe<12, 12, 6>(in, out, g, tmp));
+    vs.push_back(pipe<11, 13, 6>(in, out, g, tmp));
+    vs.push_back(pipe<13, 11, 6>(in, out, g, tmp));
+    vs.push_back(pipe<10, 14, 6>(in, out, g, tmp));
+    vs.push_back(pipe<13, 13, 6>(in, out, g, tmp));
+    vs.push_back(pipe<14, 14, 6>(in, out, g, tmp));
+    vs.push_back(pipe<12, 12, 6, true, 1>(in, out, g, tmp));
+    vs.push_back(pipe<12, 12, 6, true, 2>(in, out, g, tmp));
+    vs.push_back(pipe<12, 12, 6, false>(in, out, g));
+    vs.push_back(pipe<14, 14, 6, false>(in, out, g));
+    vs.push_back(pipe<10, 10, 6>(in, out, g, tmp));
+    vs.push_back(pipe<9, 11, 6>(in, out, g, tmp));
+  } else if (focus && std::string(focus) == "pipe20") {  // S = 20 forms
+    vs.push_back(balanced<16, 3, true, true>(in, out, g, 0, tmp));
+    vs.push_back(balanced<16, 3, false, true>(in, out, g, 0));
+    vs.push_back(pipe<10, 10, 6>(in, out, g, tmp));
+    vs.push_back(pipe<10, 10, 6, true, 1>(in, out, g, tmp));
+    vs.push_back(pipe<10, 10, 6, true, 2>(in, out, g, tmp));
+    vs.push_back(pipe<10, 10, 3>(in, out, g, tmp));
+    vs.push_back(pipe<11, 9, 6>(in, out, g, tmp));
+    vs.push_back(pipe<10, 10, 6, false>(in, out, g));
+    vs.push_back(pipe<10, 10, 6, false, 1>(in, out, g));
+    vs.push_back(pipe<10, 10, 6, false, 2>(in, out, g));
+    vs.push_back(pipe<9, 9, 6>(in, out, g, tmp));
+    vs.push_back(pipe<11, 11, 6>(in, out, g, tmp));
   } else if (focus && std::string(focus) == "deep") {  // time blocks past 16 (AGPR-backed window, 1 wave/SIMD)
     vs.push_back(balanced<16, 3, true, true>(in, out, g, 0, tmp));
     vs.push_back(balanced<10, 6, true, true>(in, out, g, 0, tmp));

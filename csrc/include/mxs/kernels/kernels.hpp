@@ -80,13 +80,15 @@ constexpr int kMaxTimeBlock = 16;
 // of 4 (whole vectors); see stencil5_deep_supported().
 constexpr int kMaxTimeBlockDeep = 32;
 // Measured default S for a w x h tile of `elem_bytes`-byte cells
-// (profiles/stencil_tuning/tunes_*, profiles/r02_deep/pipe_*): fp32 takes the
-// two-stage pipeline at S = 24 (32768^2: 8.0 vs 7.85 T cells/s at S = 16;
-// 8192^2: 6.3 vs 5.7); fp64 and the single-wave kernels: S = 16 from 2^27
-// cells, S = 12 below (the pass is VALU-bound beyond S ~ 8, so a deeper block
-// only pays where the chunk / strip aprons are small against the tile).
+// (profiles/stencil_tuning/tunes_*, profiles/r02_deep/pipe*_*): fp32 takes the
+// two-stage pipeline at S = 20, level split 11 + 9 (32768^2: 8.0-8.2 T
+// cells/s vs 7.85-7.9 single-wave at S = 16; 8192^2: 6.4-6.6 vs 5.9; ghost-ring
+// (multi-GPU) tiles 16384 x 8192 .. 32768 x 16384: +0-8%; S = 24 measured no
+// better and costs a 4% wider apron); fp64 and the single-wave kernels: S = 16
+// from 2^27 cells, S = 12 below (the pass is VALU-bound beyond S ~ 8, so a
+// deeper block only pays where the chunk / strip aprons are small against the tile).
 inline int auto_time_block(index_t w, index_t h, int elem_bytes = 4) {
-  if (elem_bytes == 4 && w >= 1024 && h >= 1024) return 24;
+  if (elem_bytes == 4 && w >= 1024 && h >= 1024) return 20;
   return w * h >= (index_t(1) << 27) ? 16 : 12;
 }
 // Whether a `steps`-step stencil5_tb launch over [x0, x1) can run: every

@@ -16,6 +16,7 @@
 
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
+#include "mxs/runtime/hip_utils.hpp"
 
 namespace mxs {
 namespace kernels {
@@ -86,10 +87,15 @@ void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_
   index_t biggest = 0;
   for (int i = 0; i < b.n; ++i) biggest = std::max(biggest, b.op[i].width * b.op[i].height);
   if (biggest == 0) return;
-  // Enough workgroups for the largest segment, at most 64 per segment: halo
-  // segments are O(perimeter) and latency-bound, more workgroups only add launch cost.
-  const index_t want = (biggest + kBlock - 1) / kBlock;
-  const int gx = int(std::min<index_t>(want, 64));
+  // One 16-byte vector per thread for the largest segment, capped so the whole
+  // batch stays around 4 waves per SIMD (1024 x 256 threads over all segments):
+  // the S-deep halos of the temporally blocked solver are MiB-sized (20 rows of
+  // a 16384-wide tile = 1.3 MB per segment), and the earlier cap of 64
+  // workgroups per segment moved them at ~0.4 TB/s (7 us per pack of the 8-GPU tile).
+  constexpr index_t kVec = 16 / sizeof(T) > 0 ? 16 / sizeof(T) : 1;
+  const index_t want = (biggest + kBlock * kVec - 1) / (kBlock * kVec);
+  const index_t cap = std::max<index_t>(64, index_t(4) * device_cu_count() / b.n);
+  const int gx = int(std::min<index_t>(want, cap));
   copy2d_batch_kernel<T><<<dim3(gx, b.n), kBlock, 0, s>>>(slot0, slot1, slot2, b);
   MXS_HIP_CHECK_LAUNCH();
 }

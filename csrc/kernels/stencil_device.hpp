@@ -1136,7 +1136,8 @@ __device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* 
 // (4 strips x 2 stages), equal shares of (4-strip group) x rows as in
 // stencil5_stream_balanced_kernel. fp32 only (rotated-pair layout); needs
 // x_end % 4 == 0 and a chunk under 2 GiB (the output buffer descriptor).
-template <int S0, int S1, int PF, bool WRAP>
+// PRIO (tuning): 1 raises the fetching stage's wave priority, 2 the storing stage's.
+template <int S0, int S1, int PF, bool WRAP, int PRIO = 0>
 __global__ __launch_bounds__(2 * kBlock) void stencil5_stream_pipe_kernel(
     const float* __restrict__ in, float* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, float c0, float c1) {
@@ -1149,6 +1150,11 @@ __global__ __launch_bounds__(2 * kBlock) void stencil5_stream_pipe_kernel(
   const index_t total = groups * rows;
   const int wave = threadIdx.x / kWaveSize;
   const int strip = wave % kWavesPerBlock, stage = wave / kWavesPerBlock;
+  if constexpr (PRIO == 1) {
+    if (stage == 0) __builtin_amdgcn_s_setprio(1);
+  } else if constexpr (PRIO == 2) {
+    if (stage == 1) __builtin_amdgcn_s_setprio(1);
+  }
   index_t a = index_t(blockIdx.x) * share;
   const index_t b = a + share < total ? a + share : total;
 #pragma unroll 1

@@ -59,7 +59,7 @@ class StencilConfig:
     # Jacobi iterations per halo exchange and per temporally blocked pass on GPU
     # (wave-streaming kernels); the ghost ring is made this deep. 1 = one
     # exchange per iteration; 0 = the measured optimum for the tile
-    # (kernels::auto_time_block: fp32 24 on the two-stage pipeline, fp64 12/16,
+    # (kernels::auto_time_block: fp32 20 on the two-stage pipeline, fp64 12/16,
     # docs/PERF.md). Up to 32 for fp32 without overlap, else capped at 16.
     time_block: int = 0
     seed: int = 1234

@@ -125,9 +125,9 @@ def test_solver_caps_deep_blocks_where_the_pipeline_cannot_run(gpu):
     assert Stencil2D(StencilConfig(dtype="f32", overlap=True, backend="rccl", loopback=True, **kw)).time_block == 16
 
 
-@pytest.mark.parametrize("dtype,block", [("f32", 24), ("f64", 12)])
+@pytest.mark.parametrize("dtype,block", [("f32", 20), ("f64", 12)])
 def test_solver_blocked_run_bitwise_equals_single_steps(gpu, dtype, block):
-    """run(20) at the auto time block (8192^2: fp32 S = 24 -> one 20-step
+    """run(20) at the auto time block (8192^2: fp32 S = 20 -> one 20-step
     pipeline pass; fp64 S = 12 -> two super-steps of 10) equals 20 one-step
     iterations bit for bit, and prepare() changes nothing."""
     kw = dict(global_width=8192, global_height=8192, dims="1x1", dtype=dtype, seed=99)
@@ -145,7 +145,7 @@ def test_solver_blocked_run_bitwise_equals_single_steps(gpu, dtype, block):
 
 
 def test_solver_odd_splits_bitwise(gpu):
-    """Near-equal splits of awkward counts at the fp32 default S = 24 (17 in one
+    """Near-equal splits of awkward counts at the fp32 default S = 20 (17 in one
     pipeline pass, 33 = 17 + 16: pipeline + single-wave kernel, then 1 and 12)
     and graphs reused across calls stay exact."""
     kw = dict(global_width=2048, global_height=1024, dims="1x1", dtype="f32", seed=5)
