@@ -80,15 +80,19 @@ constexpr int kMaxTimeBlock = 16;
 // of 4 (whole vectors); see stencil5_deep_supported().
 constexpr int kMaxTimeBlockDeep = 32;
 // Measured default S for a w x h tile of `elem_bytes`-byte cells
-// (profiles/stencil_tuning/tunes_*, profiles/r02_deep/pipe*_*): fp32 takes the
-// two-stage pipeline at S = 20, level split 11 + 9 (32768^2: 8.0-8.2 T
-// cells/s vs 7.85-7.9 single-wave at S = 16; 8192^2: 6.4-6.6 vs 5.9; ghost-ring
-// (multi-GPU) tiles 16384 x 8192 .. 32768 x 16384: +0-8%; S = 24 measured no
-// better and costs a 4% wider apron); fp64 and the single-wave kernels: S = 16
-// from 2^27 cells, S = 12 below (the pass is VALU-bound beyond S ~ 8, so a
-// deeper block only pays where the chunk / strip aprons are small against the tile).
+// (profiles/stencil_tuning/tunes_*, profiles/r02_deep/pipe*_*, profiles/r02_f64):
+// fp32 takes the two-stage pipeline at S = 20, level split 11 + 9 (32768^2:
+// 8.0-8.2 T cells/s vs 7.85-7.9 single-wave at S = 16; 8192^2: 6.4-6.6 vs 5.9;
+// ghost-ring (multi-GPU) tiles 16384 x 8192 .. 32768 x 16384: +0-8%; S = 24
+// measured no better and costs a 4% wider apron); fp64 takes the wide-lane
+// two-stage pipeline at S = 12 (6 + 6: 3.0-3.35 T cells/s vs 2.2-2.5 for the
+// natural single-wave kernel at S = 12 and 1.7-1.9 at S = 16); the fp32
+// single-wave kernels (small tiles): S = 16 from 2^27 cells, S = 12 below (the
+// pass is VALU-bound beyond S ~ 8, so a deeper block only pays where the chunk
+// / strip aprons are small against the tile).
 inline int auto_time_block(index_t w, index_t h, int elem_bytes = 4) {
   if (elem_bytes == 4 && w >= 1024 && h >= 1024) return 20;
+  if (elem_bytes == 8) return 12;
   return w * h >= (index_t(1) << 27) ? 16 : 12;
 }
 // Whether a `steps`-step stencil5_tb launch over [x0, x1) can run: every
@@ -108,8 +112,8 @@ void stencil5_rect(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
                    index_t y1, Stencil5Coeffs c, hipStream_t s);
 
 // Kernel form chosen by the most recent stencil launcher on this host process:
-// "stream_pipe" (the two-stage fp32 pipeline of blocks > 16 steps, the one the
-// benchmarks time), "stream_balanced_rot" (persistent single-wave fp32
+// "stream_pipe" (the two-stage pipeline: fp32 blocks > 16 steps, the one the
+// benchmarks time, and fp64 blocks of 12 / 16 on whole lane vectors), "stream_balanced_rot" (persistent single-wave fp32
 // rotated-pair kernel), "stream_balanced", "stream_grid_rot", "stream_grid", "tb_tile",
 // "roll", "roll_wrap", "lds", "rect" or "box". A record of the host-side
 // dispatch decision, for tests and result records; graph replays do not update it.

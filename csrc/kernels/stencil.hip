@@ -220,6 +220,75 @@ void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
   }
 }
 
+// Two-stage pipeline. fp32 (S = 17..32): the fetching stage takes one level
+// more than half, S0 = S/2 + 1 (at most 16), S1 = S - S0 — measured 2-3% ahead
+// of the even split on 4 of 5 tile shapes (profiles/r02_deep/pipe2_*,
+// pipe20_*); 6 input rows in flight up to S = 28 (the fetch ring fits beside
+// the windows at 2 waves/SIMD), 3 above. fp64 (S = 12 and 16, wide-lane body):
+// even split, 3 rows in flight — 6 + 6 is the fastest fp64 form on every
+// measured tile (8192^2 3.0 vs 2.2 T cells/s for the single-wave natural
+// kernel, 16384^2 3.35 vs 2.5; 8 + 8 2.8-3.1; odd depths lose to the apron
+// rounding: profiles/r02_f64). One 512-thread workgroup per CU: the occupancy
+// API decides, as for the single-wave balanced kernel.
+template <typename T, int S>
+constexpr int pipe_s0() {
+  if constexpr (sizeof(T) == 8) return S / 2;
+  return S / 2 + 1 < 16 ? S / 2 + 1 : 16;
+}
+template <typename T, int S>
+constexpr int pipe_pf() {
+  return (sizeof(T) == 4 && S <= 28) ? 6 : 3;
+}
+template <typename T, int S, bool WRAP>
+constexpr auto pipe_kernel() {
+  return stencil5_stream_pipe_kernel<pipe_s0<T, S>(), S - pipe_s0<T, S>(), pipe_pf<T, S>(), WRAP, 0, T>;
+}
+
+template <typename T, int S, bool WRAP>
+int pipe_blocks() {
+  static int blocks = 0;
+  if (blocks == 0) {
+    int occ = 0;
+    MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, reinterpret_cast<const void*>(pipe_kernel<T, S, WRAP>()), 2 * kBlock, 0));
+    blocks = std::max(occ, 1) * device_cu_count();
+  }
+  return blocks;
+}
+
+template <typename T, int S, bool WRAP>
+index_t pipe_share(index_t x0, index_t x1, index_t y0, index_t y1) {
+  constexpr int OW = StripShape<T, S, true>::OW;
+  const index_t groups = ((x1 - x0 + OW - 1) / OW + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int blocks = pipe_blocks<T, S, WRAP>();
+  return (groups * (y1 - y0) + blocks - 1) / blocks;
+}
+
+template <typename T, int S, bool WRAP>
+void launch_pipe(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
+                 hipStream_t s) {
+  const index_t share = pipe_share<T, S, WRAP>(x0, x1, y0, y1);
+  MXS_CHECK(std::min(share, y1 - y0) * g.pitch * index_t(sizeof(T)) < (index_t(1) << 31),
+            "stencil5_tb: a pipeline chunk must stay under 2 GiB (buffer-descriptor stores)");
+  pipe_kernel<T, S, WRAP>()<<<pipe_blocks<T, S, WRAP>(), 2 * kBlock, 0, s>>>(
+      in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
+  note("stream_pipe");
+}
+
+// Whether the fp64 wide-lane pipeline can take [x0, x1) x [y0, y1) at depth S:
+// whole 4-cell lane vectors (x0, x1 and, wrapping, the width multiples of 4),
+// the apron inside the row padding, and a chunk under 2 GiB.
+template <typename T, int S, bool WRAP>
+bool wide_pipe_ok(const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1) {
+  constexpr int SA = StripShape<T, S, true>::SA;
+  if (x0 % 4 != 0 || x1 % 4 != 0) return false;
+  if (WRAP && g.width % 4 != 0) return false;
+  const index_t lead = g.x_origin + g.halo_x;
+  if (!WRAP && (lead < SA || g.pitch < lead + (g.width + 3) / 4 * 4 + SA)) return false;
+  return std::min(pipe_share<T, S, WRAP>(x0, x1, y0, y1), y1 - y0) * g.pitch * index_t(sizeof(T)) <
+         (index_t(1) << 31);
+}
+
 // Dispatch by shape. Bulk rectangles take the wave-streaming kernel (Auto) or
 // the LDS tile (LdsTile, S <= 8): 128 fp32 columns (64 fp64: same bytes) x 32
 // rows per 256-thread workgroup, single LDS buffer. The overlap schedule's
@@ -240,51 +309,11 @@ void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, i
     if (v == StencilVariant::LdsTile)
       return launch_tb_tile<T, S, TW, 32, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
   }
-  launch_stream<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
-}
-
-// Two-stage pipeline (S = 17..32, fp32): the fetching stage takes one level
-// more than half, S0 = S/2 + 1 (at most 16), S1 = S - S0 — measured 2-3% ahead
-// of the even split on 4 of 5 tile shapes (profiles/r02_deep/pipe2_*,
-// pipe20_*); 6 input rows in flight up to S = 28 (the fetch ring fits beside
-// the windows at 2 waves/SIMD), 3 above. One 512-thread workgroup per CU: the
-// occupancy API decides, as for the single-wave balanced kernel.
-template <int S>
-constexpr int pipe_s0() {
-  return S / 2 + 1 < 16 ? S / 2 + 1 : 16;
-}
-template <int S>
-constexpr int pipe_pf() {
-  return S <= 28 ? 6 : 3;
-}
-
-template <int S, bool WRAP>
-int pipe_blocks() {
-  static int blocks = 0;
-  if (blocks == 0) {
-    int occ = 0;
-    MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<pipe_s0<S>(), S - pipe_s0<S>(), pipe_pf<S>(), WRAP>),
-        2 * kBlock, 0));
-    blocks = std::max(occ, 1) * device_cu_count();
+  if constexpr (sizeof(T) == 8 && (S == 12 || S == 16)) {
+    if (wide_pipe_ok<T, S, WRAP>(g, x0, x1, y0, y1))
+      return launch_pipe<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
   }
-  return blocks;
-}
-
-template <int S, bool WRAP>
-void launch_pipe(const float* in, float* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
-                 float c0, float c1, hipStream_t s) {
-  constexpr int OW = StreamShape<float, S>::OW;
-  const index_t strips = (x1 - x0 + OW - 1) / OW;
-  const index_t rows = y1 - y0;
-  const index_t groups = (strips + kWavesPerBlock - 1) / kWavesPerBlock;
-  const int blocks = pipe_blocks<S, WRAP>();
-  const index_t share = (groups * rows + blocks - 1) / blocks;
-  MXS_CHECK(std::min(share, rows) * g.pitch * index_t(sizeof(float)) < (index_t(1) << 31),
-            "stencil5_tb: a pipeline chunk must stay under 2 GiB (buffer-descriptor stores)");
-  stencil5_stream_pipe_kernel<pipe_s0<S>(), S - pipe_s0<S>(), pipe_pf<S>(), WRAP><<<blocks, 2 * kBlock, 0, s>>>(
-      in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
-  note("stream_pipe");
+  launch_stream<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
 }
 
 template <typename T, bool WRAP, int S = 1>
@@ -294,7 +323,7 @@ void dispatch_tb(int steps, const T* in, T* out, const TileGeom& g, index_t x0, 
     if (steps == S) return launch_tb<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, v, s);
     return dispatch_tb<T, WRAP, S + 1>(steps, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   } else if constexpr (S <= kMaxTimeBlockDeep && sizeof(T) == 4) {
-    if (steps == S) return launch_pipe<S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
+    if (steps == S) return launch_pipe<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
     return dispatch_tb<T, WRAP, S + 1>(steps, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   } else {
     MXS_CHECK(false, "stencil5_tb: steps must be in [1, " << (sizeof(T) == 4 ? kMaxTimeBlockDeep : kMaxTimeBlock)

@@ -645,6 +645,87 @@ struct StreamShape {
   static constexpr int OW = kWaveSize * N - 2 * SA;     // output columns per wave
 };
 
+// ------------------------------------------------ wide-lane fp64 layout
+// fp64 has no packed VALU and 64-bit DPP cannot take the wave shifts, so the
+// natural fp64 form (one 16-byte vector = 2 cells per lane, 128-column strips)
+// pays 2 neighbour moves (4 v_mov_b32_dpp) per 2 cells and an apron of 2S of
+// 128 columns. Four cells per lane (two 16-byte loads, 256-column strips as
+// fp32) halve both: 20 fp64 ops + 4 dword moves per 4 cells, apron 2S of 256.
+// Same per-cell operations and order as jac(): bitwise identical.
+using f64x2 = double __attribute__((ext_vector_type(2)));
+using f64x4 = double __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f64x4 jac_w4d(const f64x4& up, const f64x4& mid, const f64x4& dn, double c0, double c1) {
+  const double left = lane_shift<double, kDppWaveShr1>(mid.w);   // lane - 1's last cell
+  const double right = lane_shift<double, kDppWaveShl1>(mid.x);  // lane + 1's first cell
+  f64x4 o;
+  o.x = jac<double>(mid.x, up.x, dn.x, left, mid.y, c0, c1);
+  o.y = jac<double>(mid.y, up.y, dn.y, mid.x, mid.z, c0, c1);
+  o.z = jac<double>(mid.z, up.z, dn.z, mid.y, mid.w, c0, c1);
+  o.w = jac<double>(mid.w, up.w, dn.w, mid.z, right, c0, c1);
+  return o;
+}
+
+// Per-lane bodies of the branch-free streaming kernels (stream_chunk_fast,
+// pipe_chunk): 4 cells per lane in both, so a strip is 256 columns and the
+// apron S rounded up to 4. `enter` maps a row loaded from HBM into the
+// register layout the levels work on; `store` maps it back and writes one
+// lane's 4 cells through the chunk's buffer descriptor (an offset past the
+// range is dropped by the hardware range check: no branch, no exec mask).
+using u32x4 = unsigned __attribute__((ext_vector_type(4)));
+struct BodyRotF32 {  // rotated-pair fp32 (jac_rot4f)
+  using T = float;
+  using V = f32x4;
+  static constexpr int N = 4;
+  static __device__ __forceinline__ V zero() { return f32x4(0.f); }
+  static __device__ __forceinline__ V load(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+  static __device__ __forceinline__ V enter(const V& v) { return rot_in(v); }
+  static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, float c0, float c1) {
+    return jac_rot4f(u, m, d, c0, c1);
+  }
+  static __device__ __forceinline__ void store(const V& top, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    const f32x4 nat = rot_out(top);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, nat), r, int(off), 0, 2 /* nt */);
+  }
+};
+struct BodyWideF64 {  // 4 consecutive fp64 cells per lane (jac_w4d)
+  using T = double;
+  using V = f64x4;
+  static constexpr int N = 4;
+  static __device__ __forceinline__ V zero() { return f64x4(0.0); }
+  static __device__ __forceinline__ V load(const double* p) {
+    const f64x2 a = *reinterpret_cast<const f64x2*>(p), b = *reinterpret_cast<const f64x2*>(p + 2);
+    return __builtin_shufflevector(a, b, 0, 1, 2, 3);
+  }
+  static __device__ __forceinline__ V enter(const V& v) { return v; }
+  static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, double c0, double c1) {
+    return jac_w4d(u, m, d, c0, c1);
+  }
+  static __device__ __forceinline__ void store(const V& top, __amdgpu_buffer_rsrc_t r, unsigned off) {
+    const f64x2 lo = top.xy, hi = top.zw;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), r, int(off), 0, 2 /* nt */);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), r, int(off + 16u), 0, 2 /* nt */);
+  }
+};
+template <typename T>
+struct FastBody;
+template <>
+struct FastBody<float> {
+  using type = BodyRotF32;
+};
+template <>
+struct FastBody<double> {
+  using type = BodyWideF64;
+};
+
+// Strip geometry of the kernels: FAST = the 4-cells-per-lane bodies above,
+// else one 16-byte vector per lane (StreamShape). Identical for fp32.
+template <typename T, int S, bool FAST>
+struct StripShape {
+  static constexpr int N = FAST ? 4 : Vec16<T>::N;
+  static constexpr int SA = ((S + N - 1) / N) * N;
+  static constexpr int OW = kWaveSize * N - 2 * SA;
+};
+
 // One wave streams output rows [ys, ye) of the column strip whose first output
 // column is xw. PF = input rows in flight (a register ring, statically indexed;
 // a multiple of 3, the window's slot period).
@@ -781,12 +862,18 @@ __device__ __forceinline__ void wave_prio_update(WavePrio& wp, index_t done) {
   }
 }
 
-template <int S, int PF, bool WRAP>
-__device__ __forceinline__ void stream_chunk_rot(const float* __restrict__ in, float* __restrict__ out, index_t pitch,
-                                                 index_t core_off, index_t W, index_t H, index_t xw, index_t x_end,
-                                                 index_t ys, index_t ye, float c0, float c1, WavePrio* wp = nullptr) {
+// Generic over the per-lane body B (BodyRotF32: the rotated fp32 layout,
+// BodyWideF64: 4 fp64 cells per lane); stream_chunk_rot is the fp32 form.
+// Non-WRAP reads need x_origin + halo_x >= SA (the launcher checks it).
+template <typename B, int S, int PF, bool WRAP>
+__device__ __forceinline__ void stream_chunk_fast(const typename B::T* __restrict__ in, typename B::T* __restrict__ out,
+                                                  index_t pitch, index_t core_off, index_t W, index_t H, index_t xw,
+                                                  index_t x_end, index_t ys, index_t ye, typename B::T c0,
+                                                  typename B::T c1, WavePrio* wp = nullptr) {
   static_assert(PF % 3 == 0, "the window rotates through 3 slots: PF must be a multiple of 3");
-  using Sh = StreamShape<float, S>;
+  using T = typename B::T;
+  using V = typename B::V;
+  using Sh = StripShape<T, S, true>;
   constexpr int N = Sh::N, SA = Sh::SA, AL = SA / N;
   const int lane = threadIdx.x & (kWaveSize - 1);
   const index_t gx = xw - SA + index_t(lane) * N;
@@ -799,27 +886,27 @@ __device__ __forceinline__ void stream_chunk_rot(const float* __restrict__ in, f
     const index_t last_col = (W + N - 1) / N * N + SA - N;  // last vector of the row padding
     lx = gx < last_col ? gx : last_col;
   }
-  const float* __restrict__ pin = in + core_off + lx;
+  const T* __restrict__ pin = in + core_off + lx;
 
   // Output descriptor: rows [ys, ye) from column xw - SA (wave-uniform base).
   const index_t rows = ye - ys;
-  const float* obase = out + core_off + (xw - SA) + ys * pitch;
+  const T* obase = out + core_off + (xw - SA) + ys * pitch;
   const unsigned long long ob = reinterpret_cast<unsigned long long>(obase);
   const unsigned ob_lo = __builtin_amdgcn_readfirstlane(unsigned(ob)), ob_hi = __builtin_amdgcn_readfirstlane(unsigned(ob >> 32));
-  float* obase_u = reinterpret_cast<float*>((static_cast<unsigned long long>(ob_hi) << 32) | ob_lo);
-  const int nbytes = __builtin_amdgcn_readfirstlane(int(rows * pitch * index_t(sizeof(float))));
+  T* obase_u = reinterpret_cast<T*>((static_cast<unsigned long long>(ob_hi) << 32) | ob_lo);
+  const int nbytes = __builtin_amdgcn_readfirstlane(int(rows * pitch * index_t(sizeof(T))));
   const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(obase_u, 0, nbytes, 0x00020000);
   const bool store_lane = lane >= AL && lane < kWaveSize - AL && gx < x_end;
-  const unsigned lane_off = unsigned(lane) * unsigned(N * sizeof(float));
-  const unsigned row_bytes = unsigned(pitch) * unsigned(sizeof(float));
+  const unsigned lane_off = unsigned(lane) * unsigned(N * sizeof(T));
+  const unsigned row_bytes = unsigned(pitch) * unsigned(sizeof(T));
   constexpr unsigned kDrop = 0x80000000u;  // >= nbytes: dropped by the range check
 
   const index_t y_first = ys - S;
   const index_t last_row = ye + S - 1;
   index_t next = y_first;
   if constexpr (WRAP) next = next < 0 ? next + H : next;
-  auto fetch = [&]() -> f32x4 {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(pin + next * pitch);
+  auto fetch = [&]() -> V {
+    const V v = B::load(pin + next * pitch);
     if constexpr (WRAP) {
       ++next;
       next = next == H ? 0 : next;
@@ -829,14 +916,14 @@ __device__ __forceinline__ void stream_chunk_rot(const float* __restrict__ in, f
     return v;
   };
 
-  f32x4 win[3][S];
+  V win[3][S];
 #pragma unroll
   for (int q = 0; q < 3; ++q)
 #pragma unroll
-    for (int l = 0; l < S; ++l) win[q][l] = f32x4(0.f);
+    for (int l = 0; l < S; ++l) win[q][l] = B::zero();
 
   const index_t n_it = rows + 3 * S - 1;
-  f32x4 pf[PF];
+  V pf[PF];
 #pragma unroll
   for (int k = 0; k < PF; ++k) pf[k] = fetch();
   // Warm-up: level l first produces a row any stored cell depends on at
@@ -854,11 +941,11 @@ __device__ __forceinline__ void stream_chunk_rot(const float* __restrict__ in, f
     for (int k = 0; k < PF; ++k) {
       const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
       const int b = (ib + k) / 3;  // wave-uniform
-      win[p2][0] = rot_in(pf[k]);
+      win[p2][0] = B::enter(pf[k]);
       pf[k] = fetch();
 #pragma unroll
       for (int l = S - 2; l >= 0; --l) {
-        if (l <= b) win[p0][l + 1] = jac_rot4f(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+        if (l <= b) win[p0][l + 1] = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
       }
     }
   }
@@ -870,38 +957,45 @@ __device__ __forceinline__ void stream_chunk_rot(const float* __restrict__ in, f
       const index_t j = i + k;
       const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;  // static after the unroll
       if (j >= n_it) break;  // wave-uniform (scalar branch); without it the allocator spills to AGPRs
-      win[p2][0] = rot_in(pf[k]);
+      win[p2][0] = B::enter(pf[k]);
       pf[k] = fetch();
-      f32x4 top;
+      V top;
 #pragma unroll
       for (int l = S - 1; l >= 0; --l) {
-        const f32x4 o = jac_rot4f(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+        const V o = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
         if (l == S - 1) top = o;
         else win[p0][l + 1] = o;
       }
       const index_t r = j - (3 * S - 1);  // output row (relative to ys) of this iteration
       const bool ok = store_lane && r >= 0 && r < rows;
       const unsigned off = ok ? lane_off + unsigned(r) * row_bytes : kDrop;
-      const f32x4 nat = rot_out(top);
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, nat),
-                                             orsrc, int(off), 0, 2 /* nt */);
+      B::store(top, orsrc, off);
     }
   }
 }
 
+template <int S, int PF, bool WRAP>
+__device__ __forceinline__ void stream_chunk_rot(const float* __restrict__ in, float* __restrict__ out, index_t pitch,
+                                                 index_t core_off, index_t W, index_t H, index_t xw, index_t x_end,
+                                                 index_t ys, index_t ye, float c0, float c1, WavePrio* wp = nullptr) {
+  stream_chunk_fast<BodyRotF32, S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, ys, ye, c0, c1, wp);
+}
+
 // Grid form: workgroup = 4 waves on 4 adjacent strips of the same CH-row chunk.
-// ROT: stream_chunk_rot (fp32, DPP; launcher checks its preconditions).
+// ROT: the branch-free 4-cells-per-lane body (stream_chunk_fast: rotated-pair
+// fp32 or wide-lane fp64; the launcher checks its preconditions).
 template <typename T, int S, int PF, bool WRAP, bool DPP = true, bool ROT = false>
 __global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __restrict__ in, T* __restrict__ out,
                                                                  index_t pitch, index_t core_off, index_t W, index_t H,
                                                                  index_t x_begin, index_t x_end, index_t y_begin,
                                                                  index_t y_end, index_t CH, T c0, T c1) {
-  constexpr int OW = StreamShape<T, S>::OW;
+  constexpr int OW = StripShape<T, S, ROT>::OW;
   const index_t xw = x_begin + (index_t(blockIdx.x) * kWavesPerBlock + threadIdx.x / kWaveSize) * OW;
   if (xw >= x_end) return;  // wave-uniform
   const index_t ys = y_begin + index_t(blockIdx.y) * CH;
   const index_t ye = ys + CH < y_end ? ys + CH : y_end;
-  if constexpr (ROT) stream_chunk_rot<S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, ys, ye, c0, c1);
+  if constexpr (ROT)
+    stream_chunk_fast<typename FastBody<T>::type, S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, ys, ye, c0, c1);
   else stream_chunk<T, S, PF, WRAP, DPP>(in, out, pitch, core_off, W, H, xw, x_end, ys, ye, c0, c1);
 }
 
@@ -916,7 +1010,7 @@ template <typename T, int S, int PF, bool WRAP, bool DPP = true, bool ROT = fals
 __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
-  constexpr int OW = StreamShape<T, S>::OW;
+  constexpr int OW = StripShape<T, S, ROT>::OW;
   const index_t rows = y_end - y_begin;
   const index_t strips = (x_end - x_begin + OW - 1) / OW;
   const index_t groups = (strips + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -935,8 +1029,8 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
     if (xw < x_end) {
       wp.done = a - a0;
       if constexpr (ROT)
-        stream_chunk_rot<S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1,
-                                      &wp);
+        stream_chunk_fast<typename FastBody<T>::type, S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end,
+                                                                   y_begin + r0, y_begin + r1, c0, c1, &wp);
       else
         stream_chunk<T, S, PF, WRAP, DPP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0,
                                           c1);
@@ -974,15 +1068,17 @@ struct PipeShape {
   static constexpr int T1 = (3 * S0 + PF - 1 + PF - 1) / PF;  // stage-1 start block: ceil((3*S0 + PF - 1) / PF)
 };
 
-template <int S0, int S1, int PF, bool WRAP>
-__device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* __restrict__ out, index_t pitch,
-                                           index_t core_off, index_t W, index_t H, index_t xw, index_t x_end,
-                                           index_t ys, index_t ye, float c0, float c1, f32x4* __restrict__ ring,
-                                           int stage) {
+template <typename B, int S0, int S1, int PF, bool WRAP>
+__device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in, typename B::T* __restrict__ out,
+                                           index_t pitch, index_t core_off, index_t W, index_t H, index_t xw,
+                                           index_t x_end, index_t ys, index_t ye, typename B::T c0, typename B::T c1,
+                                           typename B::V* __restrict__ ring, int stage) {
   static_assert(PF % 3 == 0, "the window rotates through 3 slots: PF must be a multiple of 3");
   using P = PipeShape<S0, S1, PF>;
   constexpr int S = P::S, RING = P::RING, T1 = P::T1;
-  using Sh = StreamShape<float, S>;
+  using T = typename B::T;
+  using V = typename B::V;
+  using Sh = StripShape<T, S, true>;
   constexpr int N = Sh::N, SA = Sh::SA, AL = SA / N;
   const int lane = threadIdx.x & (kWaveSize - 1);
   const index_t gx = xw - SA + index_t(lane) * N;
@@ -991,7 +1087,7 @@ __device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* 
   const index_t n_it1 = rows + 3 * S1 - 1;           // stage 1: output rows [ys, ye)
   const index_t blocks0 = (n_it0 + PF - 1) / PF, blocks1 = T1 + (n_it1 + PF - 1) / PF;
   const index_t blocks = blocks0 > blocks1 ? blocks0 : blocks1;
-  f32x4* __restrict__ my = ring + lane;
+  V* __restrict__ my = ring + lane;
 
   if (stage == 0) {  // wave-uniform
     index_t lx;
@@ -1004,12 +1100,12 @@ __device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* 
       const index_t last_col = (W + N - 1) / N * N + SA - N;
       lx = gx < last_col ? gx : last_col;
     }
-    const float* __restrict__ pin = in + core_off + lx;
+    const T* __restrict__ pin = in + core_off + lx;
     const index_t last_row = ye + S - 1;
     index_t next = ys - S;
     if constexpr (WRAP) next = next < 0 ? next + H : next;
-    auto fetch = [&]() -> f32x4 {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(pin + next * pitch);
+    auto fetch = [&]() -> V {
+      const V v = B::load(pin + next * pitch);
       if constexpr (WRAP) {
         ++next;
         next = next == H ? 0 : next;
@@ -1018,12 +1114,12 @@ __device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* 
       }
       return v;
     };
-    f32x4 win[3][S0];
+    V win[3][S0];
 #pragma unroll
     for (int q = 0; q < 3; ++q)
 #pragma unroll
-      for (int l = 0; l < S0; ++l) win[q][l] = f32x4(0.f);
-    f32x4 pf[PF];
+      for (int l = 0; l < S0; ++l) win[q][l] = B::zero();
+    V pf[PF];
 #pragma unroll
     for (int k = 0; k < PF; ++k) pf[k] = fetch();
     constexpr int kWarm = (3 * (S0 - 1)) / PF * PF;  // see stream_chunk_rot: level l matters from iteration 3l + 2
@@ -1033,11 +1129,11 @@ __device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* 
       for (int k = 0; k < PF; ++k) {
         const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
         const int b = (ib + k) / 3;
-        win[p2][0] = rot_in(pf[k]);
+        win[p2][0] = B::enter(pf[k]);
         pf[k] = fetch();
 #pragma unroll
         for (int l = S0 - 2; l >= 0; --l)
-          if (l <= b) win[p0][l + 1] = jac_rot4f(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+          if (l <= b) win[p0][l + 1] = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
       }
       __syncthreads();
     }
@@ -1048,12 +1144,12 @@ __device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* 
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
         const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
-        win[p2][0] = rot_in(pf[k]);
+        win[p2][0] = B::enter(pf[k]);
         pf[k] = fetch();
-        f32x4 top;
+        V top;
 #pragma unroll
         for (int l = S0 - 1; l >= 0; --l) {
-          const f32x4 o = jac_rot4f(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+          const V o = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
           if (l == S0 - 1) top = o;
           else win[p0][l + 1] = o;
         }
@@ -1066,28 +1162,28 @@ __device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* 
     }
   } else {
     // Output descriptor over rows [ys, ye) (see stream_chunk_rot).
-    const float* obase = out + core_off + (xw - SA) + ys * pitch;
+    const T* obase = out + core_off + (xw - SA) + ys * pitch;
     const unsigned long long ob = reinterpret_cast<unsigned long long>(obase);
     const unsigned ob_lo = __builtin_amdgcn_readfirstlane(unsigned(ob)),
                    ob_hi = __builtin_amdgcn_readfirstlane(unsigned(ob >> 32));
-    float* obase_u = reinterpret_cast<float*>((static_cast<unsigned long long>(ob_hi) << 32) | ob_lo);
-    const int nbytes = __builtin_amdgcn_readfirstlane(int(rows * pitch * index_t(sizeof(float))));
+    T* obase_u = reinterpret_cast<T*>((static_cast<unsigned long long>(ob_hi) << 32) | ob_lo);
+    const int nbytes = __builtin_amdgcn_readfirstlane(int(rows * pitch * index_t(sizeof(T))));
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(obase_u, 0, nbytes, 0x00020000);
     const bool store_lane = lane >= AL && lane < kWaveSize - AL && gx < x_end && xw < x_end;
-    const unsigned lane_off = unsigned(lane) * unsigned(N * sizeof(float));
-    const unsigned row_bytes = unsigned(pitch) * unsigned(sizeof(float));
+    const unsigned lane_off = unsigned(lane) * unsigned(N * sizeof(T));
+    const unsigned row_bytes = unsigned(pitch) * unsigned(sizeof(T));
     constexpr unsigned kDrop = 0x80000000u;
-    f32x4 win[3][S1];
+    V win[3][S1];
 #pragma unroll
     for (int q = 0; q < 3; ++q)
 #pragma unroll
-      for (int l = 0; l < S1; ++l) win[q][l] = f32x4(0.f);
+      for (int l = 0; l < S1; ++l) win[q][l] = B::zero();
 #pragma unroll 1
     for (int t = 0; t < T1; ++t) __syncthreads();  // stage 0 fills the ring
     constexpr int kWarm = (3 * (S1 - 1)) / PF * PF;
 #pragma unroll 1
     for (int ib = 0; ib < kWarm; ib += PF) {
-      f32x4 inrow[PF];
+      V inrow[PF];
       const int base = (ib / PF) % 3 * PF;  // RING = 3 * PF and ib is a multiple of PF
 #pragma unroll
       for (int k = 0; k < PF; ++k) inrow[k] = my[(base + k) * kWaveSize];
@@ -1098,13 +1194,13 @@ __device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* 
         win[p2][0] = inrow[k];
 #pragma unroll
         for (int l = S1 - 2; l >= 0; --l)
-          if (l <= b) win[p0][l + 1] = jac_rot4f(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+          if (l <= b) win[p0][l + 1] = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
       }
       __syncthreads();
     }
 #pragma unroll 1
     for (index_t i = kWarm; i < (blocks - T1) * PF; i += PF) {
-      f32x4 inrow[PF];
+      V inrow[PF];
       const int base = int((i / PF) % 3) * PF;
 #pragma unroll
       for (int k = 0; k < PF; ++k) inrow[k] = my[(base + k) * kWaveSize];
@@ -1113,19 +1209,17 @@ __device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* 
         const index_t j = i + k;
         const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
         win[p2][0] = inrow[k];
-        f32x4 top;
+        V top;
 #pragma unroll
         for (int l = S1 - 1; l >= 0; --l) {
-          const f32x4 o = jac_rot4f(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+          const V o = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
           if (l == S1 - 1) top = o;
           else win[p0][l + 1] = o;
         }
         const index_t r = j - (3 * S1 - 1);
         const bool ok = store_lane && r >= 0 && r < rows;
         const unsigned off = ok ? lane_off + unsigned(r) * row_bytes : kDrop;
-        const f32x4 nat = rot_out(top);
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, nat),
-                                               orsrc, int(off), 0, 2 /* nt */);
+        B::store(top, orsrc, off);
       }
       __syncthreads();
     }
@@ -1134,16 +1228,18 @@ __device__ __forceinline__ void pipe_chunk(const float* __restrict__ in, float* 
 
 // Balanced persistent launch of the two-stage pipeline: 512-thread workgroups
 // (4 strips x 2 stages), equal shares of (4-strip group) x rows as in
-// stencil5_stream_balanced_kernel. fp32 only (rotated-pair layout); needs
-// x_end % 4 == 0 and a chunk under 2 GiB (the output buffer descriptor).
+// stencil5_stream_balanced_kernel. T = float: rotated-pair layout; T = double:
+// wide-lane body (FastBody<T>). Needs x_end % 4 == 0 and a chunk under 2 GiB
+// (the output buffer descriptor).
 // PRIO (tuning): 1 raises the fetching stage's wave priority, 2 the storing stage's.
-template <int S0, int S1, int PF, bool WRAP, int PRIO = 0>
+template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float>
 __global__ __launch_bounds__(2 * kBlock) void stencil5_stream_pipe_kernel(
-    const float* __restrict__ in, float* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
-    index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, float c0, float c1) {
+    const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
+    index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
   using P = PipeShape<S0, S1, PF>;
-  constexpr int OW = StreamShape<float, P::S>::OW;
-  __shared__ f32x4 ring[kWavesPerBlock * P::RING * kWaveSize];
+  using B = typename FastBody<T>::type;
+  constexpr int OW = StripShape<T, P::S, true>::OW;
+  __shared__ typename B::V ring[kWavesPerBlock * P::RING * kWaveSize];
   const index_t rows = y_end - y_begin;
   const index_t strips = (x_end - x_begin + OW - 1) / OW;
   const index_t groups = (strips + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -1162,7 +1258,7 @@ __global__ __launch_bounds__(2 * kBlock) void stencil5_stream_pipe_kernel(
     const index_t grp = a / rows, r0 = a - grp * rows;
     const index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
     const index_t xw = x_begin + (grp * kWavesPerBlock + strip) * OW;
-    pipe_chunk<S0, S1, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1,
+    pipe_chunk<B, S0, S1, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1,
                                  ring + strip * P::RING * kWaveSize, stage);
     a += r1 - r0;
   }

@@ -53,7 +53,10 @@ def _frozen_edge_reference(full, steps, c0=0.2, c1=0.2):
     (8192, 8192, 12, torch.float32, "stream_balanced_rot"),
     (4096, 8192, 16, torch.float32, "stream_balanced_rot"),
     (16384, 4096, 16, torch.float32, "stream_balanced_rot"),  # wide tile, deepest block
-    (4096, 4096, 12, torch.float64, "stream_balanced"),       # fp64 balanced path
+    (4096, 4096, 12, torch.float64, "stream_pipe"),           # fp64 default S: wide-lane pipeline 6 + 6
+    (2048, 1024, 16, torch.float64, "stream_pipe"),           # fp64 8 + 8
+    (300, 200, 12, torch.float64, "stream_pipe"),             # fp64, narrower than one strip group
+    (4094, 4096, 12, torch.float64, "stream_balanced"),       # width % 4 != 0: natural fp64 layout
     (8192, 8192, 8, torch.float64, "stream_balanced"),
 ])
 def test_balanced_wrap_matches_periodic_reference(gpu, w, h, steps, dtype, kernel):
@@ -83,7 +86,9 @@ def test_balanced_wrap_matches_periodic_reference(gpu, w, h, steps, dtype, kerne
     (8190, 4096, 16, None, torch.float32, "stream_balanced"),
     # Interior rectangle of the overlap schedule (vector-aligned columns).
     (8192, 4096, 12, (16, 8176, 12, 4084), torch.float32, "stream_balanced_rot"),
-    (4096, 4096, 12, None, torch.float64, "stream_balanced"),
+    (4096, 4096, 12, None, torch.float64, "stream_pipe"),
+    (4096, 2048, 16, (8, 4088, 16, 2032), torch.float64, "stream_pipe"),
+    (4094, 4096, 12, None, torch.float64, "stream_balanced"),  # ragged: natural fp64 layout
 ])
 def test_balanced_ghost_ring_matches_reference(gpu, w, h, steps, rect, dtype, kernel):
     esz = torch.tensor([], dtype=dtype).element_size()
@@ -129,7 +134,8 @@ def test_solver_caps_deep_blocks_where_the_pipeline_cannot_run(gpu):
 def test_solver_blocked_run_bitwise_equals_single_steps(gpu, dtype, block):
     """run(20) at the auto time block (8192^2: fp32 S = 20 -> one 20-step
     pipeline pass; fp64 S = 12 -> two super-steps of 10) equals 20 one-step
-    iterations bit for bit, and prepare() changes nothing."""
+    iterations bit for bit, and prepare() changes nothing. (fp64 S = 12 runs
+    the wide-lane pipeline.)"""
     kw = dict(global_width=8192, global_height=8192, dims="1x1", dtype=dtype, seed=99)
     blocked = Stencil2D(StencilConfig(**kw))
     assert blocked.time_block == block
@@ -189,6 +195,22 @@ def test_headline_rate_floor(gpu):
     rate = st.cells_per_step * 20 / (time.perf_counter() - t0) / 1e9
     assert hip().last_stencil_dispatch() == "stream_pipe"
     assert rate > 6000, f"{rate:.0f} Gcells/s"
+
+
+def test_fp64_rate_floor(gpu):
+    """fp64 (the reference's element type) at 8192^2, auto S = 12: the wide-lane
+    two-stage pipeline. Tuner: 3.0 T cells/s (natural layout: 2.2)."""
+    st = Stencil2D(StencilConfig(global_width=8192, global_height=8192, dims="1x1", dtype="f64"))
+    assert st.time_block == 12
+    st.run(12)
+    st.prepare(240)
+    st.synchronize()
+    t0 = time.perf_counter()
+    st.run(240)
+    st.synchronize()
+    rate = st.cells_per_step * 240 / (time.perf_counter() - t0) / 1e9
+    assert hip().last_stencil_dispatch() == "stream_pipe"
+    assert rate > 2500, f"{rate:.0f} Gcells/s"
 
 
 @pytest.mark.parametrize("backend,loopback", [("local", False), ("rccl", True)])
