@@ -158,8 +158,9 @@ enum class DotReduce : int {
   Racy = 4,        // NO_SYNC demonstrator: non-atomic `*out += partial` (ref_parallel-dot-product-atomics.cu:26-32)
 };
 
-// Scratch needed by the dot kernels: `partials` holds >= dot_max_blocks() Acc
-// values, `counter` one unsigned int (zeroed by the launcher every call).
+// Scratch needed by the dot kernels: `partials` holds >= grid Acc values
+// (dot_grid_size(n, kDotBlock) when grid <= 0: one workgroup per CU), `counter`
+// one unsigned int (zeroed by the launcher every call).
 int dot_grid_size(index_t n, int block);
 constexpr int kDotBlock = 256;
 

@@ -189,11 +189,15 @@ __global__ __launch_bounds__(kBlock) void dot_single_pass_kernel(const T* __rest
 }  // namespace
 
 int dot_grid_size(index_t n, int block) {
-  // 4 workgroups per CU: enough waves to stream HBM, few enough partials that the
-  // combine step (single-pass last block, two-pass finisher) is a short tail.
+  // One workgroup per CU: with kUnroll x 2 KiB of loads in flight per wave, 4
+  // waves per CU already stream HBM, and fewer partials keep the combine step
+  // (single-pass last block, two-pass finisher, atomics) a short tail.
+  // Measured on 2^27 / 2^30 fp64 (profiles/r02_reentry2/dot_sweep.jsonl, GB/s,
+  // 1 vs 4 workgroups per CU): single-pass 6242 / 6726 vs 5981 / 6633,
+  // atomic 6565 / 6756 vs 6065 / 6602, two-pass 6565 / 6750 vs 6628 / 6675.
   const index_t per_block = index_t(block) * 16;
   const index_t want = (n + per_block - 1) / per_block;
-  return int(std::max<index_t>(1, std::min<index_t>(want, index_t(device_cu_count()) * 4)));
+  return int(std::max<index_t>(1, std::min<index_t>(want, index_t(device_cu_count()))));
 }
 
 template <typename T, typename Acc>
@@ -221,7 +225,7 @@ void dot(const T* x, const T* y, index_t n, Acc* out, Acc* partials, unsigned* c
       break;
     case DotReduce::SinglePass:
       // Re-initialise the ticket every call (a memset node under graph capture).
-      MXS_HIP_CHECK(hipMemsetAsync(counter, 0, 16, s));
+      MXS_HIP_CHECK(hipMemsetAsync(counter, 0, sizeof(unsigned), s));
       dot_single_pass_kernel<T, Acc><<<grid, kBlock, 0, s>>>(x, y, n, out, partials, counter);
       break;
   }
