@@ -18,7 +18,9 @@
 //
 // Positional arguments keep the reference contract: [local width (= height) [stencil width]].
 // More options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
-// --iters N, --warmup N, --time-block S (default: measured per tile size, 12 or 16), --no-overlap, --no-graph,
+// --iters N, --warmup N, --time-block S (default: measured per tile size and dtype), --no-overlap, --no-graph,
+// --c-center C --c-neighbor C (default 0.2 / 0.2), --no-sum-form (keep the per-step evaluation in the
+// time-blocked kernels: bitwise equal to the CPU app; default: sum form when the coefficients are equal),
 // --loopback, --bind bunch|rrobin,
 // --dump / --no-dump, --checksum, --non-periodic, --seed S, --json FILE,
 // --checkpoint FILE / --resume FILE (collective MPI-IO global grid file, any
@@ -81,10 +83,15 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   // A non-periodic grid has fixed boundary values that the S-step kernels
   // would advance as cells: one exchange per iteration there (as the solver does).
   const bool all_periodic = topo.periodic_rows && topo.periodic_cols;
+  const double c_center = cli.get_double("c-center", 0.2), c_neighbor = cli.get_double("c-neighbor", 0.2);
+  // --no-sum-form: per-step evaluation everywhere (bitwise equal to the CPU app).
+  const bool sum_form = !cli.flag("no-sum-form") && c_center == c_neighbor;
   const int time_block =
       (backend == "mpi-staged" || !all_periodic)
           ? 1
-          : int(cli.get_int("time-block", iters > 0 && lw >= 64 && lh >= 64 ? kernels::auto_time_block(lw, lh, int(sizeof(T))) : 1));
+          : int(cli.get_int("time-block", iters > 0 && lw >= 64 && lh >= 64
+                                              ? kernels::auto_time_block(lw, lh, int(sizeof(T)), sum_form)
+                                              : 1));
   const TileGeom g = TileGeom::aligned(lw, lh, std::max(sw / 2, time_block), std::max(sh / 2, time_block),
                                        int(sizeof(T)));
   std::unique_ptr<RcclComm> comm;
@@ -107,7 +114,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   cfg.overlap = cli.flag("overlap") || (!cli.flag("no-overlap") && !shared_gpu && time_block == 1);
   cfg.use_graph = !cli.flag("no-graph");
   cfg.loopback_self = loopback;
-  cfg.coeffs = {cli.get_double("c-center", 0.2), cli.get_double("c-neighbor", 0.2)};
+  cfg.coeffs = {c_center, c_neighbor, sum_form};
   cfg.time_block = time_block;
   std::unique_ptr<StencilSolver<T>> solver;
   std::unique_ptr<MpiStagedHalo<T>> staged;

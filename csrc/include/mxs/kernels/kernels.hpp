@@ -39,7 +39,14 @@ void fill_random(T* tile, const TileGeom& g, index_t global_x0, index_t global_y
 struct Stencil5Coeffs {
   double center = 0.2;
   double neighbor = 0.2;
+  // With center == neighbor (= c, the 5-point average) the S-step kernels may
+  // run the sum form: each pass accumulates plain 5-point sums and scales by
+  // c^S once when it stores (8 instead of 11 VALU issue slots per 4 fp32 cells
+  // and step; stencil_device.hpp). Equal to the per-step evaluation up to
+  // rounding (a few ulp), not bit for bit. false = always the per-step form.
+  bool sum_form = true;
 };
+inline bool uses_sum_form(const Stencil5Coeffs& c) { return c.sum_form && c.center == c.neighbor; }
 
 enum class StencilVariant : int {
   Auto = 0,        // tuned default
@@ -80,19 +87,18 @@ constexpr int kMaxTimeBlock = 16;
 // of 4 (whole vectors); see stencil5_deep_supported().
 constexpr int kMaxTimeBlockDeep = 32;
 // Measured default S for a w x h tile of `elem_bytes`-byte cells
-// (profiles/stencil_tuning/tunes_*, profiles/r02_deep/pipe*_*, profiles/r02_f64):
-// fp32 takes the two-stage pipeline at S = 20, level split 11 + 9 (32768^2:
-// 8.0-8.2 T cells/s vs 7.85-7.9 single-wave at S = 16; 8192^2: 6.4-6.6 vs 5.9;
-// ghost-ring (multi-GPU) tiles 16384 x 8192 .. 32768 x 16384: +0-8%; S = 24
-// measured no better and costs a 4% wider apron); fp64 takes the wide-lane
-// two-stage pipeline at S = 12 (6 + 6: 3.0-3.35 T cells/s vs 2.2-2.5 for the
-// natural single-wave kernel at S = 12 and 1.7-1.9 at S = 16); the fp32
-// single-wave kernels (small tiles): S = 16 from 2^27 cells, S = 12 below (the
-// pass is VALU-bound beyond S ~ 8, so a deeper block only pays where the chunk
-// / strip aprons are small against the tile).
-inline int auto_time_block(index_t w, index_t h, int elem_bytes = 4) {
+// (profiles/stencil_tuning/tunes_*, profiles/r02_deep/pipe*_*, profiles/r02_f64,
+// profiles/r02_sum): fp32 takes the two-stage pipeline at S = 20 (sum form,
+// split 10 + 10: 32768^2 9.96 T cells/s, 16384 x 8192 9.18, 8192^2 7.79; the
+// per-step form 11 + 9: 8.27 / 7.56 / 6.46; S = 24-28 adds 2-4% at 32768^2
+// only); fp64 the wide-lane pipeline at S = 16 in the sum form (8 + 8: 3.5 /
+// 4.05 T cells/s at 8192^2 / 16384^2) or S = 12 per step (6 + 6: 3.0 / 3.3);
+// the fp32 single-wave kernels (small tiles): S = 16 from 2^27 cells, S = 12
+// below (the pass is VALU-bound beyond S ~ 8, so a deeper block only pays
+// where the chunk / strip aprons are small against the tile).
+inline int auto_time_block(index_t w, index_t h, int elem_bytes = 4, bool sum_form = true) {
   if (elem_bytes == 4 && w >= 1024 && h >= 1024) return 20;
-  if (elem_bytes == 8) return 12;
+  if (elem_bytes == 8) return sum_form ? 16 : 12;
   return w * h >= (index_t(1) << 27) ? 16 : 12;
 }
 // Whether a `steps`-step stencil5_tb launch over [x0, x1) can run: every

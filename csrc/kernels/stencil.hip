@@ -36,12 +36,14 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
 #include "mxs/runtime/hip_utils.hpp"
 
 #include "stencil_device.hpp"
+#include "stencil_pipe.hpp"
 
 namespace mxs {
 namespace kernels {
@@ -152,7 +154,7 @@ constexpr int stream_pf() {
   return (sizeof(T) == 4 && S <= 12) ? 6 : 3;
 }
 
-template <typename T, int S, bool WRAP>
+template <typename T, int S, bool WRAP, bool SUM>
 int balanced_blocks() {
   static int blocks = 0;
   if (blocks == 0) {
@@ -160,7 +162,7 @@ int balanced_blocks() {
     MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &occ,
         reinterpret_cast<const void*>(
-            stencil5_stream_balanced_kernel<T, S, stream_pf<T, S>(), WRAP, true, sizeof(T) == 4>),
+            stencil5_stream_balanced_kernel<T, S, stream_pf<T, S>(), WRAP, true, sizeof(T) == 4, SUM>),
         kBlock, 0));
     MXS_HIP_CHECK(hipGetDevice(&dev));
     MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -184,21 +186,23 @@ bool rot_ok(const TileGeom& g, index_t x1, index_t chunk_rows) {
   return sizeof(T) == 4 && x1 % 4 == 0 && chunk_rows * g.pitch * index_t(sizeof(T)) < (index_t(1) << 31);
 }
 
-template <typename T, int S, bool WRAP>
+// SUM: the balanced rotated kernel runs the sum form (sc = c^S, see
+// stencil_device.hpp); every other form keeps the per-step coefficients.
+template <typename T, int S, bool WRAP, bool SUM = false>
 void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
-                   hipStream_t s) {
+                   T sc, hipStream_t s) {
   constexpr int OW = StreamShape<T, S>::OW;
   constexpr bool kF32 = sizeof(T) == 4;
   const index_t strips = (x1 - x0 + OW - 1) / OW;
   const index_t rows = y1 - y0;
   const index_t groups = (strips + kWavesPerBlock - 1) / kWavesPerBlock;
-  const int blocks = balanced_blocks<T, S, WRAP>();
+  const int blocks = balanced_blocks<T, S, WRAP, SUM>();
   if (groups * rows >= index_t(blocks) * 64) {
     const index_t share = (groups * rows + blocks - 1) / blocks;
     if (kF32 && rot_ok<T>(g, x1, std::min(share, rows))) {
-      stencil5_stream_balanced_kernel<T, S, stream_pf<T, S>(), WRAP, true, kF32><<<blocks, kBlock, 0, s>>>(
-          in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
-      note("stream_balanced_rot");
+      stencil5_stream_balanced_kernel<T, S, stream_pf<T, S>(), WRAP, true, kF32, SUM><<<blocks, kBlock, 0, s>>>(
+          in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, SUM ? sc : c0, c1);
+      note(SUM ? "stream_balanced_rot_sum" : "stream_balanced_rot");
     } else {
       stencil5_stream_balanced_kernel<T, S, 3, WRAP><<<blocks, kBlock, 0, s>>>(
           in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
@@ -220,84 +224,15 @@ void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
   }
 }
 
-// Two-stage pipeline. fp32 (S = 17..32): the fetching stage takes one level
-// more than half, S0 = S/2 + 1 (at most 16), S1 = S - S0 — measured 2-3% ahead
-// of the even split on 4 of 5 tile shapes (profiles/r02_deep/pipe2_*,
-// pipe20_*); 6 input rows in flight up to S = 28 (the fetch ring fits beside
-// the windows at 2 waves/SIMD), 3 above. fp64 (S = 12 and 16, wide-lane body):
-// even split, 3 rows in flight — 6 + 6 is the fastest fp64 form on every
-// measured tile (8192^2 3.0 vs 2.2 T cells/s for the single-wave natural
-// kernel, 16384^2 3.35 vs 2.5; 8 + 8 2.8-3.1; odd depths lose to the apron
-// rounding: profiles/r02_f64). One 512-thread workgroup per CU: the occupancy
-// API decides, as for the single-wave balanced kernel.
-template <typename T, int S>
-constexpr int pipe_s0() {
-  if constexpr (sizeof(T) == 8) return S / 2;
-  return S / 2 + 1 < 16 ? S / 2 + 1 : 16;
-}
-template <typename T, int S>
-constexpr int pipe_pf() {
-  return (sizeof(T) == 4 && S <= 28) ? 6 : 3;
-}
-template <typename T, int S, bool WRAP>
-constexpr auto pipe_kernel() {
-  return stencil5_stream_pipe_kernel<pipe_s0<T, S>(), S - pipe_s0<T, S>(), pipe_pf<T, S>(), WRAP, 0, T>;
-}
-
-template <typename T, int S, bool WRAP>
-int pipe_blocks() {
-  static int blocks = 0;
-  if (blocks == 0) {
-    int occ = 0;
-    MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, reinterpret_cast<const void*>(pipe_kernel<T, S, WRAP>()), 2 * kBlock, 0));
-    blocks = std::max(occ, 1) * device_cu_count();
-  }
-  return blocks;
-}
-
-template <typename T, int S, bool WRAP>
-index_t pipe_share(index_t x0, index_t x1, index_t y0, index_t y1) {
-  constexpr int OW = StripShape<T, S, true>::OW;
-  const index_t groups = ((x1 - x0 + OW - 1) / OW + kWavesPerBlock - 1) / kWavesPerBlock;
-  const int blocks = pipe_blocks<T, S, WRAP>();
-  return (groups * (y1 - y0) + blocks - 1) / blocks;
-}
-
-template <typename T, int S, bool WRAP>
-void launch_pipe(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
-                 hipStream_t s) {
-  const index_t share = pipe_share<T, S, WRAP>(x0, x1, y0, y1);
-  MXS_CHECK(std::min(share, y1 - y0) * g.pitch * index_t(sizeof(T)) < (index_t(1) << 31),
-            "stencil5_tb: a pipeline chunk must stay under 2 GiB (buffer-descriptor stores)");
-  pipe_kernel<T, S, WRAP>()<<<pipe_blocks<T, S, WRAP>(), 2 * kBlock, 0, s>>>(
-      in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
-  note("stream_pipe");
-}
-
-// Whether the fp64 wide-lane pipeline can take [x0, x1) x [y0, y1) at depth S:
-// whole 4-cell lane vectors (x0, x1 and, wrapping, the width multiples of 4),
-// the apron inside the row padding, and a chunk under 2 GiB.
-template <typename T, int S, bool WRAP>
-bool wide_pipe_ok(const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1) {
-  constexpr int SA = StripShape<T, S, true>::SA;
-  if (x0 % 4 != 0 || x1 % 4 != 0) return false;
-  if (WRAP && g.width % 4 != 0) return false;
-  const index_t lead = g.x_origin + g.halo_x;
-  if (!WRAP && (lead < SA || g.pitch < lead + (g.width + 3) / 4 * 4 + SA)) return false;
-  return std::min(pipe_share<T, S, WRAP>(x0, x1, y0, y1), y1 - y0) * g.pitch * index_t(sizeof(T)) <
-         (index_t(1) << 31);
-}
-
 // Dispatch by shape. Bulk rectangles take the wave-streaming kernel (Auto) or
 // the LDS tile (LdsTile, S <= 8): 128 fp32 columns (64 fp64: same bytes) x 32
 // rows per 256-thread workgroup, single LDS buffer. The overlap schedule's
 // boundary strips are only S rows or S columns thin; a bulk tile or a 256-column
 // wave strip would recompute 8-32x the strip, so thin strips get a matching thin
 // LDS tile (32 x 128 for column strips, 128 x 16 for row strips).
-template <typename T, int S, bool WRAP>
+template <typename T, int S, bool WRAP, bool SUM>
 void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
-               StencilVariant v, hipStream_t s) {
+               T sc, StencilVariant v, hipStream_t s) {
   constexpr int TW = sizeof(T) == 4 ? 128 : 64;
   constexpr int NW = sizeof(T) == 4 ? 32 : 16;
   constexpr int NH = (sizeof(T) == 8 && S > 8) ? 64 : 128;  // keeps the fp64 thin tile under 64 KB of LDS
@@ -309,22 +244,33 @@ void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, i
     if (v == StencilVariant::LdsTile)
       return launch_tb_tile<T, S, TW, 32, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
   }
-  if constexpr (sizeof(T) == 8 && (S == 12 || S == 16)) {
+  if constexpr (sizeof(T) == 8 && S >= kPipeMinF64) {
     if (wide_pipe_ok<T, S, WRAP>(g, x0, x1, y0, y1))
-      return launch_pipe<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
+      return launch_pipe<T, S, WRAP, SUM>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
   }
-  launch_stream<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
+  launch_stream<T, S, WRAP, SUM && sizeof(T) == 4>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
 }
 
+// sum: c_center == c_neighbor and the caller allows the sum form (the fast
+// bodies then take sc = c^S); S = 1 always keeps the per-step form.
 template <typename T, bool WRAP, int S = 1>
-void dispatch_tb(int steps, const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
-                 T c0, T c1, StencilVariant v, hipStream_t s) {
+void dispatch_tb(int steps, bool sum, const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0,
+                 index_t y1, T c0, T c1, StencilVariant v, hipStream_t s) {
+  const T sc = T(std::pow(double(c1), double(S)));
   if constexpr (S <= kMaxTimeBlock) {
-    if (steps == S) return launch_tb<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, v, s);
-    return dispatch_tb<T, WRAP, S + 1>(steps, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+    if (steps == S) {
+      if constexpr (S > 1) {
+        if (sum) return launch_tb<T, S, WRAP, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s);
+      }
+      return launch_tb<T, S, WRAP, false>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s);
+    }
+    return dispatch_tb<T, WRAP, S + 1>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   } else if constexpr (S <= kMaxTimeBlockDeep && sizeof(T) == 4) {
-    if (steps == S) return launch_pipe<T, S, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
-    return dispatch_tb<T, WRAP, S + 1>(steps, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+    if (steps == S) {
+      if (sum) return launch_pipe<T, S, WRAP, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+      return launch_pipe<T, S, WRAP, false>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+    }
+    return dispatch_tb<T, WRAP, S + 1>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   } else {
     MXS_CHECK(false, "stencil5_tb: steps must be in [1, " << (sizeof(T) == 4 ? kMaxTimeBlockDeep : kMaxTimeBlock)
                                                           << "], got " << steps);
@@ -354,8 +300,9 @@ void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, 
               "stencil5_tb: row padding too small for the x apron");
   }
   const T c0 = T(c.center), c1 = T(c.neighbor);
-  if (wrap) dispatch_tb<T, true>(steps, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
-  else dispatch_tb<T, false>(steps, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+  const bool sum = uses_sum_form(c) && v != StencilVariant::LdsTile;
+  if (wrap) dispatch_tb<T, true>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+  else dispatch_tb<T, false>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   MXS_HIP_CHECK_LAUNCH();
 }
 
@@ -389,6 +336,9 @@ void stencil_box(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1,
 }
 
 const char* last_stencil_dispatch() { return g_last_dispatch.load(std::memory_order_relaxed); }
+namespace detail {
+void note_dispatch(const char* k) { note(k); }
+}  // namespace detail
 
 #define MXS_INST_STENCIL(T)                                                                                    \
   template void stencil5_rows<T>(const T*, T*, const TileGeom&, index_t, index_t, Stencil5Coeffs, hipStream_t, \

@@ -682,7 +682,7 @@ struct BodyRotF32 {  // rotated-pair fp32 (jac_rot4f)
   static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, float c0, float c1) {
     return jac_rot4f(u, m, d, c0, c1);
   }
-  static __device__ __forceinline__ void store(const V& top, __amdgpu_buffer_rsrc_t r, unsigned off) {
+  static __device__ __forceinline__ void store(const V& top, __amdgpu_buffer_rsrc_t r, unsigned off, float) {
     const f32x4 nat = rot_out(top);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, nat), r, int(off), 0, 2 /* nt */);
   }
@@ -700,21 +700,78 @@ struct BodyWideF64 {  // 4 consecutive fp64 cells per lane (jac_w4d)
   static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, double c0, double c1) {
     return jac_w4d(u, m, d, c0, c1);
   }
-  static __device__ __forceinline__ void store(const V& top, __amdgpu_buffer_rsrc_t r, unsigned off) {
+  static __device__ __forceinline__ void store(const V& top, __amdgpu_buffer_rsrc_t r, unsigned off, double) {
     const f64x2 lo = top.xy, hi = top.zw;
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, lo), r, int(off), 0, 2 /* nt */);
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, hi), r, int(off + 16u), 0, 2 /* nt */);
   }
 };
-template <typename T>
+
+// Sum form (c_center == c_neighbor == c, the default 5-point average). The
+// S-level recurrence u' = c * (5-point sum of u) is linear with one uniform
+// scale, so a pass carries v_l = u_l / c^l — plain 5-point sums, no multiply —
+// and applies c^S once when it stores (the kernels' c0 argument holds c^S).
+// The horizontal 3-sums come from pair sums: with p = u[2k] + u[2k+1],
+// h3(x) = p(x) + u[x even ? x - 1 : x + 1]. Rotated fp32: 8 VALU issue slots
+// per 4 cells and level instead of 11 (2 ns + 1 pair + 1 + 2 DPP h3 + 2 sum);
+// wide fp64: 14 fp64 ops + 4 moves instead of 20 + 4. The result equals the
+// step-by-step evaluation up to rounding (not bit for bit: different
+// association, one scale per pass instead of one per step); magnitudes grow
+// as 5^S inside a pass (|u| up to 3e38 / 5^S stays finite).
+__device__ __forceinline__ f32x4 sum_rot4f(const f32x4& up, const f32x4& mid, const f32x4& dn) {
+  const f32x2 am = mid.xy, bm = mid.zw;  // (c1, c2), (c3, c0)
+  const f32x2 ns_a = up.xy + dn.xy, ns_b = up.zw + dn.zw;
+  const f32x2 p = am + bm.yx;            // (c0 + c1, c2 + c3)
+  const f32x2 h_a = p + am.yx;           // (p01 + c2, p23 + c1) = h3(c1), h3(c2)
+  f32x2 h_b;                             // h3(c3) = p23 + c4, h3(c0) = p01 + c[-1]
+  h_b.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bm.y), kDppWaveShl1, 0xf, 0xf, true)) + p.y;
+  h_b.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bm.x), kDppWaveShr1, 0xf, 0xf, true)) + p.x;
+  f32x4 o;
+  o.xy = ns_a + h_a;
+  o.zw = ns_b + h_b;
+  return o;
+}
+__device__ __forceinline__ f64x4 sum_w4d(const f64x4& up, const f64x4& mid, const f64x4& dn) {
+  const double left = lane_shift<double, kDppWaveShr1>(mid.w);
+  const double right = lane_shift<double, kDppWaveShl1>(mid.x);
+  const double p01 = mid.x + mid.y, p23 = mid.z + mid.w;
+  f64x4 o;
+  o.x = (up.x + dn.x) + (p01 + left);
+  o.y = (up.y + dn.y) + (p01 + mid.z);
+  o.z = (up.z + dn.z) + (p23 + mid.y);
+  o.w = (up.w + dn.w) + (p23 + right);
+  return o;
+}
+struct BodySumF32 : BodyRotF32 {
+  static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, float, float) { return sum_rot4f(u, m, d); }
+  static __device__ __forceinline__ void store(const V& top, __amdgpu_buffer_rsrc_t r, unsigned off, float scale) {
+    BodyRotF32::store(top * scale, r, off, scale);
+  }
+};
+struct BodySumF64 : BodyWideF64 {
+  static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, double, double) { return sum_w4d(u, m, d); }
+  static __device__ __forceinline__ void store(const V& top, __amdgpu_buffer_rsrc_t r, unsigned off, double scale) {
+    BodyWideF64::store(top * scale, r, off, scale);
+  }
+};
+
+template <typename T, bool SUM = false>
 struct FastBody;
 template <>
-struct FastBody<float> {
+struct FastBody<float, false> {
   using type = BodyRotF32;
 };
 template <>
-struct FastBody<double> {
+struct FastBody<double, false> {
   using type = BodyWideF64;
+};
+template <>
+struct FastBody<float, true> {
+  using type = BodySumF32;
+};
+template <>
+struct FastBody<double, true> {
+  using type = BodySumF64;
 };
 
 // Strip geometry of the kernels: FAST = the 4-cells-per-lane bodies above,
@@ -969,7 +1026,7 @@ __device__ __forceinline__ void stream_chunk_fast(const typename B::T* __restric
       const index_t r = j - (3 * S - 1);  // output row (relative to ys) of this iteration
       const bool ok = store_lane && r >= 0 && r < rows;
       const unsigned off = ok ? lane_off + unsigned(r) * row_bytes : kDrop;
-      B::store(top, orsrc, off);
+      B::store(top, orsrc, off, c0);
     }
   }
 }
@@ -1006,7 +1063,7 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __rest
 // so the apron columns two neighbouring waves both read are L2 hits — and a
 // share that crosses a group boundary restarts there. No tail round, and
 // (3S-1)/share redundant rows instead of (3S-1)/CH per chunk.
-template <typename T, int S, int PF, bool WRAP, bool DPP = true, bool ROT = false>
+template <typename T, int S, int PF, bool WRAP, bool DPP = true, bool ROT = false, bool SUM = false>
 __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
@@ -1029,8 +1086,8 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
     if (xw < x_end) {
       wp.done = a - a0;
       if constexpr (ROT)
-        stream_chunk_fast<typename FastBody<T>::type, S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end,
-                                                                   y_begin + r0, y_begin + r1, c0, c1, &wp);
+        stream_chunk_fast<typename FastBody<T, SUM>::type, S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end,
+                                                                        y_begin + r0, y_begin + r1, c0, c1, &wp);
       else
         stream_chunk<T, S, PF, WRAP, DPP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0,
                                           c1);
@@ -1219,7 +1276,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
         const index_t r = j - (3 * S1 - 1);
         const bool ok = store_lane && r >= 0 && r < rows;
         const unsigned off = ok ? lane_off + unsigned(r) * row_bytes : kDrop;
-        B::store(top, orsrc, off);
+        B::store(top, orsrc, off, c0);
       }
       __syncthreads();
     }
@@ -1232,12 +1289,12 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 // wide-lane body (FastBody<T>). Needs x_end % 4 == 0 and a chunk under 2 GiB
 // (the output buffer descriptor).
 // PRIO (tuning): 1 raises the fetching stage's wave priority, 2 the storing stage's.
-template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float>
+template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float, bool SUM = false>
 __global__ __launch_bounds__(2 * kBlock) void stencil5_stream_pipe_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
   using P = PipeShape<S0, S1, PF>;
-  using B = typename FastBody<T>::type;
+  using B = typename FastBody<T, SUM>::type;
   constexpr int OW = StripShape<T, P::S, true>::OW;
   __shared__ typename B::V ring[kWavesPerBlock * P::RING * kWaveSize];
   const index_t rows = y_end - y_begin;

@@ -1,0 +1,105 @@
+// Two-stage pipeline launchers (stencil_device.hpp: stencil5_stream_pipe_kernel),
+// compiled in their own translation units (stencil_pipe_f32.hip,
+// stencil_pipe_f64.hip: ~100 kernel instantiations) and called by the shape
+// dispatch in stencil.hip.
+#pragma once
+
+#include <algorithm>
+
+#include "mxs/core/error.hpp"
+#include "mxs/kernels/kernels.hpp"
+#include "mxs/runtime/hip_utils.hpp"
+#include "stencil_device.hpp"
+
+namespace mxs {
+namespace kernels {
+namespace detail {
+
+void note_dispatch(const char* kernel);  // stencil.hip: last_stencil_dispatch() record
+
+// fp64 depths the wide-lane pipeline takes (S0 = S/2, S1 = S - S0 <= 8 levels
+// per stage: the windows fit 2 waves/SIMD without spilling).
+constexpr int kPipeMinF64 = 9;
+
+// Two-stage pipeline. fp32 (S = 17..32), per-step form: the fetching stage
+// takes one level more than half, S0 = S/2 + 1 (at most 16) — measured 2-3%
+// ahead of the even split on 4 of 5 tile shapes (profiles/r02_deep/pipe2_*,
+// pipe20_*); sum form: the even split (S = 20: 10 + 10 beats 11 + 9 by 4-5% on
+// 32768^2, 16384 x 8192 and 8192^2, profiles/r02_sum). 6 input rows in flight
+// up to S = 28 (the fetch ring fits beside the windows at 2 waves/SIMD), 3
+// above. fp64 (S = 12 and 16, wide-lane body): even split, 3 rows in flight —
+// 6 + 6 is the fastest per-step fp64 form on every measured tile (8192^2 3.0
+// vs 2.2 T cells/s for the single-wave natural kernel, 16384^2 3.35 vs 2.5;
+// odd depths lose to the apron rounding: profiles/r02_f64), 8 + 8 the fastest
+// sum form (3.5 / 4.05). One 512-thread workgroup per CU: the occupancy API
+// decides, as for the single-wave balanced kernel.
+template <typename T, int S, bool SUM>
+constexpr int pipe_s0() {
+  if constexpr (sizeof(T) == 8 || SUM) return S / 2;
+  return S / 2 + 1 < 16 ? S / 2 + 1 : 16;
+}
+template <typename T, int S>
+constexpr int pipe_pf() {
+  return (sizeof(T) == 4 && S <= 28) ? 6 : 3;
+}
+template <typename T, int S, bool WRAP, bool SUM>
+constexpr auto pipe_kernel() {
+  return stencil5_stream_pipe_kernel<pipe_s0<T, S, SUM>(), S - pipe_s0<T, S, SUM>(), pipe_pf<T, S>(), WRAP, 0, T, SUM>;
+}
+
+template <typename T, int S, bool WRAP, bool SUM>
+int pipe_blocks() {
+  static int blocks = 0;
+  if (blocks == 0) {
+    int occ = 0;
+    MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, reinterpret_cast<const void*>(pipe_kernel<T, S, WRAP, SUM>()), 2 * kBlock, 0));
+    blocks = std::max(occ, 1) * device_cu_count();
+  }
+  return blocks;
+}
+
+template <typename T, int S, bool WRAP, bool SUM>
+index_t pipe_share(index_t x0, index_t x1, index_t y0, index_t y1) {
+  constexpr int OW = StripShape<T, S, true>::OW;
+  const index_t groups = ((x1 - x0 + OW - 1) / OW + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int blocks = pipe_blocks<T, S, WRAP, SUM>();
+  return (groups * (y1 - y0) + blocks - 1) / blocks;
+}
+
+template <typename T, int S, bool WRAP, bool SUM>
+void launch_pipe_impl(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
+                 T sc, hipStream_t s) {
+  const index_t share = pipe_share<T, S, WRAP, SUM>(x0, x1, y0, y1);
+  MXS_CHECK(std::min(share, y1 - y0) * g.pitch * index_t(sizeof(T)) < (index_t(1) << 31),
+            "stencil5_tb: a pipeline chunk must stay under 2 GiB (buffer-descriptor stores)");
+  pipe_kernel<T, S, WRAP, SUM>()<<<pipe_blocks<T, S, WRAP, SUM>(), 2 * kBlock, 0, s>>>(
+      in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, SUM ? sc : c0, c1);
+  note_dispatch(SUM ? "stream_pipe_sum" : "stream_pipe");
+}
+
+// Whether the fp64 wide-lane pipeline can take [x0, x1) x [y0, y1) at depth S:
+// whole 4-cell lane vectors (x0, x1 and, wrapping, the width multiples of 4),
+// the apron inside the row padding, and a chunk under 2 GiB.
+template <typename T, int S, bool WRAP>
+bool wide_pipe_ok_impl(const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1) {
+  constexpr int SA = StripShape<T, S, true>::SA;
+  if (x0 % 4 != 0 || x1 % 4 != 0) return false;
+  if (WRAP && g.width % 4 != 0) return false;
+  const index_t lead = g.x_origin + g.halo_x;
+  if (!WRAP && (lead < SA || g.pitch < lead + (g.width + 3) / 4 * 4 + SA)) return false;
+  return std::min(pipe_share<T, S, WRAP, false>(x0, x1, y0, y1), y1 - y0) * g.pitch * index_t(sizeof(T)) <
+         (index_t(1) << 31);
+}
+
+
+// Explicitly instantiated in the pipeline TUs.
+template <typename T, int S, bool WRAP, bool SUM>
+void launch_pipe(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
+                 T sc, hipStream_t s);
+template <typename T, int S, bool WRAP>
+bool wide_pipe_ok(const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1);
+
+}  // namespace detail
+}  // namespace kernels
+}  // namespace mxs

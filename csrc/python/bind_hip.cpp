@@ -160,10 +160,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("variant") = "auto");
   m.def(
       "auto_time_block",
-      [](index_t w, index_t h, const std::string& dt) {
-        return kernels::auto_time_block(w, h, parse_dtype(dt) == DType::F32 ? 4 : 8);
+      [](index_t w, index_t h, const std::string& dt, bool sum_form) {
+        return kernels::auto_time_block(w, h, parse_dtype(dt) == DType::F32 ? 4 : 8, sum_form);
       },
-      py::arg("width"), py::arg("height"), py::arg("dtype") = "f32",
+      py::arg("width"), py::arg("height"), py::arg("dtype") = "f32", py::arg("sum_form") = true,
       "measured default Jacobi steps per pass / halo exchange for a tile");
   m.attr("MAX_TIME_BLOCK") = kernels::kMaxTimeBlock;
   m.attr("MAX_TIME_BLOCK_DEEP") = kernels::kMaxTimeBlockDeep;
@@ -175,8 +175,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
       "stencil5_tb",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0,
          index_t y1, double c0, double c1, bool wrap, const std::string& dt, std::uintptr_t s,
-         const std::string& variant) {
-        kernels::Stencil5Coeffs c{c0, c1};
+         const std::string& variant, bool sum_form) {
+        kernels::Stencil5Coeffs c{c0, c1, sum_form};
         const kernels::StencilVariant v = parse_variant(variant);
         if (parse_dtype(dt) == DType::F32)
           kernels::stencil5_tb<float>(ptr<float>(in), ptr<float>(out), g, steps, x0, x1, y0, y1, c, wrap, strm(s), v);
@@ -186,7 +186,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
       },
       py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("steps"), py::arg("x0"), py::arg("x1"), py::arg("y0"),
       py::arg("y1"), py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2, py::arg("wrap") = false,
-      py::arg("dtype") = "f32", py::arg("stream") = 0, py::arg("variant") = "auto");
+      py::arg("dtype") = "f32", py::arg("stream") = 0, py::arg("variant") = "auto", py::arg("sum_form") = true,
+      "S Jacobi steps over [x0, x1) x [y0, y1); sum_form: allow the sum form when c_center == c_neighbor");
   m.def(
       "stencil5_rect",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
@@ -321,7 +322,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        const RcclComm* comm, const std::string& dt, HaloBackend backend, bool overlap,
                        bool use_graph, bool loopback_self, StencilKind kind, double c0, double c1, int box_radius,
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
-                       py::object bootstrap, int graph_supersteps) {
+                       py::object bootstrap, int graph_supersteps, bool sum_form) {
              SolverConfig cfg;
              cfg.bootstrap = wrap_allgather(bootstrap);
              cfg.graph_supersteps = graph_supersteps;
@@ -332,7 +333,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
              cfg.fuse_periodic_self = fuse_periodic;
              cfg.time_block = time_block;
              cfg.kind = kind;
-             cfg.coeffs = {c0, c1};
+             cfg.coeffs = {c0, c1, sum_form};
              cfg.variant = parse_variant(variant);
              if (kind == StencilKind::Box) cfg.box = make_box(box_radius, box_w);
              auto h = std::make_unique<SolverHandle>();
@@ -350,7 +351,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("kind") = StencilKind::Jacobi5, py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2,
            py::arg("box_radius") = 1, py::arg("box_weights") = std::vector<float>{}, py::arg("variant") = "auto",
            py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
-           py::arg("graph_supersteps") = 0, py::keep_alive<1, 7>())
+           py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::keep_alive<1, 7>())
       .def("step", [](SolverHandle& h) { h.visit([](auto& s) { s.step(); }); })
       .def("graph_supersteps", [](SolverHandle& h) { return h.visit([](auto& s) { return s.graph_supersteps(); }); })
       .def(

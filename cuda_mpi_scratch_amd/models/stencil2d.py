@@ -50,6 +50,11 @@ class StencilConfig:
     box_weights: list = field(default_factory=list)
     c_center: float = 0.2
     c_neighbor: float = 0.2
+    # c_center == c_neighbor: let the time-blocked GPU kernels run the sum form
+    # (plain 5-point sums per level, c^S applied once per pass: ~20% faster,
+    # equal to the per-step evaluation up to a few ulp). False: per-step
+    # evaluation, bitwise equal to S single steps and to the CPU paths.
+    sum_form: bool = True
     backend: str = "auto"            # auto | rccl | ipc | local | torch
     overlap: bool | None = None      # None = auto (on only for time_block 1 on unshared GPUs)
     graph: bool = True
@@ -59,7 +64,8 @@ class StencilConfig:
     # Jacobi iterations per halo exchange and per temporally blocked pass on GPU
     # (wave-streaming kernels); the ghost ring is made this deep. 1 = one
     # exchange per iteration; 0 = the measured optimum for the tile
-    # (kernels::auto_time_block: fp32 20 on the two-stage pipeline, fp64 12/16,
+    # (kernels::auto_time_block: fp32 20 on the two-stage pipeline, fp64 16 in
+    # the sum form, else 12;
     # docs/PERF.md). Up to 32 for fp32 without overlap, else capped at 16.
     time_block: int = 0
     seed: int = 1234
@@ -90,8 +96,9 @@ class Stencil2D:
         # exchange-only run (its dumps show a stencil_width/2 ghost ring).
         # A ghost ring deeper than a neighbour's tile would need cells two tiles away.
         tb = cfg.time_block
+        self.sum_form = bool(cfg.sum_form and cfg.c_center == cfg.c_neighbor)
         if tb <= 0 and dev.type == "cuda":
-            tb = hip().auto_time_block(d.width, d.height, cfg.dtype)
+            tb = hip().auto_time_block(d.width, d.height, cfg.dtype, self.sum_form)
         # A physical (non-periodic) edge holds fixed boundary values that the
         # S-step kernels would advance as cells: time blocking needs every edge
         # to be a neighbour's (the native solver enforces the same rule).
@@ -145,7 +152,7 @@ class Stencil2D:
             self.solver = H.StencilSolver(d.topo, d.rank, self.geom, self.a.data_ptr(), self.b.data_ptr(), self.comm,
                                           cfg.dtype, be, overlap, cfg.graph, cfg.loopback, kind, cfg.c_center,
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
-                                          self.time_block, boot, cfg.graph_supersteps)
+                                          self.time_block, boot, cfg.graph_supersteps, self.sum_form)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()

@@ -44,6 +44,11 @@ def _frozen_edge_reference(full, steps, c0=0.2, c1=0.2):
     return u
 
 
+def _expect(kernel, sum_form):
+    """Dispatch record: the fast bodies name their sum form (c_center == c_neighbor)."""
+    return kernel + "_sum" if sum_form and kernel in ("stream_pipe", "stream_balanced_rot") else kernel
+
+
 @pytest.mark.parametrize("w,h,steps,dtype,kernel", [
     (8192, 8192, 24, torch.float32, "stream_pipe"),           # BASELINE config 2 (1 GPU), auto S: two-stage pipeline
     (8192, 8192, 20, torch.float32, "stream_pipe"),           # the driver's 20-step window in one pass
@@ -55,11 +60,13 @@ def _frozen_edge_reference(full, steps, c0=0.2, c1=0.2):
     (16384, 4096, 16, torch.float32, "stream_balanced_rot"),  # wide tile, deepest block
     (4096, 4096, 12, torch.float64, "stream_pipe"),           # fp64 default S: wide-lane pipeline 6 + 6
     (2048, 1024, 16, torch.float64, "stream_pipe"),           # fp64 8 + 8
+    (2048, 1024, 15, torch.float64, "stream_pipe"),           # fp64 7 + 8 (near-equal splits of long runs)
     (300, 200, 12, torch.float64, "stream_pipe"),             # fp64, narrower than one strip group
     (4094, 4096, 12, torch.float64, "stream_balanced"),       # width % 4 != 0: natural fp64 layout
     (8192, 8192, 8, torch.float64, "stream_balanced"),
 ])
-def test_balanced_wrap_matches_periodic_reference(gpu, w, h, steps, dtype, kernel):
+@pytest.mark.parametrize("sum_form", [True, False])
+def test_balanced_wrap_matches_periodic_reference(gpu, w, h, steps, dtype, kernel, sum_form):
     g = core().TileGeom.aligned(w, h, 1, 1, torch.tensor([], dtype=dtype).element_size())
     gen = torch.Generator(device=gpu).manual_seed(w + h + steps)
     u = torch.rand(h, w, generator=gen, device=gpu, dtype=torch.float64).to(dtype)
@@ -67,8 +74,8 @@ def test_balanced_wrap_matches_periodic_reference(gpu, w, h, steps, dtype, kerne
     _core(src, g, w, h).copy_(u)
     dst = torch.zeros_like(src)
     hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, 0, w, 0, h, 0.2, 0.2, True, dtype_name(src),
-                      torch.cuda.current_stream().cuda_stream, "auto")
-    assert hip().last_stencil_dispatch() == kernel
+                      torch.cuda.current_stream().cuda_stream, "auto", sum_form)
+    assert hip().last_stencil_dispatch() == _expect(kernel, sum_form)
     torch.cuda.synchronize()
     ref = jacobi_reference_global(u, steps)
     tol = 2e-6 if dtype == torch.float32 else 1e-14
@@ -90,7 +97,8 @@ def test_balanced_wrap_matches_periodic_reference(gpu, w, h, steps, dtype, kerne
     (4096, 2048, 16, (8, 4088, 16, 2032), torch.float64, "stream_pipe"),
     (4094, 4096, 12, None, torch.float64, "stream_balanced"),  # ragged: natural fp64 layout
 ])
-def test_balanced_ghost_ring_matches_reference(gpu, w, h, steps, rect, dtype, kernel):
+@pytest.mark.parametrize("sum_form", [True, False])
+def test_balanced_ghost_ring_matches_reference(gpu, w, h, steps, rect, dtype, kernel, sum_form):
     esz = torch.tensor([], dtype=dtype).element_size()
     g = core().TileGeom.aligned(w, h, steps, steps, esz)
     gen = torch.Generator(device=gpu).manual_seed(steps * 7 + w)
@@ -100,8 +108,8 @@ def test_balanced_ghost_ring_matches_reference(gpu, w, h, steps, rect, dtype, ke
     dst = torch.full_like(src, -3.0)
     x0, x1, y0, y1 = rect or (0, w, 0, h)
     hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, x0, x1, y0, y1, 0.2, 0.2, False, dtype_name(src),
-                      torch.cuda.current_stream().cuda_stream, "auto")
-    assert hip().last_stencil_dispatch() == kernel
+                      torch.cuda.current_stream().cuda_stream, "auto", sum_form)
+    assert hip().last_stencil_dispatch() == _expect(kernel, sum_form)
     torch.cuda.synchronize()
     got = _core(dst, g, w, h)
     ref = _frozen_edge_reference(full, steps)[steps:steps + h, steps:steps + w]
@@ -132,11 +140,10 @@ def test_solver_caps_deep_blocks_where_the_pipeline_cannot_run(gpu):
 
 @pytest.mark.parametrize("dtype,block", [("f32", 20), ("f64", 12)])
 def test_solver_blocked_run_bitwise_equals_single_steps(gpu, dtype, block):
-    """run(20) at the auto time block (8192^2: fp32 S = 20 -> one 20-step
-    pipeline pass; fp64 S = 12 -> two super-steps of 10) equals 20 one-step
-    iterations bit for bit, and prepare() changes nothing. (fp64 S = 12 runs
-    the wide-lane pipeline.)"""
-    kw = dict(global_width=8192, global_height=8192, dims="1x1", dtype=dtype, seed=99)
+    """Per-step form: run(20) at the auto time block (8192^2: fp32 S = 20 -> one
+    20-step pipeline pass; fp64 S = 12 -> two super-steps of 10) equals 20
+    one-step iterations bit for bit, and prepare() changes nothing."""
+    kw = dict(global_width=8192, global_height=8192, dims="1x1", dtype=dtype, seed=99, sum_form=False)
     blocked = Stencil2D(StencilConfig(**kw))
     assert blocked.time_block == block
     blocked.prepare(20)
@@ -154,7 +161,7 @@ def test_solver_odd_splits_bitwise(gpu):
     """Near-equal splits of awkward counts at the fp32 default S = 20 (17 in one
     pipeline pass, 33 = 17 + 16: pipeline + single-wave kernel, then 1 and 12)
     and graphs reused across calls stay exact."""
-    kw = dict(global_width=2048, global_height=1024, dims="1x1", dtype="f32", seed=5)
+    kw = dict(global_width=2048, global_height=1024, dims="1x1", dtype="f32", seed=5, sum_form=False)
     a = Stencil2D(StencilConfig(**kw))
     for n in (17, 33, 1, 12):
         a.run(n)
@@ -181,10 +188,26 @@ def test_non_periodic_runs_single_step_and_keeps_boundary(gpu):
     assert torch.equal(st.full_view()[0], full0[0]), "a physical boundary row changed"
 
 
+@pytest.mark.parametrize("dtype,block,tol", [("f32", 20, 2e-6), ("f64", 16, 1e-14)])
+def test_solver_sum_form_matches_per_step(gpu, dtype, block, tol):
+    """Default (sum form, c_center == c_neighbor): two passes at the auto block
+    agree with as many single steps to a few ulp, on the sum-form pipeline."""
+    kw = dict(global_width=4096, global_height=2048, dims="1x1", dtype=dtype, seed=12)
+    fast = Stencil2D(StencilConfig(**kw))
+    assert fast.time_block == block and fast.sum_form
+    fast.run(2 * block)
+    fast.synchronize()
+    assert hip().last_stencil_dispatch() == "stream_pipe_sum"
+    single = Stencil2D(StencilConfig(time_block=1, **kw))
+    single.run(2 * block)
+    single.synchronize()
+    assert (fast.core_view().double() - single.core_view().double()).abs().max().item() <= tol
+
+
 def test_headline_rate_floor(gpu):
     """Regression floor near the measured rate: 32768^2 fp32, a 20-step window
-    after prepare() (the driver's --steps 20 --warmup 5): one 20-step pipeline
-    pass. Tuner: 7.9 T cells/s."""
+    after prepare() (the driver's --steps 20 --warmup 5): one 20-step sum-form
+    pipeline pass. Tuner: 9.96 T cells/s (per-step form 8.27)."""
     st = Stencil2D(StencilConfig(global_width=32768, global_height=32768, dims="1x1", dtype="f32"))
     st.run(5)
     st.prepare(20)
@@ -193,24 +216,25 @@ def test_headline_rate_floor(gpu):
     st.run(20)
     st.synchronize()
     rate = st.cells_per_step * 20 / (time.perf_counter() - t0) / 1e9
-    assert hip().last_stencil_dispatch() == "stream_pipe"
-    assert rate > 6000, f"{rate:.0f} Gcells/s"
+    assert hip().last_stencil_dispatch() == "stream_pipe_sum"
+    assert rate > 7500, f"{rate:.0f} Gcells/s"
 
 
 def test_fp64_rate_floor(gpu):
-    """fp64 (the reference's element type) at 8192^2, auto S = 12: the wide-lane
-    two-stage pipeline. Tuner: 3.0 T cells/s (natural layout: 2.2)."""
+    """fp64 (the reference's element type) at 8192^2, auto S = 16: the wide-lane
+    two-stage pipeline in the sum form. Tuner: 3.5 T cells/s (per-step 6 + 6:
+    3.0; natural layout: 2.2)."""
     st = Stencil2D(StencilConfig(global_width=8192, global_height=8192, dims="1x1", dtype="f64"))
-    assert st.time_block == 12
-    st.run(12)
+    assert st.time_block == 16
+    st.run(16)
     st.prepare(240)
     st.synchronize()
     t0 = time.perf_counter()
     st.run(240)
     st.synchronize()
     rate = st.cells_per_step * 240 / (time.perf_counter() - t0) / 1e9
-    assert hip().last_stencil_dispatch() == "stream_pipe"
-    assert rate > 2500, f"{rate:.0f} Gcells/s"
+    assert hip().last_stencil_dispatch() == "stream_pipe_sum"
+    assert rate > 2900, f"{rate:.0f} Gcells/s"
 
 
 @pytest.mark.parametrize("backend,loopback", [("local", False), ("rccl", True)])

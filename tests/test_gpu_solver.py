@@ -89,11 +89,14 @@ def _multi_step_reference(full, steps, c0=0.2, c1=0.2):
     return u
 
 
+@pytest.mark.parametrize("sum_form", [False, True])
 @pytest.mark.parametrize("variant", ["auto", "lds"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 @pytest.mark.parametrize("steps", [1, 2, 3, 4, 5, 8, 12, 16])
 @pytest.mark.parametrize("shape", [(300, 70), (129, 33), (1024, 96)])
-def test_stencil5_tb_kernel_matches_steps(gpu, dtype, steps, shape, variant):
+def test_stencil5_tb_kernel_matches_steps(gpu, dtype, steps, shape, variant, sum_form):
+    """Per-step form (sum_form=False): the fma sequence of S single steps, to
+    the reference's own rounding. Sum form (c_center == c_neighbor): a few ulp."""
     from cuda_mpi_scratch_amd import core, hip
     from cuda_mpi_scratch_amd.ops.stencil import dtype_name
 
@@ -107,11 +110,14 @@ def test_stencil5_tb_kernel_matches_steps(gpu, dtype, steps, shape, variant):
     src = host.to(gpu)
     dst = torch.full_like(src, -3.0)
     hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, 0, w, 0, h, 0.2, 0.2, False, dtype_name(src),
-                      torch.cuda.current_stream().cuda_stream, variant)
+                      torch.cuda.current_stream().cuda_stream, variant, sum_form)
     torch.cuda.synchronize()
     got = dst.cpu().view(g.total_height(), g.pitch)[g.halo_y:g.halo_y + h, g.x_origin + g.halo_x:g.x_origin + g.halo_x + w]
     ref = _multi_step_reference(full, steps)[steps:steps + h, steps:steps + w]
-    tol = 2e-7 if dtype == torch.float32 else 1e-15
+    if sum_form:
+        tol = 1.5e-6 if dtype == torch.float32 else 1e-14
+    else:
+        tol = 2e-7 if dtype == torch.float32 else 1e-15
     assert torch.allclose(got.double(), ref.double(), rtol=tol, atol=tol)
 
 
