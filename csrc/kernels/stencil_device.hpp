@@ -590,18 +590,20 @@ template <>
 __device__ __forceinline__ float lane_shift<float, kDppWaveShl1>(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), kDppWaveShl1, 0xf, 0xf, true));
 }
+// 64-bit DPP takes no wave shifts: two dword moves. bound_ctrl zero-fills the
+// shifted-in lane (0.0), so no zeroed `old` register (one v_mov each) is needed.
 template <>
 __device__ __forceinline__ double lane_shift<double, kDppWaveShr1>(double v) {
   const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, int(b & 0xffffffff), kDppWaveShr1, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), kDppWaveShr1, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(int(b & 0xffffffff), kDppWaveShr1, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(int(b >> 32), kDppWaveShr1, 0xf, 0xf, true);
   return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
 template <>
 __device__ __forceinline__ double lane_shift<double, kDppWaveShl1>(double v) {
   const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, int(b & 0xffffffff), kDppWaveShl1, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, int(b >> 32), kDppWaveShl1, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_mov_dpp(int(b & 0xffffffff), kDppWaveShl1, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(int(b >> 32), kDppWaveShl1, 0xf, 0xf, true);
   return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
 }
 
@@ -718,12 +720,22 @@ struct BodyWideF64 {  // 4 consecutive fp64 cells per lane (jac_w4d)
 // step-by-step evaluation up to rounding (not bit for bit: different
 // association, one scale per pass instead of one per step); magnitudes grow
 // as 5^S inside a pass (|u| up to 3e38 / 5^S stays finite).
+// (a.x + b.y, a.y + b.x): one v_pk_add_f32 with the halves of src1 swapped by
+// op_sel. Written as asm so the swap is never materialised as a register pair
+// of its own (from a shufflevector the backend copies swapped pairs with
+// v_mov_b32: ~1 per level-row of the sum body, measured in the ISA). Plain
+// VALU, no hazard the compiler would have to know about.
+__device__ __forceinline__ f32x2 pk_add_swap(const f32x2& a, const f32x2& b) {
+  f32x2 r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0]" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
 __device__ __forceinline__ f32x4 sum_rot4f(const f32x4& up, const f32x4& mid, const f32x4& dn) {
   const f32x2 am = mid.xy, bm = mid.zw;  // (c1, c2), (c3, c0)
   const f32x2 ns_a = up.xy + dn.xy, ns_b = up.zw + dn.zw;
-  const f32x2 p = am + bm.yx;            // (c0 + c1, c2 + c3)
-  const f32x2 h_a = p + am.yx;           // (p01 + c2, p23 + c1) = h3(c1), h3(c2)
-  f32x2 h_b;                             // h3(c3) = p23 + c4, h3(c0) = p01 + c[-1]
+  const f32x2 p = pk_add_swap(am, bm);   // (c1 + c0, c2 + c3)
+  const f32x2 h_a = pk_add_swap(p, am);  // (p01 + c2, p23 + c1) = h3(c1), h3(c2)
+  f32x2 h_b;                             // h3(c3) = c4 + p23, h3(c0) = c[-1] + p01
   h_b.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bm.y), kDppWaveShl1, 0xf, 0xf, true)) + p.y;
   h_b.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bm.x), kDppWaveShr1, 0xf, 0xf, true)) + p.x;
   f32x4 o;
