@@ -19,6 +19,7 @@
 // Positional arguments keep the reference contract: [local width (= height) [stencil width]].
 // More options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
 // --iters N, --warmup N, --time-block S (default: measured per tile size and dtype), --no-overlap, --no-graph,
+// --no-direct-halo (IPC backend: pack -> put -> unpack instead of the device-initiated push),
 // --c-center C --c-neighbor C (default 0.2 / 0.2), --no-sum-form (keep the per-step evaluation in the
 // time-blocked kernels: bitwise equal to the CPU app; default: sum form when the coefficients are equal),
 // --loopback, --bind bunch|rrobin,
@@ -104,6 +105,9 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   SolverConfig cfg;
   cfg.backend = backend == "rccl" ? HaloBackend::Rccl : backend == "ipc" ? HaloBackend::Ipc : HaloBackend::Local;
   if (backend == "ipc") cfg.bootstrap = [](const std::string& b) { return mpi_allgather_bytes(MPI_COMM_WORLD, b); };
+  // IPC: device-initiated halo (each pass pushes its edge bands into the
+  // neighbours' tiles) unless --no-direct-halo asks for pack -> put -> unpack.
+  cfg.direct_halo = backend == "ipc" && !cli.flag("no-direct-halo");
   // Overlap (interior on a forked stream while the halo moves) defaults on only
   // for one-exchange-per-iteration runs: with temporal blocking the exchange is
   // ~5-8% of a super-step and the concurrent thin boundary strips cost more than

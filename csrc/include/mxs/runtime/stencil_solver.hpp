@@ -46,6 +46,7 @@
 #include <vector>
 
 #include "mxs/halo/exchange.hpp"
+#include "mxs/halo/ipc_direct.hpp"
 #include "mxs/kernels/kernels.hpp"
 #include "mxs/runtime/hip_utils.hpp"
 
@@ -75,6 +76,11 @@ struct SolverConfig {
   HostAllgather bootstrap;
   // Super-steps captured per hipGraph (0 = auto: ~1 ms of work per launch).
   int graph_supersteps = 0;
+  // HaloBackend::Ipc: device-initiated halo (halo/ipc_direct.hpp) — after each
+  // pass one launch copies the output tile's edge bands straight into the
+  // neighbours' ghost rings and publishes a ready counter; the next pass waits
+  // for the neighbours' counters. Replaces pack -> put -> wait -> unpack.
+  bool direct_halo = false;
 };
 
 template <typename T>
@@ -111,6 +117,7 @@ class StencilSolver {
   const std::string& graph_status() const { return graph_status_; }
   const HaloPlan& plan() const { return ex_->plan(); }
   bool fused_periodic() const { return fused_; }
+  bool direct_halo() const { return direct_ != nullptr; }
   bool overlapped() const { return cfg_.overlap; }
   int time_block() const { return block_; }
   int graph_supersteps() const { return chain_; }
@@ -150,6 +157,10 @@ class StencilSolver {
   T* nxt_;
   const RcclComm* comm_ = nullptr;  // watchdog waits (synchronize) when set
   std::unique_ptr<HaloExchanger<T>> ex_;
+  std::unique_ptr<IpcDirectHalo<T>> direct_;  // SolverConfig::direct_halo
+  // Direct halo: refresh the current tile's ghost ring from the neighbours
+  // (push of the current bands; the next pass waits for theirs).
+  void prime();
   Stream main_, side_;
   Event fork_, interior_;
   std::vector<std::unique_ptr<GraphSet>> graphs_;  // at most kMaxGraphSets sizes, oldest evicted

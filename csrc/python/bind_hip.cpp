@@ -322,10 +322,11 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        const RcclComm* comm, const std::string& dt, HaloBackend backend, bool overlap,
                        bool use_graph, bool loopback_self, StencilKind kind, double c0, double c1, int box_radius,
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
-                       py::object bootstrap, int graph_supersteps, bool sum_form) {
+                       py::object bootstrap, int graph_supersteps, bool sum_form, bool direct_halo) {
              SolverConfig cfg;
              cfg.bootstrap = wrap_allgather(bootstrap);
              cfg.graph_supersteps = graph_supersteps;
+             cfg.direct_halo = direct_halo;
              cfg.backend = backend;
              cfg.overlap = overlap;
              cfg.use_graph = use_graph;
@@ -351,8 +352,11 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("kind") = StencilKind::Jacobi5, py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2,
            py::arg("box_radius") = 1, py::arg("box_weights") = std::vector<float>{}, py::arg("variant") = "auto",
            py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
-           py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::keep_alive<1, 7>())
+           py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = false,
+           py::keep_alive<1, 7>())
       .def("step", [](SolverHandle& h) { h.visit([](auto& s) { s.step(); }); })
+      .def("direct_halo", [](SolverHandle& h) { return h.visit([](auto& s) { return s.direct_halo(); }); },
+           "whether halos are pushed tile-to-tile by the device (IPC backend, direct mode)")
       .def("graph_supersteps", [](SolverHandle& h) { return h.visit([](auto& s) { return s.graph_supersteps(); }); })
       .def(
           "run", [](SolverHandle& h, int n) { h.visit([n](auto& s) { s.run(n); }); }, py::arg("iters"),

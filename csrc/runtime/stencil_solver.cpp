@@ -51,6 +51,9 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   boot.allgather = cfg_.bootstrap;
   boot.timeout_s = comm_timeout() > 0 ? comm_timeout() : 60.0;
   ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm, &boot);
+  const bool all_self_nbrs = plan.sends.empty();
+  if (cfg_.direct_halo && cfg_.backend == HaloBackend::Ipc && cfg_.kind == StencilKind::Jacobi5 && !all_self_nbrs)
+    direct_ = std::make_unique<IpcDirectHalo<T>>(topo, rank, tile_, buf_a_, buf_b_, cfg_.bootstrap, boot.timeout_s);
   cfg_.bootstrap = nullptr;  // setup only; drop it (it may hold a Python callable)
   // Super-steps per graph launch: enough for ~1 ms of work per launch (the
   // launch gap is ~10 us), estimated at 5 T cell-iterations/s; at most 8.
@@ -96,6 +99,12 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
   if (fused_) {
     if (S == 1) kernels::stencil5_periodic<T>(cur, nxt, tile_, cfg_.coeffs, m);
     else kernels::stencil5_tb<T>(cur, nxt, tile_, S, 0, w, 0, h, cfg_.coeffs, true, m, cfg_.variant);
+    return;
+  }
+  if (direct_) {  // the neighbours pushed cur's ghost ring after their previous pass
+    direct_->wait(m);
+    update(cur, nxt, S, 0, w, 0, h, m);
+    direct_->push(nxt, m);
     return;
   }
   if (!cfg_.overlap) {
@@ -237,9 +246,19 @@ void StencilSolver<T>::run_group(int S, int count) {
   }
 }
 
+// Direct halo: every pass pushes its output bands, so the current tile's ghost
+// ring is fresh after any pass. Before the first pass of a call it may not be
+// (construction, a checkpoint load or a caller writing the field): push the
+// current bands once; the first pass waits for the neighbours' pushes.
+template <typename T>
+void StencilSolver<T>::prime() {
+  if (direct_) direct_->push(cur_, main_.get());
+}
+
 template <typename T>
 void StencilSolver<T>::run(int iters) {
   MXS_TRACE_RANGE("stencil.run");
+  if (iters > 0) prime();
   Group gr[2];
   split(iters, gr);
   for (const Group& g : gr) run_group(g.S, g.count);
@@ -248,6 +267,7 @@ void StencilSolver<T>::run(int iters) {
 template <typename T>
 void StencilSolver<T>::prepare(int iters) {
   MXS_TRACE_RANGE("stencil.prepare");
+  prime();
   Group gr[2];
   split(iters, gr);
   for (const Group& g : gr) {
@@ -267,6 +287,7 @@ void StencilSolver<T>::prepare(int iters) {
 template <typename T>
 void StencilSolver<T>::warm(int iters, int passes) {
   MXS_TRACE_RANGE("stencil.warm");
+  prime();
   Group gr[2];
   split(iters, gr);
   for (int p = 0; p < passes; ++p)
@@ -294,6 +315,7 @@ void StencilSolver<T>::synchronize() {
   main_.sync();
   side_.sync();
   ex_->check();  // IPC backend: device-side waits carry their own deadline
+  if (direct_) direct_->check();
 }
 
 template class StencilSolver<float>;

@@ -71,6 +71,10 @@ class StencilConfig:
     seed: int = 1234
     init: str = "random"             # random | rank
     graph_supersteps: int = 0        # super-steps per hipGraph launch (0 = auto, ~1 ms of work)
+    # IPC backend: device-initiated halo — each pass's output bands are pushed
+    # tile-to-tile into the neighbours' ghost rings (no pack / unpack launches).
+    # None = on whenever the backend is ipc.
+    direct_halo: bool | None = None
 
     @property
     def halo(self) -> int:
@@ -152,7 +156,8 @@ class Stencil2D:
             self.solver = H.StencilSolver(d.topo, d.rank, self.geom, self.a.data_ptr(), self.b.data_ptr(), self.comm,
                                           cfg.dtype, be, overlap, cfg.graph, cfg.loopback, kind, cfg.c_center,
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
-                                          self.time_block, boot, cfg.graph_supersteps, self.sum_form)
+                                          self.time_block, boot, cfg.graph_supersteps, self.sum_form,
+                                          backend == "ipc" and cfg.direct_halo is not False)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
@@ -294,6 +299,8 @@ class Stencil2D:
                if tb > 1 else "")
         if self.solver.fused_periodic():
             return "fused-periodic (1x1 self-exchange in the kernel addressing)" + blk
+        if self.solver.direct_halo():
+            return "ipc direct (device-initiated push of each pass's edge bands into the neighbours' tiles)" + blk
         return f"{self.backend}" + (" + overlap" if self.solver.overlapped() else "") + blk
 
     # ----------------------------------------------------------------- dump

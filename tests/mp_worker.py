@@ -84,9 +84,10 @@ def task_gpu_solver(args):
     cfg = StencilConfig(global_width=args["w"], global_height=args["h"], dims=args["dims"],
                         dtype=args.get("dtype", "f32"), seed=args.get("seed", 5), backend=args.get("backend", "auto"),
                         overlap=args.get("overlap", True), graph=args.get("graph", True),
-                        time_block=args.get("time_block", 12))
+                        time_block=args.get("time_block", 12), direct_halo=args.get("direct", None))
     st = Stencil2D(cfg, ctx)
-    st.run(args["iters"])
+    for n in args.get("runs", [args["iters"]]):
+        st.run(n)
     st.synchronize()
     g = st.gather_global()
     out = {"rank": ctx.rank, "backend": st.backend, "halo": st.halo_mode(), "graph": st.graph_status(),

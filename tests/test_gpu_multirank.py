@@ -37,3 +37,34 @@ def test_ipc_solver_f64_bitwise_vs_single_rank(gpu):
     one = run_ranks("gpu_solver", 1, dict(args, dims="1x1"), gpu=True)
     four = run_ranks("gpu_solver", 4, dict(args, dims="2x2"), gpu=True)
     assert torch.equal(torch.tensor(one[0]["grid"]), torch.tensor(four[0]["grid"]))
+
+
+@pytest.mark.parametrize("n,dims,dtype,time_block,runs", [
+    (2, "1x2", "f32", 20, [20, 20]),      # fp32 default S: two-stage pipeline, left/right pushes
+    (2, "2x1", "f32", 20, [7, 33]),       # up/down pushes, left/right self copies; odd splits
+    (4, "2x2", "f32", 12, [29]),          # corners through the diagonal neighbour
+    (6, "2x3", "f64", 16, [16, 16]),      # fp64 wide-lane pipeline
+    (4, "2x2", "f32", 5, [11]),           # bands of 5 columns: 4-byte push path
+    (2, "1x2", "f32", 1, [6]),            # one push per iteration
+])
+def test_ipc_direct_halo_matches_global_reference(gpu, n, dims, dtype, time_block, runs):
+    """Device-initiated halo (IPC backend, direct mode): each pass pushes its
+    edge bands into the neighbours' ghost rings; several run() calls re-prime."""
+    w, h, seed = 272, 216, 13
+    iters = sum(runs)
+    res = run_ranks("gpu_solver", n, {"w": w, "h": h, "dims": dims, "iters": iters, "runs": runs, "seed": seed,
+                                      "dtype": dtype, "time_block": time_block, "direct": True}, gpu=True)
+    assert all(r["backend"] == "ipc" and r["halo"].startswith("ipc direct") for r in res), res
+    got = torch.tensor(res[0]["grid"], dtype=torch.float64)
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed, dtype=torch.float64), iters)
+    assert (got - ref).abs().max().item() < (1e-5 if dtype == "f32" else 1e-12)
+
+
+def test_ipc_direct_halo_bitwise_vs_classic_exchange(gpu):
+    """The push and the pack -> put -> unpack exchange deliver the same ghost
+    cells: identical results, bit for bit (4 ranks, 2 x 2)."""
+    args = {"w": 264, "h": 200, "dims": "2x2", "iters": 40, "seed": 4, "time_block": 20, "overlap": False}
+    direct = run_ranks("gpu_solver", 4, dict(args, direct=True), gpu=True)
+    classic = run_ranks("gpu_solver", 4, dict(args, direct=False), gpu=True)
+    assert direct[0]["halo"].startswith("ipc direct") and not classic[0]["halo"].startswith("ipc direct")
+    assert torch.equal(torch.tensor(direct[0]["grid"]), torch.tensor(classic[0]["grid"]))
