@@ -6,6 +6,7 @@
 #include <chrono>
 #include <vector>
 
+#include "mxs/core/fault.hpp"
 #include "mxs/core/trace.hpp"
 #include "mxs/runtime/hip_utils.hpp"
 
@@ -81,6 +82,12 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
   st.bytes = bytes;
   MXS_CHECK(peer >= 0 && peer < comm.size(), "pingpong: bad peer " << peer);
   const bool ping = comm.rank() <= peer;
+  // Every wait on the transfer stream goes through the communication watchdog
+  // (--comm-timeout): a dead or hung peer fails the run instead of hanging it.
+  auto drain = [&](const char* what) {
+    if (peer != comm.rank() && comm_timeout() > 0) comm.wait(stream, what);
+    MXS_HIP_CHECK(hipStreamSynchronize(stream));
+  };
   // Deterministic payload (the reference filled host_data[i] = i, mpi-pingpong-gpu.cpp:44).
   std::vector<unsigned char> pattern(bytes);
   for (size_t i = 0; i < bytes; ++i) pattern[i] = static_cast<unsigned char>((i * 131u + 7u) % 251u);
@@ -89,7 +96,7 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
   MXS_HIP_CHECK(hipStreamSynchronize(stream));
 
   for (int i = 0; i < warmup; ++i) round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
-  MXS_HIP_CHECK(hipStreamSynchronize(stream));
+  drain("pingpong warm-up (RCCL)");
 
   std::vector<double> rtts;
   if (mode == PingPongMode::Blocking) {
@@ -97,7 +104,7 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
     for (int i = 0; i < reps; ++i) {
       const auto t0 = std::chrono::steady_clock::now();
       round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
-      MXS_HIP_CHECK(hipStreamSynchronize(stream));
+      drain("pingpong round trip (RCCL)");
       const auto t1 = std::chrono::steady_clock::now();
       rtts.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count());
     }
@@ -110,7 +117,7 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
       e0.record(stream);
       for (int i = 0; i < per; ++i) round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
       e1.record(stream);
-      e1.sync();
+      drain("pingpong batch (RCCL)");
       rtts.push_back(double(e1.since(e0)) * 1000.0 / per);
     }
     if (mode == PingPongMode::Overlap) {
@@ -123,7 +130,7 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
       t0.record(stream);
       for (int i = 0; i < per; ++i) round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
       t1.record(stream);
-      t1.sync();
+      drain("pingpong overlap, comm alone (RCCL)");
       st.comm_alone_us = t1.since(t0) * 1000.0;
       const int probe = 4096;
       t0.record(cs);
@@ -144,7 +151,7 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
       for (int i = 0; i < per; ++i) round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
       t1.record(stream);
       t2.record(cs);
-      t1.sync();
+      drain("pingpong overlap, comm + compute (RCCL)");
       t2.sync();
       st.overlapped_us = std::max(t1.since(t0), t2.since(t0)) * 1000.0;
     }
