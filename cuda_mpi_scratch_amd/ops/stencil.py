@@ -115,3 +115,23 @@ def jacobi_reference_global(u: torch.Tensor, iters: int, c_center=0.2, c_neighbo
         else:
             u = c_neighbor * sums + c_center * u
     return u
+
+
+def jacobi_sum_reference_global(u: torch.Tensor, steps: int, c: float = 0.2) -> torch.Tensor:
+    """One sum-form pass of `steps` levels on the periodic torus, in the exact
+    association of the GPU sum bodies (stencil_device.hpp sum_rot4f / sum_w4d):
+    v' = (n + s) + h3 with the horizontal 3-sum built from pair sums,
+    h3(x) = (u[x] + u[x+1]) + u[x-1] for even x, (u[x-1] + u[x]) + u[x+1] for odd
+    x, then one multiply by c^S — c first rounded to the element type as the
+    per-step coefficient is, the power taken in fp64, then rounded — so the
+    GPU's time-blocked sum-form pass must match it bit for bit (global x
+    parity: the kernels' 4-cell lane vectors start at multiples of 4)."""
+    v = u.clone()
+    even = (torch.arange(u.shape[1]) % 2 == 0).to(u.device)
+    for _ in range(steps):
+        n, s = torch.roll(v, 1, 0), torch.roll(v, -1, 0)
+        w, e = torch.roll(v, 1, 1), torch.roll(v, -1, 1)
+        h3 = torch.where(even, (v + e) + w, (w + v) + e)
+        v = (n + s) + h3
+    c_t = float(torch.tensor(c, dtype=u.dtype))
+    return v * torch.tensor(c_t ** steps, dtype=torch.float64).to(u.dtype)

@@ -188,6 +188,31 @@ def test_non_periodic_runs_single_step_and_keeps_boundary(gpu):
     assert torch.equal(st.full_view()[0], full0[0]), "a physical boundary row changed"
 
 
+@pytest.mark.parametrize("w,h,steps,dtype,kernel", [
+    (8192, 8192, 20, torch.float32, "stream_pipe_sum"),          # the default fp32 pass (10 + 10)
+    (4096, 2048, 32, torch.float32, "stream_pipe_sum"),
+    (8192, 8192, 12, torch.float32, "stream_balanced_rot_sum"),  # single-wave sum body
+    (4096, 2048, 16, torch.float64, "stream_pipe_sum"),          # the default fp64 pass (8 + 8)
+    (2048, 1024, 13, torch.float64, "stream_pipe_sum"),
+])
+def test_sum_form_bitwise_vs_cpu_sum_reference(gpu, w, h, steps, dtype, kernel):
+    """The sum-form kernels reproduce ops.jacobi_sum_reference_global (plain
+    pair-shared 5-point sums, one c^S scale) bit for bit."""
+    from cuda_mpi_scratch_amd.ops import jacobi_sum_reference_global
+
+    g = core().TileGeom.aligned(w, h, 1, 1, torch.tensor([], dtype=dtype).element_size())
+    gen = torch.Generator(device=gpu).manual_seed(w + steps)
+    u = torch.rand(h, w, generator=gen, device=gpu, dtype=torch.float64).to(dtype)
+    src = torch.zeros(g.alloc_elems(), dtype=dtype, device=gpu)
+    _core(src, g, w, h).copy_(u)
+    dst = torch.zeros_like(src)
+    hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, 0, w, 0, h, 0.2, 0.2, True, dtype_name(src),
+                      torch.cuda.current_stream().cuda_stream, "auto", True)
+    assert hip().last_stencil_dispatch() == kernel
+    torch.cuda.synchronize()
+    assert torch.equal(_core(dst, g, w, h), jacobi_sum_reference_global(u, steps))
+
+
 @pytest.mark.parametrize("dtype,block,tol", [("f32", 20, 2e-6), ("f64", 16, 1e-14)])
 def test_solver_sum_form_matches_per_step(gpu, dtype, block, tol):
     """Default (sum form, c_center == c_neighbor): two passes at the auto block
