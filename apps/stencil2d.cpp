@@ -115,6 +115,8 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   // cross-process waits plus the forked branch oversubscribe the GPU's queues and
   // get time-sliced (measured: 3-28 vs ~3000 Gcells/s).
   const bool shared_gpu = env.local_size() > dev.devices_used;
+  // Ranks sharing a GPU: each persistent stencil kernel takes its share of the chip.
+  kernels::set_gpu_share(shared_gpu ? std::max(1, env.local_size() / std::max(1, dev.devices_used)) : 1);
   cfg.overlap = cli.flag("overlap") || (!cli.flag("no-overlap") && !shared_gpu && time_block == 1);
   cfg.use_graph = !cli.flag("no-graph");
   cfg.loopback_self = loopback;

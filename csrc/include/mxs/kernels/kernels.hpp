@@ -117,6 +117,13 @@ template <typename T>
 void stencil5_rect(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0,
                    index_t y1, Stencil5Coeffs c, hipStream_t s);
 
+// Processes sharing this GPU (ranks of one node bound to the same device, the
+// IPC configuration). The persistent stencil kernels size their grid to the
+// resident capacity of the chip divided by this, so the kernels of all sharing
+// ranks are co-resident instead of queueing in rounds behind each other.
+void set_gpu_share(int processes);
+int gpu_share();
+
 // Kernel form chosen by the most recent stencil launcher on this host process:
 // "stream_pipe" (the two-stage pipeline: fp32 blocks > 16 steps, the one the
 // benchmarks time, and fp64 blocks of 12 / 16 on whole lane vectors), "stream_balanced_rot" (persistent single-wave fp32

@@ -168,7 +168,7 @@ int balanced_blocks() {
     MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     blocks = std::max(occ, 2) * std::max(cus, 1);
   }
-  return blocks;
+  return std::max(1, blocks / gpu_share());
 }
 
 // Wave-streaming kernels (stencil_device.hpp). Bulk rectangles: the balanced
@@ -336,6 +336,12 @@ void stencil_box(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1,
 }
 
 const char* last_stencil_dispatch() { return g_last_dispatch.load(std::memory_order_relaxed); }
+
+namespace {
+std::atomic<int> g_gpu_share{1};
+}
+void set_gpu_share(int processes) { g_gpu_share.store(std::max(1, processes), std::memory_order_relaxed); }
+int gpu_share() { return g_gpu_share.load(std::memory_order_relaxed); }
 namespace detail {
 void note_dispatch(const char* k) { note(k); }
 }  // namespace detail

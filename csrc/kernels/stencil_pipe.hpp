@@ -56,7 +56,7 @@ int pipe_blocks() {
         &occ, reinterpret_cast<const void*>(pipe_kernel<T, S, WRAP, SUM>()), 2 * kBlock, 0));
     blocks = std::max(occ, 1) * device_cu_count();
   }
-  return blocks;
+  return std::max(1, blocks / gpu_share());
 }
 
 template <typename T, int S, bool WRAP, bool SUM>

@@ -171,6 +171,9 @@ PYBIND11_MODULE(_mxs_hip, m) {
       "last_stencil_dispatch", [] { return std::string(kernels::last_stencil_dispatch()); },
       "kernel form chosen by the most recent stencil launcher (e.g. 'stream_balanced_rot')");
   m.def("device_cu_count", &device_cu_count, "compute units of the current HIP device");
+  m.def("set_gpu_share", &kernels::set_gpu_share, py::arg("processes"),
+        "processes sharing this GPU: persistent stencil kernels take 1/processes of the chip");
+  m.def("gpu_share", &kernels::gpu_share);
   m.def(
       "stencil5_tb",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0,

@@ -145,6 +145,9 @@ class Stencil2D:
         self._cur, self._nxt = self.a, self.b
         if backend in ("rccl", "local", "ipc"):
             H = hip()
+            # Ranks sharing this GPU: each persistent kernel takes its share of
+            # the chip, so all of them are resident at once.
+            H.set_gpu_share(max(1, local // max(1, torch.cuda.device_count())) if self.shared_gpu else 1)
             if backend == "rccl":
                 self.comm = self.ctx.native_comm()
             torch.cuda.synchronize()
