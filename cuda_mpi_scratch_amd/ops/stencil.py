@@ -98,15 +98,19 @@ def box_reference(src, dst, geom, x0, x1, y0, y1, weights) -> None:
 
 
 def jacobi_reference_global(u: torch.Tensor, iters: int, c_center=0.2, c_neighbor=0.2,
-                            periodic=True) -> torch.Tensor:
-    """Whole-grid reference (periodic torus) for validating decompositions."""
+                            periodic=True, boundary: float = 0.0) -> torch.Tensor:
+    """Whole-grid reference for validating decompositions: a periodic torus, or
+    (periodic=False) a grid whose outside ring holds the fixed value `boundary`
+    (the models' physical edges: a ghost ring initialised once, never exchanged)."""
     u = u.clone()
     for _ in range(iters):
         if periodic:
             n, s = torch.roll(u, 1, 0), torch.roll(u, -1, 0)
             w, e = torch.roll(u, 1, 1), torch.roll(u, -1, 1)
         else:
-            raise NotImplementedError("non-periodic global reference")
+            p = torch.nn.functional.pad(u[None, None], (1, 1, 1, 1), value=boundary)[0, 0]
+            n, s = p[:-2, 1:-1], p[2:, 1:-1]
+            w, e = p[1:-1, :-2], p[1:-1, 2:]
         sums = (n + s) + (w + e)
         if u.dtype == torch.float32:
             c1 = torch.tensor(c_neighbor, dtype=torch.float32).double()

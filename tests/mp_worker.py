@@ -32,7 +32,8 @@ def task_jacobi(args):
     ctx = init(backend="gloo", device="cpu")
     cfg = StencilConfig(global_width=args["w"], global_height=args["h"], dims=args["dims"],
                         dtype=args.get("dtype", "f32"), seed=args.get("seed", 5), kind=args.get("kind", "jacobi5"),
-                        box_weights=args.get("box_weights", []), stencil_width=args.get("stencil_width", 3))
+                        box_weights=args.get("box_weights", []), stencil_width=args.get("stencil_width", 3),
+                        periodic=args.get("periodic", True))
     st = Stencil2D(cfg, ctx, device="cpu")
     st.run(args["iters"])
     g = st.gather_global()

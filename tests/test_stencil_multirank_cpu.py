@@ -43,6 +43,18 @@ def test_decomposition_invariance_bitwise(dims, n):
     assert torch.equal(got, ref), (got - ref).abs().max()
 
 
+@pytest.mark.parametrize("dims,n", [("2x2", 4), ("1x3", 3), ("3x1", 3)])
+def test_non_periodic_decomposition_matches_fixed_boundary_reference(dims, n):
+    """Physical edges (non-periodic grid): the ghost ring outside the global
+    grid keeps its initial 0, so every decomposition equals the whole-grid
+    Jacobi with a fixed zero boundary, bit for bit."""
+    w, h, iters = 36, 30, 7
+    res = run_ranks("jacobi", n, {"w": w, "h": h, "dims": dims, "iters": iters, "seed": 8, "periodic": False})
+    got = torch.tensor(res[0]["grid"], dtype=torch.float64).float()
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, 8), iters, periodic=False)
+    assert torch.equal(got, ref), (got - ref).abs().max()
+
+
 def test_decomposition_invariance_box_f64():
     k = 5
     wts = [float(torch.tensor(1 / 25.0, dtype=torch.float32))] * (k * k)
