@@ -97,7 +97,16 @@ constexpr int kMaxTimeBlockDeep = 32;
 // below (the pass is VALU-bound beyond S ~ 8, so a deeper block only pays
 // where the chunk / strip aprons are small against the tile).
 inline int auto_time_block(index_t w, index_t h, int elem_bytes = 4, bool sum_form = true) {
-  if (elem_bytes == 4 && w >= 1024 && h >= 1024) return 20;
+  if (elem_bytes == 4 && w >= 1024 && h >= 1024) {
+    // The pipeline runs 4-strip groups of 256 - 2 * SA output columns: when
+    // the last group at S = 20 (216 columns per strip) is partial and S = 24
+    // (208) fills it, the idle strips cost more than the deeper block (8192^2,
+    // sum form: 38 strips in 10 groups at S = 20, 8.05 T cells/s; 40 at
+    // S = 24, 8.20; profiles/r02_sum).
+    auto strips = [&](int ow) { return (w + ow - 1) / ow; };
+    if (sum_form && strips(216) % 4 != 0 && strips(208) % 4 == 0) return 24;
+    return 20;
+  }
   if (elem_bytes == 8) return sum_form ? 16 : 12;
   return w * h >= (index_t(1) << 27) ? 16 : 12;
 }
