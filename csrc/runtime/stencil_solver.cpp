@@ -68,6 +68,14 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
 
 template <typename T>
 StencilSolver<T>::~StencilSolver() {
+  // Direct halo: the neighbours' last pushes write into our tiles; wait for
+  // them (device deadline) before the caller may free or reuse the buffers.
+  if (direct_) {
+    try {
+      direct_->wait(main_.get());
+    } catch (...) {
+    }
+  }
   (void)hipStreamSynchronize(main_.get());
   (void)hipStreamSynchronize(side_.get());
 }
@@ -312,6 +320,9 @@ void StencilSolver<T>::synchronize() {
   // With a remote peer and a watchdog timeout, wait by polling so a dead or
   // hung peer fails the job instead of blocking it.
   if (comm_ && comm_timeout() > 0) comm_->wait(main_.get(), "stencil halo exchange (RCCL)");
+  // Direct halo: also wait for the neighbours' pushes into our tiles, so the
+  // field (ghost ring included) is final and no peer still writes into it.
+  if (direct_) direct_->wait(main_.get());
   main_.sync();
   side_.sync();
   ex_->check();  // IPC backend: device-side waits carry their own deadline
