@@ -14,12 +14,17 @@ says so.
 
 One step = one full Jacobi iteration of the global grid: every core cell is
 updated every step. Halos are exchanged communication-avoiding style: an
-S-deep ghost ring (S = --time-block; default 16 for tiles of >= 2^27 cells,
-12 below, as measured) is exchanged once per super-step and the
-wave-streaming kernel runs the super-step's iterations in one pass over HBM;
-the result is bitwise identical to one 1-deep exchange + one sweep per step
+S-deep ghost ring (S = --time-block; default kernels::auto_time_block: 20 for
+fp32 tiles of >= 1024 x 1024, or 24 where it fills the last 4-strip group) is
+exchanged once per super-step and the two-stage wave pipeline runs the
+super-step's iterations in one pass over HBM. The 5-point weights are equal
+(0.2), so the kernel runs the sum form — S levels of unscaled 5-point sums,
+one scale by 0.2^S at the store — within a few ulp of one 1-deep exchange + one
+sweep per step and bitwise equal to its CPU model
+(ops/stencil.py:jacobi_sum_reference_global; tests/test_gpu_headline.py).
+`--no-sum-form` runs the per-step form, bitwise identical to the 1-deep loop
 (tests/test_gpu_solver.py). K steps run as ceil(K / S) near-equal super-steps
-(K = 20 -> 10 + 10).
+(K = 20 at S = 20 -> one pass).
 
 Timing: W untimed warm-up steps, then ``prepare(K)`` (graph capture + upload
 and one launch of every kernel shape the timed window uses, state unchanged)
@@ -169,7 +174,7 @@ def main(argv=None) -> int:
     p.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     p.add_argument("--variant", default="auto", choices=["auto", "roll", "lds"])
     p.add_argument("--time-block", type=int, default=0,
-                   help="Jacobi steps per halo exchange / kernel pass (0 = measured default per tile: 12 or 16)")
+                   help="Jacobi steps per halo exchange / kernel pass (0 = measured default per tile, kernels::auto_time_block: 20 or 24 for fp32)")
     p.add_argument("--no-sum-form", action="store_true",
                    help="per-step evaluation in the time-blocked kernels (bitwise equal to S single steps; "
                         "default: the sum form, c^S applied once per pass, for the equal default coefficients)")

@@ -6,10 +6,15 @@
 // S-deep halo (same bytes per iteration as S 1-deep exchanges, S x fewer
 // latency-bound messages) and then advances S iterations in one pass over HBM
 // (kernels::stencil5_tb: the wave-streaming kernel, ~S x less HBM traffic per
-// iteration). S = 1 is the classic one-exchange-per-iteration loop. Results are
-// bitwise identical for any S. run(K) splits K into ceil(K / S) near-equal
-// super-steps (K = 20, S = 16 -> 10 + 10, not 16 + a short HBM-bound 4), so a
-// short timed window costs the same per iteration as a long one.
+// iteration). S = 1 is the classic one-exchange-per-iteration loop. With the
+// per-step form (coeffs.sum_form = false, or center != neighbor) results are
+// bitwise identical for any S; the sum form (center == neighbor, the default)
+// sums S levels unscaled and applies c^S once, within a few ulp of the
+// per-step result and bitwise equal to ops/stencil.py's
+// jacobi_sum_reference_global. run(K) splits K into ceil(K / S) near-equal
+// super-steps (K = 20, S = 24 -> one 20, K = 30 -> 15 + 15, not 24 + a short
+// HBM-bound 6), so a short timed window costs the same per iteration as a
+// long one.
 //
 // Physical (non-periodic) edges: the S-step kernels advance the ghost ring as
 // ordinary cells at every intermediate level, which is exactly right for a
