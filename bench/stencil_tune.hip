@@ -374,6 +374,15 @@ int main(int argc, char** argv) {
     vs.push_back(pipe<10, 10, 6, false, 0, true>(in, out, g));
     vs.push_back(pipe<10, 10, 9, false, 0, true>(in, out, g));
     vs.push_back(pipe<12, 12, 6, false, 0, true>(in, out, g));
+  } else if (focus && std::string(focus) == "sum3") {  // shallower sum-form pipelines (narrower apron)
+    vs.push_back(pipe<10, 10, 6, true, 0, true>(in, out, g, tmp));
+    vs.push_back(pipe<8, 8, 6, true, 0, true>(in, out, g, tmp));
+    vs.push_back(pipe<8, 8, 9, true, 0, true>(in, out, g, tmp));
+    vs.push_back(pipe<9, 9, 6, true, 0, true>(in, out, g, tmp));
+    vs.push_back(pipe<9, 9, 9, true, 0, true>(in, out, g, tmp));
+    vs.push_back(pipe<10, 10, 6, false, 0, true>(in, out, g));
+    vs.push_back(pipe<8, 8, 6, false, 0, true>(in, out, g));
+    vs.push_back(pipe<9, 9, 6, false, 0, true>(in, out, g));
   } else if (focus && std::string(focus) == "deep") {  // time blocks past 16 (AGPR-backed window, 1 wave/SIMD)
     vs.push_back(balanced<16, 3, true, true>(in, out, g, 0, tmp));
     vs.push_back(balanced<10, 6, true, true>(in, out, g, 0, tmp));
