@@ -168,8 +168,9 @@ struct Copy2DBatch {
   int n = 0;
   Copy2D op[kMaxCopies];
 };
+// grid_x: workgroups per copy (0 = sized from the largest copy; tuning only).
 template <typename T>
-void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s);
+void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x = 0);
 
 // ---------------------------------------------------------------- dot (K2-K8)
 enum class DotReduce : int {

@@ -29,20 +29,37 @@ constexpr int kBlock = 256;
 // stride is added as (whole rows, remaining columns) with a carry. (A 64-bit
 // divide per element made the 16-deep halo pack of the 8-GPU tile, 3 MiB,
 // take 12-14 us per launch.)
-template <typename U, typename F>
-__device__ __forceinline__ void for_each_2d(index_t width, index_t height, F&& f) {
+//
+// kInFlight elements per thread are loaded before any is stored: a pack of the
+// 8-GPU tile's 20-deep halo gives each thread 2-3 vectors, and one load ->
+// store round trip per element serialised them (6 us per launch, of which
+// ~4 us memory latency; profiles/r02_tile).
+constexpr int kInFlight = 4;
+
+template <typename V, typename Src, typename Dst>
+__device__ __forceinline__ void copy_2d(index_t width, index_t height, Src&& src, Dst&& dst) {
   const index_t stride = index_t(gridDim.x) * blockDim.x;
   const index_t t = index_t(blockIdx.x) * blockDim.x + threadIdx.x;
   index_t y = t / width, x = t - y * width;
   const index_t dy = stride / width, dx = stride - dy * width;
-  for (; y < height;) {
-    f(x, y);
-    x += dx;
-    y += dy;
-    if (x >= width) {
-      x -= width;
-      ++y;
+  while (y < height) {
+    V v[kInFlight];
+    index_t xs[kInFlight], ys[kInFlight];
+#pragma unroll
+    for (int k = 0; k < kInFlight; ++k) {
+      xs[k] = x;
+      ys[k] = y;
+      if (y < height) v[k] = *src(x, y);
+      x += dx;
+      y += dy;
+      if (x >= width) {
+        x -= width;
+        ++y;
+      }
     }
+#pragma unroll
+    for (int k = 0; k < kInFlight; ++k)
+      if (ys[k] < height) *dst(xs[k], ys[k]) = v[k];
   }
 }
 
@@ -53,14 +70,7 @@ __global__ __launch_bounds__(kBlock) void copy2d_batch_kernel(T* __restrict__ s0
   // Wave-uniform selects (a runtime-indexed pointer array would go to scratch).
   const T* __restrict__ src = (op.src_slot == 0 ? s0 : (op.src_slot == 1 ? s1 : s2)) + op.src_off;
   T* __restrict__ dst = (op.dst_slot == 0 ? s0 : (op.dst_slot == 1 ? s1 : s2)) + op.dst_off;
-  const index_t n = op.width * op.height;
-  if (n <= 0) return;
-  const index_t stride = index_t(gridDim.x) * blockDim.x;
-  if (op.width == 1) {  // column segment: no division in the loop
-    for (index_t i = index_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
-      dst[i * op.dst_stride] = src[i * op.src_stride];
-    return;
-  }
+  if (op.width <= 0 || op.height <= 0) return;
   // 16-byte vectors when both sides allow it (the S-deep halos of the
   // temporally blocked solver: aligned core, widths multiples of 4 fp32).
   constexpr index_t N = 16 / sizeof(T);
@@ -68,20 +78,21 @@ __global__ __launch_bounds__(kBlock) void copy2d_batch_kernel(T* __restrict__ s0
   const bool vec = N > 1 && op.width % N == 0 && op.src_stride % N == 0 && op.dst_stride % N == 0 &&
                    (reinterpret_cast<uintptr_t>(src) % 16) == 0 && (reinterpret_cast<uintptr_t>(dst) % 16) == 0;
   if (vec) {
-    for_each_2d<V>(op.width / N, op.height, [&](index_t x, index_t y) {
-      *reinterpret_cast<V*>(dst + y * op.dst_stride + x * N) =
-          *reinterpret_cast<const V*>(src + y * op.src_stride + x * N);
-    });
+    copy_2d<V>(
+        op.width / N, op.height,
+        [&](index_t x, index_t y) { return reinterpret_cast<const V*>(src + y * op.src_stride + x * N); },
+        [&](index_t x, index_t y) { return reinterpret_cast<V*>(dst + y * op.dst_stride + x * N); });
     return;
   }
-  for_each_2d<T>(op.width, op.height,
-                 [&](index_t x, index_t y) { dst[y * op.dst_stride + x] = src[y * op.src_stride + x]; });
+  copy_2d<T>(
+      op.width, op.height, [&](index_t x, index_t y) { return src + y * op.src_stride + x; },
+      [&](index_t x, index_t y) { return dst + y * op.dst_stride + x; });
 }
 
 }  // namespace
 
 template <typename T>
-void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s) {
+void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x) {
   if (b.n <= 0) return;
   MXS_CHECK(b.n <= kMaxCopies, "copy2d_batch: too many copies " << b.n);
   index_t biggest = 0;
@@ -95,16 +106,16 @@ void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_
   constexpr index_t kVec = 16 / sizeof(T) > 0 ? 16 / sizeof(T) : 1;
   const index_t want = (biggest + kBlock * kVec - 1) / (kBlock * kVec);
   const index_t cap = std::max<index_t>(64, index_t(4) * device_cu_count() / b.n);
-  const int gx = int(std::min<index_t>(want, cap));
+  const int gx = grid_x > 0 ? grid_x : int(std::min<index_t>(want, cap));
   copy2d_batch_kernel<T><<<dim3(gx, b.n), kBlock, 0, s>>>(slot0, slot1, slot2, b);
   MXS_HIP_CHECK_LAUNCH();
 }
 
-template void copy2d_batch<float>(float*, float*, float*, const Copy2DBatch&, hipStream_t);
-template void copy2d_batch<double>(double*, double*, double*, const Copy2DBatch&, hipStream_t);
-template void copy2d_batch<int>(int*, int*, int*, const Copy2DBatch&, hipStream_t);
+template void copy2d_batch<float>(float*, float*, float*, const Copy2DBatch&, hipStream_t, int);
+template void copy2d_batch<double>(double*, double*, double*, const Copy2DBatch&, hipStream_t, int);
+template void copy2d_batch<int>(int*, int*, int*, const Copy2DBatch&, hipStream_t, int);
 template void copy2d_batch<unsigned char>(unsigned char*, unsigned char*, unsigned char*, const Copy2DBatch&,
-                                          hipStream_t);
+                                          hipStream_t, int);
 
 }  // namespace kernels
 }  // namespace mxs

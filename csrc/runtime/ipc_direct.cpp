@@ -18,6 +18,7 @@ namespace {
 using u64 = unsigned long long;
 constexpr u64 kBlobMagic = 0x4d58534950434432ull;  // "MXSIPCD2"
 constexpr int kBlock = 256;
+constexpr int kInFlight = 4;  // loads per thread issued before its stores
 
 // One band copy: our core band -> a neighbour's ghost band (element strides).
 struct PtrCopy {
@@ -70,15 +71,32 @@ __global__ __launch_bounds__(kBlock) void push_kernel(PushBatch b, int elem_byte
   const index_t t = index_t(blockIdx.x) * blockDim.x + threadIdx.x;
   index_t y = t / w, x = t - y * w;
   const index_t dy = stride / w, dx = stride - dy * w;
+  // kInFlight loads before the stores (see kernels/halo.hip: copy_2d).
   while (y < op.height) {
-    const index_t so = y * sstride + x * unit, d_o = y * dstride + x * unit;
-    if (vec) store_sys16(dst + d_o, *reinterpret_cast<const u32x4*>(src + so));
-    else store_sys4(dst + d_o, *reinterpret_cast<const unsigned*>(src + so));
-    x += dx;
-    y += dy;
-    if (x >= w) {
-      x -= w;
-      ++y;
+    u32x4 v[kInFlight];
+    index_t d_o[kInFlight];
+    bool ok[kInFlight];
+#pragma unroll
+    for (int k = 0; k < kInFlight; ++k) {
+      ok[k] = y < op.height;
+      const index_t so = y * sstride + x * unit;
+      d_o[k] = y * dstride + x * unit;
+      if (ok[k]) {
+        if (vec) v[k] = *reinterpret_cast<const u32x4*>(src + so);
+        else v[k].x = *reinterpret_cast<const unsigned*>(src + so);
+      }
+      x += dx;
+      y += dy;
+      if (x >= w) {
+        x -= w;
+        ++y;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kInFlight; ++k) {
+      if (!ok[k]) continue;
+      if (vec) store_sys16(dst + d_o[k], v[k]);
+      else store_sys4(dst + d_o[k], v[k].x);
     }
   }
 }
