@@ -1301,20 +1301,23 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 // wide-lane body (FastBody<T>). Needs x_end % 4 == 0 and a chunk under 2 GiB
 // (the output buffer descriptor).
 // PRIO (tuning): 1 raises the fetching stage's wave priority, 2 the storing stage's.
-template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float, bool SUM = false>
-__global__ __launch_bounds__(2 * kBlock) void stencil5_stream_pipe_kernel(
+// G: strips per workgroup (2G waves; the barriers of one block of rows span the
+// workgroup, so smaller groups decouple the strips of a CU).
+template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float, bool SUM = false,
+          int G = kWavesPerBlock>
+__global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
   using P = PipeShape<S0, S1, PF>;
   using B = typename FastBody<T, SUM>::type;
   constexpr int OW = StripShape<T, P::S, true>::OW;
-  __shared__ typename B::V ring[kWavesPerBlock * P::RING * kWaveSize];
+  __shared__ typename B::V ring[G * P::RING * kWaveSize];
   const index_t rows = y_end - y_begin;
   const index_t strips = (x_end - x_begin + OW - 1) / OW;
-  const index_t groups = (strips + kWavesPerBlock - 1) / kWavesPerBlock;
+  const index_t groups = (strips + G - 1) / G;
   const index_t total = groups * rows;
   const int wave = threadIdx.x / kWaveSize;
-  const int strip = wave % kWavesPerBlock, stage = wave / kWavesPerBlock;
+  const int strip = wave % G, stage = wave / G;
   if constexpr (PRIO == 1) {
     if (stage == 0) __builtin_amdgcn_s_setprio(1);
   } else if constexpr (PRIO == 2) {
@@ -1326,7 +1329,7 @@ __global__ __launch_bounds__(2 * kBlock) void stencil5_stream_pipe_kernel(
   while (a < b) {  // workgroup-uniform: all 8 waves take every chunk (barriers inside)
     const index_t grp = a / rows, r0 = a - grp * rows;
     const index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
-    const index_t xw = x_begin + (grp * kWavesPerBlock + strip) * OW;
+    const index_t xw = x_begin + (grp * G + strip) * OW;
     pipe_chunk<B, S0, S1, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1,
                                  ring + strip * P::RING * kWaveSize, stage);
     a += r1 - r0;
