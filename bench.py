@@ -43,7 +43,7 @@ Extras (not the headline number, BASELINE configs 2/3/5):
     single-pass device reduction + RCCL all-reduce of the partial (GB/s read);
   * N = 1: 8192^2 fp32 and fp64 single-GPU stencil rates;
   * N >= 2: GPU-GPU ping-pong between ranks 0 and 1, 8 B - 256 MiB, RCCL
-    blocking / async / overlap and device-initiated HIP IPC. Summary
+    blocking / async / overlap (device-initiated HIP IPC with --pingpong-ipc). Summary
     (latency at 8 B, GB/s at 1 MiB / 16 MiB / 256 MiB) in extras, the full
     sweep in gpurun_out/bench_pingpong_n<N>.json.
 """
@@ -116,13 +116,18 @@ def dot_extras(ctx, extras: dict, n_global: int) -> None:
     del dp
 
 
-def pingpong_extras(ctx, extras: dict, max_bytes: int) -> None:
-    """BASELINE metric 2 / config 3: ranks 0 <-> 1, 8 B - 256 MiB."""
+def pingpong_extras(ctx, extras: dict, max_bytes: int, with_ipc: bool = False) -> None:
+    """BASELINE metric 2 / config 3: ranks 0 <-> 1, 8 B - 256 MiB.
+
+    RCCL only by default: the headline line is printed after the extras, and a
+    fault in a transport that has never crossed GPUs in this tree (HIP IPC
+    between two devices; tested between processes sharing one) would take the
+    whole record with it. ``--pingpong-ipc`` adds the IPC sweep."""
     from cuda_mpi_scratch_amd.models.pingpong import PingPong
 
     sweep = []
-    plan = ((("rccl", ("blocking", "async", "overlap")), ("ipc", ("device",))) if torch.cuda.is_available()
-            else (("torch", ("blocking",)),))  # CPU rehearsal: gloo send/recv
+    gpu_plan = (("rccl", ("blocking", "async", "overlap")),) + ((("ipc", ("device",)),) if with_ipc else ())
+    plan = gpu_plan if torch.cuda.is_available() else (("torch", ("blocking",)),)  # CPU rehearsal: gloo send/recv
     for transport, modes in plan:
         try:
             sizes = [b for b in PINGPONG_SIZES if b <= max_bytes]
@@ -190,6 +195,8 @@ def main(argv=None) -> int:
                         "short window runs at sustained clocks (0 = off)")
     p.add_argument("--dot-n", type=int, default=2**30, help="global dot-product length (extras)")
     p.add_argument("--pingpong-max", type=int, default=256 << 20, help="largest ping-pong message (extras)")
+    p.add_argument("--pingpong-ipc", action="store_true",
+                   help="N >= 2 extras: also sweep the HIP IPC ping-pong transport (default: RCCL only)")
     p.add_argument("--comm-timeout", type=float, default=300.0,
                    help="seconds a halo / all-reduce wait may take before the run fails (0 = forever)")
     args = p.parse_args(argv)
@@ -258,7 +265,7 @@ def main(argv=None) -> int:
                 stencil_rate(ctx, 8192, 8192, "f64", 600, 48, args.clock_warmup_ms / 1e3, time_block=args.time_block,
                              sum_form=not args.no_sum_form), 2)
         else:
-            pingpong_extras(ctx, extras, args.pingpong_max)
+            pingpong_extras(ctx, extras, args.pingpong_max, args.pingpong_ipc)
         ctx.barrier()
 
     if ctx.is_root:
