@@ -105,6 +105,12 @@ inline int auto_time_block(index_t w, index_t h, int elem_bytes = 4, bool sum_fo
     // S = 24, 8.20; profiles/r02_sum).
     auto strips = [&](int ow) { return (w + ow - 1) / ow; };
     if (sum_form && strips(216) % 4 != 0 && strips(208) % 4 == 0) return 24;
+    // Tiles of >= 2^30 cells (chunks of ~4800 rows, warm-up negligible): the
+    // deeper block relieves HBM (4.0 -> 3.4 TB/s) and wins, 32768^2 sum form
+    // 10.1-10.5 T cells/s at S = 24 vs 10.0 at 20 in three tuner runs; at
+    // 32768 x 16384 and below S = 20 stays ahead (profiles/r02_sum/s24_*). A
+    // 20-step run is still one S = 20 pass (run(K) splits K near-equally).
+    if (sum_form && w * h >= (index_t(1) << 30)) return 24;
     return 20;
   }
   if (elem_bytes == 8) return sum_form ? 16 : 12;

@@ -31,6 +31,7 @@ __device__ __forceinline__ T jac(T c, T n, T s, T w, T e, T c0, T c1) {
 }
 
 constexpr int kWavesPerBlock = 4;
+constexpr int kNumXcds = 8;  // MI355X: workgroups are dealt round-robin over 8 XCDs
 constexpr int kBlock = kWavesPerBlock * kWaveSize;
 
 // ------------------------------------------------------------- RegisterRoll
@@ -1303,8 +1304,11 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 // PRIO (tuning): 1 raises the fetching stage's wave priority, 2 the storing stage's.
 // G: strips per workgroup (2G waves; the barriers of one block of rows span the
 // workgroup, so smaller groups decouple the strips of a CU).
+// XM (tuning): XCD-major share order — the workgroups one XCD runs (blockIdx
+// congruent mod 8) take consecutive shares, so vertically adjacent chunks, which
+// read the same 2S apron rows, share that XCD's L2.
 template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float, bool SUM = false,
-          int G = kWavesPerBlock>
+          int G = kWavesPerBlock, bool XM = false>
 __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
@@ -1323,7 +1327,11 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
   } else if constexpr (PRIO == 2) {
     if (stage == 1) __builtin_amdgcn_s_setprio(1);
   }
-  index_t a = index_t(blockIdx.x) * share;
+  index_t slot = blockIdx.x;
+  if constexpr (XM) {
+    if (gridDim.x % kNumXcds == 0) slot = (blockIdx.x % kNumXcds) * (gridDim.x / kNumXcds) + blockIdx.x / kNumXcds;
+  }
+  index_t a = slot * share;
   const index_t b = a + share < total ? a + share : total;
 #pragma unroll 1
   while (a < b) {  // workgroup-uniform: all 8 waves take every chunk (barriers inside)

@@ -233,8 +233,10 @@ def test_solver_sum_form_matches_per_step(gpu, dtype, block, tol):
 def test_headline_rate_floor(gpu):
     """Regression floor near the measured rate: 32768^2 fp32, a 20-step window
     after prepare() (the driver's --steps 20 --warmup 5): one 20-step sum-form
-    pipeline pass. Tuner: 9.96 T cells/s (per-step form 8.27)."""
+    pipeline pass (the tile's block is 24, which a 20-step run splits into one
+    pass of 20). Tuner: 9.96 T cells/s (per-step form 8.27)."""
     st = Stencil2D(StencilConfig(global_width=32768, global_height=32768, dims="1x1", dtype="f32"))
+    assert st.time_block == 24
     st.run(5)
     st.prepare(20)
     st.synchronize()
