@@ -226,6 +226,38 @@ Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullpt
   return v;
 }
 
+// Three-stage wave pipeline (S = S0 + S1 + S2 levels; 768-thread workgroups).
+template <int S0, int S1, int S2, int PF, bool WRAP = true, bool SUM = true>
+Variant pipe3(const float* in, float* out, const TileGeom& g, float* tmp = nullptr) {
+  int per_cu = 0, cus = 0;
+  constexpr int threads = 3 * 4 * kWaveSize;
+  MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu, reinterpret_cast<const void*>(stencil5_stream_pipe3_kernel<S0, S1, S2, PF, WRAP, float, SUM>),
+      threads, 0));
+  MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const int blocks = std::max(1, per_cu * cus);
+  char buf[128];
+  std::snprintf(buf, sizeof(buf), "pipe3_s%d+%d+%d_pf%d_b%d%s%s", S0, S1, S2, PF, per_cu, WRAP ? "_wrap" : "",
+                SUM ? "_sum" : "");
+  constexpr int S = S0 + S1 + S2;
+  const float c0 = SUM ? float(std::pow(0.2, S)) : 0.2f;
+  auto mk = [=](const float* I, float* O) {
+    return [=](hipStream_t s) {
+      constexpr int OW = StreamShape<float, S>::OW;
+      const index_t groups = ((g.width + OW - 1) / OW + 3) / 4;
+      const index_t share = (groups * g.height + blocks - 1) / blocks;
+      stencil5_stream_pipe3_kernel<S0, S1, S2, PF, WRAP, float, SUM><<<blocks, threads, 0, s>>>(
+          I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, c0, 0.2f);
+    };
+  };
+  Variant v{buf, mk(in, out)};
+  v.launch2 = mk(out, const_cast<float*>(in));
+  v.steps = S;
+  v.ref = ref_for<S, WRAP>(in, out, g, tmp);
+  if (SUM) v.tol = 2e-6f;
+  return v;
+}
+
 int main(int argc, char** argv) {
   const index_t W = argc > 1 ? atol(argv[1]) : 32768;
   const index_t H = argc > 2 ? atol(argv[2]) : 32768;
@@ -386,6 +418,15 @@ int main(int argc, char** argv) {
     vs.push_back(pipe<10, 10, 6, false, 0, true, 2>(in, out, g));
     vs.push_back(pipe<10, 10, 6, false, 0, true, 1>(in, out, g));
     vs.push_back(pipe<12, 12, 6, false, 0, true, 2>(in, out, g));
+  } else if (focus && std::string(focus) == "pipe3") {  // three-stage pipeline (3 waves / SIMD)
+    vs.push_back(pipe<10, 10, 6, true, 0, true>(in, out, g, tmp));
+    vs.push_back(pipe3<7, 7, 6, 6>(in, out, g, tmp));
+    vs.push_back(pipe3<6, 7, 7, 6>(in, out, g, tmp));
+    vs.push_back(pipe3<7, 6, 7, 6>(in, out, g, tmp));
+    vs.push_back(pipe3<8, 8, 8, 6>(in, out, g, tmp));
+    vs.push_back(pipe3<7, 7, 6, 3>(in, out, g, tmp));
+    vs.push_back(pipe<12, 12, 6, true, 0, true>(in, out, g, tmp));
+    vs.push_back(pipe3<7, 7, 6, 6, false>(in, out, g));
   } else if (focus && std::string(focus) == "s24") {  // S = 20 vs 24 (sum form) on large tiles
     vs.push_back(pipe<10, 10, 6, true, 0, true>(in, out, g, tmp));
     vs.push_back(pipe<12, 12, 6, true, 0, true>(in, out, g, tmp));

@@ -116,6 +116,30 @@ Variant pipe(const TileGeom& g, double* tmp) {
   return v;
 }
 
+// Three-stage pipeline (768-thread workgroups, 3 waves per SIMD), sum form.
+template <int S0, int S1, int S2, int PF, bool WRAP>
+Variant pipe3(const TileGeom& g, double* tmp) {
+  constexpr int S = S0 + S1 + S2;
+  const int blocks =
+      resident(reinterpret_cast<const void*>(stencil5_stream_pipe3_kernel<S0, S1, S2, PF, WRAP, double, true>), 768);
+  const double c0 = std::pow(0.2, S);
+  Variant v;
+  v.launch = [=](const double* I, double* O, hipStream_t s) {
+    constexpr int OW = StripShape<double, S, true>::OW;
+    const index_t groups = ((g.width + OW - 1) / OW + 3) / 4;
+    const index_t share = (groups * g.height + blocks - 1) / blocks;
+    stencil5_stream_pipe3_kernel<S0, S1, S2, PF, WRAP, double, true><<<blocks, 768, 0, s>>>(
+        I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, c0, 0.2);
+  };
+  char buf[128];
+  std::snprintf(buf, sizeof(buf), "pipe3_s%d+%d+%d_pf%d_b%d%s_sum", S0, S1, S2, PF, blocks / 256, WRAP ? "_wrap" : "");
+  v.name = buf;
+  v.steps = S;
+  v.ref = ref_fn<S, WRAP>(g, tmp);
+  v.tol = 1e-14;
+  return v;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -160,6 +184,14 @@ int main(int argc, char** argv) {
     vs.push_back(balanced<12, false, false>(g, tmp));
     vs.push_back(pipe<6, 6, 3, false>(g, tmp));
     vs.push_back(pipe<5, 5, 3, false>(g, tmp));
+  }
+  if (f == "pipe3") {  // three-stage pipeline vs the two-stage 8 + 8 sum form
+    vs.push_back(pipe<8, 8, 3, true, true>(g, tmp));
+    vs.push_back(pipe3<5, 5, 5, 3, true>(g, tmp));
+    vs.push_back(pipe3<5, 5, 6, 3, true>(g, tmp));
+    vs.push_back(pipe3<6, 5, 5, 3, true>(g, tmp));
+    vs.push_back(pipe3<6, 6, 6, 3, true>(g, tmp));
+    vs.push_back(pipe3<6, 6, 4, 3, true>(g, tmp));
   }
   if (f == "sum") {  // sum form (c_center == c_neighbor) vs the general wide-lane body
     vs.push_back(pipe<6, 6, 3, true>(g, tmp));
