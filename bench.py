@@ -29,11 +29,13 @@ sweep per step and bitwise equal to its CPU model
 Timing: W untimed warm-up steps, then ``prepare(K)`` (graph capture + upload
 and one launch of every kernel shape the timed window uses, state unchanged)
 and ``--clock-warmup-ms`` (default 200) of further untimed, state-preserving
-launches of those shapes — a short window (K = 20 is one ~3 ms pass) otherwise
+launches of those shapes — a short window (K = 20 is one ~2 ms pass) otherwise
 runs partly below the sustained clocks while DVFS ramps up (cold 3.27 ms vs
 2.6 ms warm, profiles/r02_deep/clock_ramp.txt) — then K timed steps
-bracketed by barrier + device synchronisation on both sides; the time is the
-max over ranks. Every one of the K steps runs in full inside the window.
+bracketed by barrier + device synchronisation on both sides: each rank's
+clock starts after the opening barrier and stops once its device work has
+completed, before the closing barrier; the time is the max over ranks. Every
+one of the K steps runs in full inside the window.
 
     python bench.py                       # N=1
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
@@ -71,6 +73,12 @@ def _sync():
 
 
 def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0) -> float:
+    """K steps bracketed by barrier + device synchronisation on both sides; the
+    max over ranks. Each rank's clock stops when its own device work is done,
+    before the closing barrier: a 20-step window at N = 8 is one ~0.3 ms pass,
+    and an NCCL barrier (a device all-reduce + synchronisation) inside it would
+    be a large share of it. The halo exchange couples the ranks, so the slowest
+    rank's (t1 - t0) still covers every rank's K steps."""
     st.run(warmup)
     st.prepare(steps)  # graphs + first launches of the timed shapes, outside the window
     st.warm(steps, warm_s)  # untimed, state-preserving: sustained clocks for a short window
@@ -82,8 +90,8 @@ def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0) -> float:
     st.run(steps)
     st.synchronize()  # polls under the communication watchdog when a peer can hang
     _sync()
-    ctx.barrier()
     t1 = time.perf_counter()
+    ctx.barrier()
     return ctx.allreduce_max(t1 - t0)
 
 

@@ -36,15 +36,18 @@ void wait_with_timeout(Done&& done, const char* what, OnTimeout&& on_timeout) {
   using clock = std::chrono::steady_clock;
   const double limit = comm_timeout();
   const auto t0 = clock::now();
-  int spins = 0;
   while (!done()) {
-    if (limit > 0 && std::chrono::duration<double>(clock::now() - t0).count() > limit) {
+    const double waited = std::chrono::duration<double>(clock::now() - t0).count();
+    if (limit > 0 && waited > limit) {
       on_timeout();
       raise_error(std::string(what) + " timed out after " + std::to_string(limit) +
                   " s: a peer rank is dead or hung (communication watchdog)");
     }
-    // Spin briefly (latency), then back off so a long wait does not burn a core.
-    if (++spins > 1000) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    // Spin for the first 20 ms (a timed window ends inside it: a 20-step
+    // window on the 8-GPU tile is one ~0.3 ms pass, and a 50 us sleep -
+    // 60-100 us with the scheduler - added ~20% to it; profiles/r02_window),
+    // then back off so a long wait does not burn a core.
+    if (waited > 0.02) std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
 }
 

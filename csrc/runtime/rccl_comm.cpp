@@ -1,5 +1,6 @@
 #include "mxs/comm/rccl_comm.hpp"
 
+#include <chrono>
 #include <cstring>
 
 #include "mxs/core/fault.hpp"
@@ -36,13 +37,22 @@ bool RcclComm::healthy(std::string* msg) const {
 }
 
 void RcclComm::wait(hipStream_t stream, const char* what) const {
+  // The stream is polled on every spin; the communicator's async error state
+  // (a call into RCCL) only once per millisecond: querying it on every spin
+  // delayed noticing the completion of a 20-step window by ~100 us.
+  using clock = std::chrono::steady_clock;
+  auto next_check = clock::now();
   wait_with_timeout(
       [&] {
         const hipError_t q = hipStreamQuery(stream);
         if (q == hipSuccess) return true;
         if (q != hipErrorNotReady) MXS_HIP_CHECK(q);
-        std::string msg;
-        if (!healthy(&msg)) raise_error(std::string(what) + ": RCCL communicator failed: " + msg);
+        const auto now = clock::now();
+        if (now >= next_check) {
+          next_check = now + std::chrono::milliseconds(1);
+          std::string msg;
+          if (!healthy(&msg)) raise_error(std::string(what) + ": RCCL communicator failed: " + msg);
+        }
         return false;
       },
       what, [&] { abort(); });
