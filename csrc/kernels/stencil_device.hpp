@@ -1153,7 +1153,11 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
   const int lane = threadIdx.x & (kWaveSize - 1);
   const index_t gx = xw - SA + index_t(lane) * N;
   const index_t rows = ye - ys;
-  const index_t n_it0 = rows + 2 * S1 + 3 * S0 - 1;  // stage 0: level-S0 rows [ys - S1, ye + S1)
+  // Stage 0 starts D rows early so that its ring writes start block-aligned
+  // (row k is emitted at iteration 3*S0 - 1 + D + k, a multiple of PF for k = 0):
+  // no per-row slot wrap. The lead rows only feed level-S0 rows before ys - S1.
+  constexpr int D = (PF - (3 * S0 - 1) % PF) % PF;
+  const index_t n_it0 = rows + 2 * S1 + 3 * S0 - 1 + D;  // stage 0: level-S0 rows [ys - S1, ye + S1)
   const index_t n_it1 = rows + 3 * S1 - 1;           // stage 1: output rows [ys, ye)
   const index_t blocks0 = (n_it0 + PF - 1) / PF, blocks1 = T1 + (n_it1 + PF - 1) / PF;
   const index_t blocks = blocks0 > blocks1 ? blocks0 : blocks1;
@@ -1172,15 +1176,30 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
     }
     const T* __restrict__ pin = in + core_off + lx;
     const index_t last_row = ye + S - 1;
-    index_t next = ys - S;
+    // The first PF rows (the D lead rows clamped to the first needed row when
+    // there is no wrap: they may lie above the ghost ring).
+    V pf[PF];
+#pragma unroll
+    for (int k = 0; k < PF; ++k) {
+      index_t r = ys - S - D + k;
+      if constexpr (WRAP) r = r < 0 ? r + H : r;
+      else r = r < ys - S ? ys - S : r;
+      pf[k] = B::load(pin + r * pitch);
+    }
+    index_t next = ys - S - D + PF;
     if constexpr (WRAP) next = next < 0 ? next + H : next;
+    index_t roff = next * pitch;  // element offset of row `next`, stepped (no multiply per row)
     auto fetch = [&]() -> V {
-      const V v = B::load(pin + next * pitch);
+      const V v = B::load(pin + roff);
       if constexpr (WRAP) {
         ++next;
-        next = next == H ? 0 : next;
+        const bool wrap = next == H;
+        next = wrap ? 0 : next;
+        roff = wrap ? 0 : roff + pitch;
       } else {
-        next = next < last_row ? next + 1 : next;
+        const bool adv = next < last_row;
+        next = adv ? next + 1 : next;
+        roff = adv ? roff + pitch : roff;
       }
       return v;
     };
@@ -1189,9 +1208,6 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
     for (int q = 0; q < 3; ++q)
 #pragma unroll
       for (int l = 0; l < S0; ++l) win[q][l] = B::zero();
-    V pf[PF];
-#pragma unroll
-    for (int k = 0; k < PF; ++k) pf[k] = fetch();
     constexpr int kWarm = (3 * (S0 - 1)) / PF * PF;  // see stream_chunk_rot: level l matters from iteration 3l + 2
 #pragma unroll 1
     for (int ib = 0; ib < kWarm; ib += PF) {
@@ -1207,10 +1223,12 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
       }
       __syncthreads();
     }
+    // Ring slot of each block's first row k = i - (3*S0 - 1): a wave-uniform
+    // counter stepping by PF modulo RING (a 64-bit modulo per block cost ~40
+    // scalar instructions).
+    int base = ((kWarm - (3 * S0 - 1 + D)) % RING + RING) % RING;  // 0, PF or 2 PF
 #pragma unroll 1
     for (index_t i = kWarm; i < blocks * PF; i += PF) {
-      // Ring slot of this block's first row k = i - (3*S0 - 1) (wave-uniform, once per block).
-      const int base = int((i - (3 * S0 - 1) + index_t(RING) * (3 * S0)) % RING);
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
         const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
@@ -1223,11 +1241,12 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
           if (l == S0 - 1) top = o;
           else win[p0][l + 1] = o;
         }
-        // Row k = j - (3*S0 - 1) of stage 1's input (rotated layout); writes
-        // for k < 0 land in slots no reader touches before they are rewritten.
-        const int slot = base + k < RING ? base + k : base + k - RING;
-        my[slot * kWaveSize] = top;
+        // Row k = j - (3*S0 - 1 + D) of stage 1's input (rotated layout);
+        // writes for k < 0 land in slots no reader touches before they are
+        // rewritten. base + k < RING: blocks are ring-aligned.
+        my[(base + k) * kWaveSize] = top;
       }
+      base = base + PF < RING ? base + PF : 0;
       __syncthreads();
     }
   } else {
@@ -1268,12 +1287,13 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
       }
       __syncthreads();
     }
+    int base = (kWarm / PF) % 3 * PF;  // ring slot of the block's first row (counter, see stage 0)
 #pragma unroll 1
     for (index_t i = kWarm; i < (blocks - T1) * PF; i += PF) {
       V inrow[PF];
-      const int base = int((i / PF) % 3) * PF;
 #pragma unroll
       for (int k = 0; k < PF; ++k) inrow[k] = my[(base + k) * kWaveSize];
+      base = base + PF < RING ? base + PF : 0;
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
         const index_t j = i + k;
