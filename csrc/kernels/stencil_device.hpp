@@ -975,13 +975,18 @@ __device__ __forceinline__ void stream_chunk_fast(const typename B::T* __restric
   const index_t last_row = ye + S - 1;
   index_t next = y_first;
   if constexpr (WRAP) next = next < 0 ? next + H : next;
+  index_t roff = next * pitch;  // element offset of row `next`, stepped (see pipe_chunk)
   auto fetch = [&]() -> V {
-    const V v = B::load(pin + next * pitch);
+    const V v = B::load(pin + roff);
     if constexpr (WRAP) {
       ++next;
-      next = next == H ? 0 : next;
+      const bool wrap = next == H;
+      next = wrap ? 0 : next;
+      roff = wrap ? 0 : roff + pitch;
     } else {
-      next = next < last_row ? next + 1 : next;
+      const bool adv = next < last_row;
+      next = adv ? next + 1 : next;
+      roff = adv ? roff + pitch : roff;
     }
     return v;
   };
