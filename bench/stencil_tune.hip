@@ -195,26 +195,28 @@ Variant balanced(const float* in, float* out, const TileGeom& g, int per_cu, flo
 }
 
 // Two-stage wave pipeline (S = S0 + S1 levels; 512-thread workgroups).
-template <int S0, int S1, int PF, bool WRAP = true, int PRIO = 0, bool SUM = false, int G = 4, bool XM = false>
+template <int S0, int S1, int PF, bool WRAP = true, int PRIO = 0, bool SUM = false, int G = 4, bool XM = false,
+          bool JOINT = false>
 Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullptr) {
   int per_cu = 0, cus = 0;
   constexpr int threads = 2 * G * kWaveSize;
   MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu, reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM>),
+      &per_cu, reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM, JOINT>),
       threads, 0));
   MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const int blocks = std::max(1, per_cu * cus);
   char buf[128];
-  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s%s%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
+  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s%s%s%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
                 PRIO == 1 ? "_prio0" : (PRIO == 2 ? "_prio1" : ""), SUM ? "_sum" : "",
-                G == 4 ? "" : (G == 2 ? "_g2" : "_g1"), XM ? "_xcd" : "");
+                G == 4 ? "" : (G == 2 ? "_g2" : "_g1"), XM ? "_xcd" : "", JOINT ? "_joint" : "");
   const float c0 = SUM ? float(std::pow(0.2, S0 + S1)) : 0.2f;  // sum form: c0 carries c^S
   auto mk = [=](const float* I, float* O) {
     return [=](hipStream_t s) {
       constexpr int OW = StreamShape<float, S0 + S1>::OW;
-      const index_t groups = ((g.width + OW - 1) / OW + G - 1) / G;
+      constexpr int OWG = JointShape<S0, S1, G>::OWG;
+      const index_t groups = JOINT ? (g.width + OWG - 1) / OWG : ((g.width + OW - 1) / OW + G - 1) / G;
       const index_t share = (groups * g.height + blocks - 1) / blocks;
-      stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM><<<blocks, threads, 0, s>>>(
+      stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM, JOINT><<<blocks, threads, 0, s>>>(
           I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, c0, 0.2f);
     };
   };
@@ -427,6 +429,35 @@ int main(int argc, char** argv) {
     vs.push_back(pipe3<7, 7, 6, 3>(in, out, g, tmp));
     vs.push_back(pipe<12, 12, 6, true, 0, true>(in, out, g, tmp));
     vs.push_back(pipe3<7, 7, 6, 6, false>(in, out, g));
+  } else if (focus && std::string(focus) == "joint") {  // joint stage-1 windows vs per-strip aprons
+    // Every joint variant is checked BITWISE against the per-strip pipeline of
+    // the same S (the split does not change the arithmetic).
+    auto joint_vs = [&](Variant j, const Variant& plain) {
+      j.ref = plain.launch;
+      j.tol = 0.f;
+      return j;
+    };
+    const Variant p20 = pipe<10, 10, 6, true, 0, true>(in, out, g, tmp);
+    const Variant p24 = pipe<12, 12, 6, true, 0, true>(in, out, g, tmp);
+    const Variant p28 = pipe<14, 14, 6, true, 0, true>(in, out, g, tmp);
+    const Variant n20 = pipe<10, 10, 6, false, 0, true>(in, out, g);
+    const Variant n24 = pipe<12, 12, 6, false, 0, true>(in, out, g);
+    vs.push_back(p20);
+    vs.push_back(p24);
+    vs.push_back(joint_vs(pipe<10, 10, 6, true, 0, true, 4, false, true>(in, out, g), p20));
+    vs.push_back(joint_vs(pipe<8, 12, 6, true, 0, true, 4, false, true>(in, out, g), p20));
+    vs.push_back(joint_vs(pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g), p20));
+    vs.push_back(joint_vs(pipe<12, 12, 6, true, 0, true, 4, false, true>(in, out, g), p24));
+    vs.push_back(joint_vs(pipe<8, 16, 6, true, 0, true, 4, false, true>(in, out, g), p24));
+    vs.push_back(p28);
+    vs.push_back(joint_vs(pipe<16, 16, 3, true, 0, true, 4, false, true>(in, out, g),
+                          pipe<16, 16, 3, true, 0, true>(in, out, g, tmp)));
+    vs.push_back(joint_vs(pipe<12, 16, 6, true, 0, true, 4, false, true>(in, out, g), p28));
+    vs.push_back(joint_vs(pipe<12, 12, 6, true, 0, false, 4, false, true>(in, out, g),
+                          pipe<12, 12, 6, true, 0, false>(in, out, g, tmp)));
+    vs.push_back(n20);
+    vs.push_back(joint_vs(pipe<8, 12, 6, false, 0, true, 4, false, true>(in, out, g), n20));
+    vs.push_back(joint_vs(pipe<12, 12, 6, false, 0, true, 4, false, true>(in, out, g), n24));
   } else if (focus && std::string(focus) == "s24") {  // S = 20 vs 24 (sum form) on large tiles
     vs.push_back(pipe<10, 10, 6, true, 0, true>(in, out, g, tmp));
     vs.push_back(pipe<12, 12, 6, true, 0, true>(in, out, g, tmp));

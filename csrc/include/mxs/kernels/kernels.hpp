@@ -98,18 +98,19 @@ constexpr int kMaxTimeBlockDeep = 32;
 // where the chunk / strip aprons are small against the tile).
 inline int auto_time_block(index_t w, index_t h, int elem_bytes = 4, bool sum_form = true) {
   if (elem_bytes == 4 && w >= 1024 && h >= 1024) {
-    // The pipeline runs 4-strip groups of 256 - 2 * SA output columns: when
-    // the last group at S = 20 (216 columns per strip) is partial and S = 24
-    // (208) fills it, the idle strips cost more than the deeper block (8192^2,
-    // sum form: 38 strips in 10 groups at S = 20, 8.05 T cells/s; 40 at
-    // S = 24, 8.20; profiles/r02_sum).
-    auto strips = [&](int ow) { return (w + ow - 1) / ow; };
-    if (sum_form && strips(216) % 4 != 0 && strips(208) % 4 == 0) return 24;
+    // The pipeline runs workgroups of 4 strips; with joint stage-1 windows a
+    // group stores 912 columns at S = 20 (12 + 8) and 904 at S = 24 (12 + 12),
+    // and a partial last group costs a whole one. S = 24 when it needs no more
+    // groups than S = 20 (4096 wide: 5 and 5); otherwise the extra group costs
+    // more than the deeper block saves (8192^2 sum form: 9 vs 10 groups,
+    // 8.6-8.9 T cells/s at S = 20 vs 8.4 at 24; 16384 wide: 18 vs 19 groups,
+    // 9.8-10.0 vs 9.4; profiles/r02_joint).
+    auto groups = [&](int owg) { return (w + owg - 1) / owg; };
+    if (sum_form && groups(904) <= groups(912)) return 24;
     // Tiles of >= 2^30 cells (chunks of ~4800 rows, warm-up negligible): the
-    // deeper block relieves HBM (4.0 -> 3.4 TB/s) and wins, 32768^2 sum form
-    // 10.1-10.5 T cells/s at S = 24 vs 10.0 at 20 in three tuner runs; at
-    // 32768 x 16384 and below S = 20 stays ahead (profiles/r02_sum/s24_*). A
-    // 20-step run is still one S = 20 pass (run(K) splits K near-equally).
+    // deeper block relieves HBM and wins even at one group more, 32768^2 sum
+    // form 11.1 T cells/s at S = 24 vs 10.9 at 20 (37 vs 36 groups). A 20-step
+    // run is still one S = 20 pass (run(K) splits K near-equally).
     if (sum_form && w * h >= (index_t(1) << 30)) return 24;
     return 20;
   }
@@ -138,6 +139,13 @@ void stencil5_rect(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
 // ranks are co-resident instead of queueing in rounds behind each other.
 void set_gpu_share(int processes);
 int gpu_share();
+
+// Joint stage-1 windows in the fp32 two-stage pipeline (stencil_device.hpp:
+// JointShape): on by default for time blocks that split into two multiples of
+// 4 levels (S = 20, 24, 28, 32); off runs the per-strip layout (bitwise equal
+// output). MXS_PIPE_JOINT=0 in the environment turns it off at start-up.
+void set_pipe_joint(bool on);
+bool pipe_joint();
 
 // Kernel form chosen by the most recent stencil launcher on this host process:
 // "stream_pipe" (the two-stage pipeline: fp32 blocks > 16 steps, the one the

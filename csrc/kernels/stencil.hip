@@ -37,6 +37,8 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <cstdlib>
+#include <string>
 
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
@@ -339,9 +341,15 @@ const char* last_stencil_dispatch() { return g_last_dispatch.load(std::memory_or
 
 namespace {
 std::atomic<int> g_gpu_share{1};
-}
+std::atomic<bool> g_pipe_joint{[] {
+  const char* e = std::getenv("MXS_PIPE_JOINT");
+  return !(e && std::string(e) == "0");
+}()};
+}  // namespace
 void set_gpu_share(int processes) { g_gpu_share.store(std::max(1, processes), std::memory_order_relaxed); }
 int gpu_share() { return g_gpu_share.load(std::memory_order_relaxed); }
+void set_pipe_joint(bool on) { g_pipe_joint.store(on, std::memory_order_relaxed); }
+bool pipe_joint() { return g_pipe_joint.load(std::memory_order_relaxed); }
 namespace detail {
 void note_dispatch(const char* k) { note(k); }
 }  // namespace detail

@@ -1143,20 +1143,57 @@ struct PipeShape {
   static constexpr int T1 = (3 * S0 + PF - 1 + PF - 1) / PF;  // stage-1 start block: ceil((3*S0 + PF - 1) / PF)
 };
 
-template <typename B, int S0, int S1, int PF, bool WRAP>
+// Joint stage-1 windows (JOINT). In the layout above every strip pays the
+// apron of all S levels: 256 - 2 SA(S) output columns per strip (208 of 256 at
+// S = 24). Stage 1 does not need its own strip's stage-0 edges, though: the
+// level-S0 columns a stage-0 wave gets right (all but A0 = S0 rounded up to 4
+// per side) are laid side by side, for the G strips of the workgroup, in ONE
+// LDS row of G * OW0 valid columns, and stage 1's G windows (256 columns each,
+// stride OW1 = 256 - 2 A1) are cut from that row. Stage 0's apron is still
+// paid per strip, stage 1's once per group: OWG = G (256 - 2 A0) - 2 A1 output
+// columns per group, capped at G * OW1 (S = 24 as 12 + 12: 904 vs 4 x 208 =
+// 832, +8.7% per pass at the same VALU work; S = 20 as 8 + 12: 928 vs 864;
+// S = 28 as 12 + 16: 896 vs 800). The stage-0 lanes that hold no valid
+// column write into the row's tail (G * 2 A0 / 4 slots, exactly the lanes that
+// need one), which stage 1 only reads into columns it never stores. Same
+// operations per cell as the per-strip layout: bitwise identical output.
+template <int S0, int S1, int G>
+struct JointShape {
+  static constexpr int A0 = (S0 + 3) / 4 * 4, A1 = (S1 + 3) / 4 * 4;  // per-stage aprons (4-column lanes)
+  static constexpr int OW0 = 256 - 2 * A0;    // valid level-S0 columns per stage-0 wave
+  static constexpr int OW1 = 256 - 2 * A1;    // stride of stage 1's windows
+  static constexpr int SPAN = G * OW0;        // valid columns of the joint row
+  // Output columns per group: the joint row's valid span less stage 1's apron,
+  // or what the G windows can store (G * OW1) when that is less (A0 < A1).
+  static constexpr int OWG = SPAN - 2 * A1 < G * OW1 ? SPAN - 2 * A1 : G * OW1;
+  static constexpr int ROW = G * kWaveSize;   // joint row length in lane vectors (SPAN / 4 + the tail)
+  static constexpr int LEAD = A0 + A1;        // input columns left of the group's first output column
+  static_assert((G - 1) * OW1 + 256 <= 4 * ROW, "stage-1 windows must stay inside the joint row");
+  static_assert(OWG > 0, "time block too deep for a joint group");
+};
+
+template <typename B, int S0, int S1, int PF, bool WRAP, bool JOINT = false, int G = kWavesPerBlock>
 __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in, typename B::T* __restrict__ out,
                                            index_t pitch, index_t core_off, index_t W, index_t H, index_t xw,
                                            index_t x_end, index_t ys, index_t ye, typename B::T c0, typename B::T c1,
-                                           typename B::V* __restrict__ ring, int stage) {
+                                           typename B::V* __restrict__ ring, int stage, int strip = 0) {
   static_assert(PF % 3 == 0, "the window rotates through 3 slots: PF must be a multiple of 3");
   using P = PipeShape<S0, S1, PF>;
   constexpr int S = P::S, RING = P::RING, T1 = P::T1;
   using T = typename B::T;
   using V = typename B::V;
   using Sh = StripShape<T, S, true>;
+  using J = JointShape<S0, S1, G>;
   constexpr int N = Sh::N, SA = Sh::SA, AL = SA / N;
+  static_assert(!JOINT || N == 4, "joint windows assume 4-cell lanes");
   const int lane = threadIdx.x & (kWaveSize - 1);
-  const index_t gx = xw - SA + index_t(lane) * N;
+  // Per-strip layout: xw = the strip's first output column, both stages cover
+  // [xw - SA, xw - SA + 256). Joint: xw = the GROUP's first output column;
+  // stage-0 wave `strip` covers [xw - LEAD + strip OW0, + 256), stage-1 wave
+  // `strip` the window [xw - A1 + strip OW1, + 256).
+  const index_t gx = JOINT ? (stage == 0 ? xw - J::LEAD + index_t(strip) * J::OW0 : xw - J::A1 + index_t(strip) * J::OW1) +
+                                 index_t(lane) * N
+                           : xw - SA + index_t(lane) * N;
   const index_t rows = ye - ys;
   // Stage 0 starts D rows early so that its ring writes start block-aligned
   // (row k is emitted at iteration 3*S0 - 1 + D + k, a multiple of PF for k = 0):
@@ -1166,14 +1203,28 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
   const index_t n_it1 = rows + 3 * S1 - 1;           // stage 1: output rows [ys, ye)
   const index_t blocks0 = (n_it0 + PF - 1) / PF, blocks1 = T1 + (n_it1 + PF - 1) / PF;
   const index_t blocks = blocks0 > blocks1 ? blocks0 : blocks1;
-  V* __restrict__ my = ring + lane;
+  // This lane's slot in a ring row, and the ring's row stride (lane vectors).
+  constexpr int RSTRIDE = JOINT ? J::ROW : kWaveSize;
+  int slot = lane;
+  if constexpr (JOINT) {
+    constexpr int AL0 = J::A0 / 4;  // stage-0 lanes per side without a valid level-S0 column
+    if (stage == 0) {
+      const bool valid = lane >= AL0 && lane < kWaveSize - AL0;
+      const int tail = J::SPAN / 4 + strip * 2 * AL0 + (lane < AL0 ? lane : lane - (kWaveSize - 2 * AL0));
+      slot = valid ? strip * (J::OW0 / 4) + lane - AL0 : tail;
+    } else {
+      slot = strip * (J::OW1 / 4) + lane;
+    }
+  }
+  V* __restrict__ my = ring + slot;
 
   if (stage == 0) {  // wave-uniform
     index_t lx;
-    if (xw >= x_end) {
+    if (!JOINT && xw >= x_end) {
       lx = 0;  // idle strip past the rectangle: any valid address, nothing it makes is stored
     } else if constexpr (WRAP) {
-      if (W >= kWaveSize * N) lx = gx < 0 ? gx + W : (gx >= W ? gx - W : gx);
+      // Joint groups read up to G * 256 columns past their first output column.
+      if (W >= (JOINT ? G : 1) * kWaveSize * N) lx = gx < 0 ? gx + W : (gx >= W ? gx - W : gx);
       else lx = ((gx % W) + W) % W;
     } else {
       const index_t last_col = (W + N - 1) / N * N + SA - N;
@@ -1249,21 +1300,31 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
         // Row k = j - (3*S0 - 1 + D) of stage 1's input (rotated layout);
         // writes for k < 0 land in slots no reader touches before they are
         // rewritten. base + k < RING: blocks are ring-aligned.
-        my[(base + k) * kWaveSize] = top;
+        my[(base + k) * RSTRIDE] = top;
       }
       base = base + PF < RING ? base + PF : 0;
       __syncthreads();
     }
   } else {
     // Output descriptor over rows [ys, ye) (see stream_chunk_rot).
-    const T* obase = out + core_off + (xw - SA) + ys * pitch;
+    const index_t x0w = gx - index_t(lane) * N;  // the window's first column
+    const T* obase = out + core_off + x0w + ys * pitch;
     const unsigned long long ob = reinterpret_cast<unsigned long long>(obase);
     const unsigned ob_lo = __builtin_amdgcn_readfirstlane(unsigned(ob)),
                    ob_hi = __builtin_amdgcn_readfirstlane(unsigned(ob >> 32));
     T* obase_u = reinterpret_cast<T*>((static_cast<unsigned long long>(ob_hi) << 32) | ob_lo);
     const int nbytes = __builtin_amdgcn_readfirstlane(int(rows * pitch * index_t(sizeof(T))));
     const __amdgpu_buffer_rsrc_t orsrc = __builtin_amdgcn_make_buffer_rsrc(obase_u, 0, nbytes, 0x00020000);
-    const bool store_lane = lane >= AL && lane < kWaveSize - AL && gx < x_end && xw < x_end;
+    bool store_lane;
+    if constexpr (JOINT) {
+      // Inside this window's own apron and inside the group's output span
+      // [A1, A1 + OWG) (the last window may run past it); windows tile the group.
+      constexpr int AL1 = J::A1 / 4;
+      const int q = strip * J::OW1 + lane * N;  // joint-row column of this lane's first cell
+      store_lane = lane >= AL1 && lane < kWaveSize - AL1 && q + N <= J::A1 + J::OWG && gx < x_end;
+    } else {
+      store_lane = lane >= AL && lane < kWaveSize - AL && gx < x_end && xw < x_end;
+    }
     const unsigned lane_off = unsigned(lane) * unsigned(N * sizeof(T));
     const unsigned row_bytes = unsigned(pitch) * unsigned(sizeof(T));
     constexpr unsigned kDrop = 0x80000000u;
@@ -1280,7 +1341,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
       V inrow[PF];
       const int base = (ib / PF) % 3 * PF;  // RING = 3 * PF and ib is a multiple of PF
 #pragma unroll
-      for (int k = 0; k < PF; ++k) inrow[k] = my[(base + k) * kWaveSize];
+      for (int k = 0; k < PF; ++k) inrow[k] = my[(base + k) * RSTRIDE];
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
         const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
@@ -1297,7 +1358,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
     for (index_t i = kWarm; i < (blocks - T1) * PF; i += PF) {
       V inrow[PF];
 #pragma unroll
-      for (int k = 0; k < PF; ++k) inrow[k] = my[(base + k) * kWaveSize];
+      for (int k = 0; k < PF; ++k) inrow[k] = my[(base + k) * RSTRIDE];
       base = base + PF < RING ? base + PF : 0;
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
@@ -1332,18 +1393,20 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 // XM (tuning): XCD-major share order — the workgroups one XCD runs (blockIdx
 // congruent mod 8) take consecutive shares, so vertically adjacent chunks, which
 // read the same 2S apron rows, share that XCD's L2.
+// JOINT: joint stage-1 windows (JointShape), OWG output columns per group.
 template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float, bool SUM = false,
-          int G = kWavesPerBlock, bool XM = false>
+          int G = kWavesPerBlock, bool XM = false, bool JOINT = false>
 __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
   using P = PipeShape<S0, S1, PF>;
   using B = typename FastBody<T, SUM>::type;
   constexpr int OW = StripShape<T, P::S, true>::OW;
+  constexpr int OWG = JointShape<S0, S1, G>::OWG;
   __shared__ typename B::V ring[G * P::RING * kWaveSize];
   const index_t rows = y_end - y_begin;
   const index_t strips = (x_end - x_begin + OW - 1) / OW;
-  const index_t groups = (strips + G - 1) / G;
+  const index_t groups = JOINT ? (x_end - x_begin + OWG - 1) / OWG : (strips + G - 1) / G;
   const index_t total = groups * rows;
   const int wave = threadIdx.x / kWaveSize;
   const int strip = wave % G, stage = wave / G;
@@ -1362,9 +1425,14 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
   while (a < b) {  // workgroup-uniform: all 8 waves take every chunk (barriers inside)
     const index_t grp = a / rows, r0 = a - grp * rows;
     const index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
-    const index_t xw = x_begin + (grp * G + strip) * OW;
-    pipe_chunk<B, S0, S1, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1,
-                                 ring + strip * P::RING * kWaveSize, stage);
+    if constexpr (JOINT) {
+      pipe_chunk<B, S0, S1, PF, WRAP, true, G>(in, out, pitch, core_off, W, H, x_begin + grp * OWG, x_end,
+                                               y_begin + r0, y_begin + r1, c0, c1, ring, stage, strip);
+    } else {
+      const index_t xw = x_begin + (grp * G + strip) * OW;
+      pipe_chunk<B, S0, S1, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1,
+                                      ring + strip * P::RING * kWaveSize, stage);
+    }
     a += r1 - r0;
   }
 }

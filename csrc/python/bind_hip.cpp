@@ -174,6 +174,9 @@ PYBIND11_MODULE(_mxs_hip, m) {
   m.def("set_gpu_share", &kernels::set_gpu_share, py::arg("processes"),
         "processes sharing this GPU: persistent stencil kernels take 1/processes of the chip");
   m.def("gpu_share", &kernels::gpu_share);
+  m.def("set_pipe_joint", &kernels::set_pipe_joint, py::arg("on"),
+        "joint stage-1 windows in the fp32 two-stage pipeline (default on; bitwise equal output)");
+  m.def("pipe_joint", &kernels::pipe_joint);
   m.def(
       "stencil5_tb",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0,

@@ -50,7 +50,7 @@ def _expect(kernel, sum_form):
 
 
 @pytest.mark.parametrize("w,h,steps,dtype,kernel", [
-    (8192, 8192, 24, torch.float32, "stream_pipe"),           # BASELINE config 2 (1 GPU), auto S: two-stage pipeline
+    (8192, 8192, 24, torch.float32, "stream_pipe"),           # BASELINE config 2 (1 GPU) at S = 24: two-stage pipeline
     (8192, 8192, 20, torch.float32, "stream_pipe"),           # the driver's 20-step window in one pass
     (4096, 2048, 17, torch.float32, "stream_pipe"),           # odd split 8 + 9
     (2048, 1024, 32, torch.float32, "stream_pipe"),           # deepest block, PF = 3
@@ -215,7 +215,7 @@ def test_sum_form_bitwise_vs_cpu_sum_reference(gpu, w, h, steps, dtype, kernel):
 
 @pytest.mark.parametrize("dtype,block,tol", [("f32", 24, 2e-6), ("f64", 16, 1e-14)])
 def test_solver_sum_form_matches_per_step(gpu, dtype, block, tol):
-    # 4096 wide: 19 strips of 216 columns at S = 20, 20 of 208 at S = 24 (whole groups).
+    # 4096 wide: 5 joint groups at S = 20 (912 columns each) and at S = 24 (904): auto S = 24.
     """Default (sum form, c_center == c_neighbor): two passes at the auto block
     agree with as many single steps to a few ulp, on the sum-form pipeline."""
     kw = dict(global_width=4096, global_height=2048, dims="1x1", dtype=dtype, seed=12)
@@ -282,3 +282,41 @@ def test_warm_and_prepare_leave_the_state_alone(gpu, backend, loopback):
     b.run(20)
     b.synchronize()
     assert torch.equal(a.core_view(), b.core_view())
+
+
+@pytest.mark.parametrize("w,h,steps,wrap,rect", [
+    (8192, 4096, 24, True, None),                  # 32768^2's split (12 + 12), 9 joint groups + a partial one
+    (8192, 4096, 20, True, None),                  # 8 + 12
+    (2048, 1024, 32, True, None),                  # 16 + 16, PF = 3
+    (2048, 1024, 28, True, None),                  # 12 + 16
+    (300, 200, 24, True, None),                    # one partial group, modulo wrap
+    (8192, 2048, 20, False, None),                 # ghost-ring tile (multi-GPU)
+    (4096, 2048, 24, False, (8, 4088, 24, 2024)),  # interior rectangle
+])
+@pytest.mark.parametrize("sum_form", [True, False])
+def test_pipe_joint_windows_bitwise_vs_per_strip(gpu, w, h, steps, wrap, rect, sum_form):
+    """Joint stage-1 windows (stage 0's valid columns of a workgroup's 4 strips
+    in one LDS row) give the same output bit for bit as the per-strip layout,
+    and write nothing outside the rectangle."""
+    g = core().TileGeom.aligned(w, h, 1 if wrap else steps, 1 if wrap else steps, 4)
+    gen = torch.Generator(device=gpu).manual_seed(w * 3 + steps)
+    src = torch.rand(g.alloc_elems(), generator=gen, device=gpu, dtype=torch.float32)
+    x0, x1, y0, y1 = rect or (0, w, 0, h)
+    outs = []
+    old = hip().pipe_joint()
+    try:
+        for joint in (True, False):
+            hip().set_pipe_joint(joint)
+            dst = torch.full_like(src, -3.0)
+            hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, x0, x1, y0, y1, 0.2, 0.2, wrap, "f32",
+                              torch.cuda.current_stream().cuda_stream, "auto", sum_form)
+            assert hip().last_stencil_dispatch() == _expect("stream_pipe", sum_form)
+            torch.cuda.synchronize()
+            outs.append(dst)
+    finally:
+        hip().set_pipe_joint(old)
+    assert torch.equal(outs[0], outs[1])
+    got = _core(outs[0], g, w, h)
+    mask = torch.ones(h, w, dtype=torch.bool, device=gpu)
+    mask[y0:y1, x0:x1] = False
+    assert bool((got[mask] == -3.0).all()) and bool((got[~mask] != -3.0).all())

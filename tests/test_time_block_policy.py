@@ -16,12 +16,13 @@ def _hip():
 @pytest.mark.parametrize(
     "w,h,dtype,sum_form,expected",
     [
-        (32768, 32768, "f32", True, 24),   # >= 2^30 cells: S = 24 relieves HBM (10.1-10.5 vs 10.0 T)
-        (32768, 32768, "f32", False, 20),  # per-step form: 11 + 9
-        (32768, 16384, "f32", True, 20),   # 2-GPU tile: S = 20 ahead
+        (32768, 32768, "f32", True, 24),   # >= 2^30 cells: S = 24 (37 joint groups) 11.1 vs 10.9 T at 20
+        (32768, 32768, "f32", False, 20),  # per-step form
+        (32768, 16384, "f32", True, 20),   # 2-GPU tile: 36 vs 37 joint groups
         (16384, 16384, "f32", True, 20),   # 4-GPU tile
-        (16384, 8192, "f32", True, 20),    # 8-GPU tile: 76 strips fill 19 groups at S = 20
-        (8192, 8192, "f32", True, 24),     # 38 strips (partial group) at 20, 40 at 24
+        (16384, 8192, "f32", True, 20),    # 8-GPU tile: 18 joint groups at S = 20, 19 at 24
+        (8192, 8192, "f32", True, 20),     # 9 joint groups at 20, 10 at 24 (8.6-8.9 vs 8.4 T)
+        (4096, 2048, "f32", True, 24),     # 5 joint groups either way: the deeper block
         (8192, 8192, "f64", True, 16),     # wide-lane pipeline 8 + 8
         (8192, 8192, "f64", False, 12),    # per-step 6 + 6
         (512, 512, "f32", True, 12),       # small tiles: single-wave kernels
