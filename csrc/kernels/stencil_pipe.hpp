@@ -49,19 +49,21 @@ constexpr int pipe_pf() {
 // cells/s for 8 + 12 and 10.0 per-strip 10 + 10; 8 + 12 is 2-3% ahead on the
 // 16384-wide and 8192-wide tiles), 24 = 12 + 12 (11.1 vs 10.2 per-strip),
 // 28 = 12 + 16 (11.5), 32 = 16 + 16 (11.8; PF = 3).
+// fp64 (wide-lane body, 4 doubles per lane: the same 256-column strips): the
+// sum form's S = 16 as 8 + 8, 944 vs 896 columns per group.
 template <typename T, int S>
 constexpr bool pipe_joint_ok() {
-  return sizeof(T) == 4 && S % 4 == 0 && S >= 20;
+  return sizeof(T) == 4 ? (S % 4 == 0 && S >= 20) : S == 16;
 }
-template <int S>
+template <typename T, int S>
 constexpr int joint_s0() {
-  return S >= 32 ? 16 : 12;
+  return sizeof(T) == 8 ? S / 2 : (S >= 32 ? 16 : 12);
 }
 
 template <typename T, int S, bool WRAP, bool SUM, bool JOINT = false>
 constexpr auto pipe_kernel() {
   if constexpr (JOINT)
-    return stencil5_stream_pipe_kernel<joint_s0<S>(), S - joint_s0<S>(), pipe_pf<T, S>(), WRAP, 0, T, SUM,
+    return stencil5_stream_pipe_kernel<joint_s0<T, S>(), S - joint_s0<T, S>(), pipe_pf<T, S>(), WRAP, 0, T, SUM,
                                        kWavesPerBlock, false, true>;
   else
     return stencil5_stream_pipe_kernel<pipe_s0<T, S, SUM>(), S - pipe_s0<T, S, SUM>(), pipe_pf<T, S>(), WRAP, 0, T,
@@ -83,7 +85,7 @@ int pipe_blocks() {
 template <typename T, int S, bool WRAP, bool SUM, bool JOINT = false>
 index_t pipe_share(index_t x0, index_t x1, index_t y0, index_t y1) {
   constexpr int OW = StripShape<T, S, true>::OW;
-  constexpr int OWG = JointShape<joint_s0<S>(), S - joint_s0<S>(), kWavesPerBlock>::OWG;
+  constexpr int OWG = JointShape<joint_s0<T, S>(), S - joint_s0<T, S>(), kWavesPerBlock>::OWG;
   const index_t groups =
       JOINT ? (x1 - x0 + OWG - 1) / OWG : ((x1 - x0 + OW - 1) / OW + kWavesPerBlock - 1) / kWavesPerBlock;
   const int blocks = pipe_blocks<T, S, WRAP, SUM, JOINT>();

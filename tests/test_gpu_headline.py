@@ -284,23 +284,26 @@ def test_warm_and_prepare_leave_the_state_alone(gpu, backend, loopback):
     assert torch.equal(a.core_view(), b.core_view())
 
 
-@pytest.mark.parametrize("w,h,steps,wrap,rect", [
-    (8192, 4096, 24, True, None),                  # 32768^2's split (12 + 12), 9 joint groups + a partial one
-    (8192, 4096, 20, True, None),                  # 8 + 12
-    (2048, 1024, 32, True, None),                  # 16 + 16, PF = 3
-    (2048, 1024, 28, True, None),                  # 12 + 16
-    (300, 200, 24, True, None),                    # one partial group, modulo wrap
-    (8192, 2048, 20, False, None),                 # ghost-ring tile (multi-GPU)
-    (4096, 2048, 24, False, (8, 4088, 24, 2024)),  # interior rectangle
+@pytest.mark.parametrize("w,h,steps,wrap,rect,dtype", [
+    (8192, 4096, 24, True, None, "f32"),           # 32768^2's split (12 + 12), 9 joint groups + a partial one
+    (8192, 4096, 20, True, None, "f32"),           # 12 + 8
+    (2048, 1024, 32, True, None, "f32"),           # 16 + 16, PF = 3
+    (2048, 1024, 28, True, None, "f32"),           # 12 + 16
+    (300, 200, 24, True, None, "f32"),             # one partial group, modulo wrap
+    (8192, 2048, 20, False, None, "f32"),          # ghost-ring tile (multi-GPU)
+    (4096, 2048, 24, False, (8, 4088, 24, 2024), "f32"),  # interior rectangle
+    (4096, 2048, 16, True, None, "f64"),           # fp64 wide lanes, 8 + 8
+    (2048, 1024, 16, False, (8, 2040, 16, 1008), "f64"),
 ])
 @pytest.mark.parametrize("sum_form", [True, False])
-def test_pipe_joint_windows_bitwise_vs_per_strip(gpu, w, h, steps, wrap, rect, sum_form):
+def test_pipe_joint_windows_bitwise_vs_per_strip(gpu, w, h, steps, wrap, rect, dtype, sum_form):
     """Joint stage-1 windows (stage 0's valid columns of a workgroup's 4 strips
     in one LDS row) give the same output bit for bit as the per-strip layout,
     and write nothing outside the rectangle."""
-    g = core().TileGeom.aligned(w, h, 1 if wrap else steps, 1 if wrap else steps, 4)
+    tdt = torch.float32 if dtype == "f32" else torch.float64
+    g = core().TileGeom.aligned(w, h, 1 if wrap else steps, 1 if wrap else steps, tdt.itemsize)
     gen = torch.Generator(device=gpu).manual_seed(w * 3 + steps)
-    src = torch.rand(g.alloc_elems(), generator=gen, device=gpu, dtype=torch.float32)
+    src = torch.rand(g.alloc_elems(), generator=gen, device=gpu, dtype=torch.float64).to(tdt)
     x0, x1, y0, y1 = rect or (0, w, 0, h)
     outs = []
     old = hip().pipe_joint()
@@ -308,7 +311,7 @@ def test_pipe_joint_windows_bitwise_vs_per_strip(gpu, w, h, steps, wrap, rect, s
         for joint in (True, False):
             hip().set_pipe_joint(joint)
             dst = torch.full_like(src, -3.0)
-            hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, x0, x1, y0, y1, 0.2, 0.2, wrap, "f32",
+            hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, x0, x1, y0, y1, 0.2, 0.2, wrap, dtype,
                               torch.cuda.current_stream().cuda_stream, "auto", sum_form)
             assert hip().last_stencil_dispatch() == _expect("stream_pipe", sum_form)
             torch.cuda.synchronize()
