@@ -458,6 +458,9 @@ int main(int argc, char** argv) {
     vs.push_back(n20);
     vs.push_back(joint_vs(pipe<8, 12, 6, false, 0, true, 4, false, true>(in, out, g), n20));
     vs.push_back(joint_vs(pipe<12, 12, 6, false, 0, true, 4, false, true>(in, out, g), n24));
+  } else if (focus && std::string(focus) == "jointpmc") {  // counters: the S = 20 default, per-strip vs joint
+    vs.push_back(pipe<10, 10, 6, true, 0, true>(in, out, g, tmp));
+    vs.push_back(pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g));
   } else if (focus && std::string(focus) == "s24") {  // S = 20 vs 24 (sum form) on large tiles
     vs.push_back(pipe<10, 10, 6, true, 0, true>(in, out, g, tmp));
     vs.push_back(pipe<12, 12, 6, true, 0, true>(in, out, g, tmp));
