@@ -45,9 +45,10 @@ constexpr int pipe_pf() {
 // Joint stage-1 windows (JointShape): fp32 time blocks that split into two
 // multiples of 4 levels, so the joint read reach A0 + A1 equals the per-strip
 // apron SA(S) and the ghost-ring / padding requirements do not change. Splits
-// (tuner, sum form, profiles/r02_joint): 20 = 12 + 8 (32768^2 10.9 vs 10.7 T
-// cells/s for 8 + 12 and 10.0 per-strip 10 + 10; 8 + 12 is 2-3% ahead on the
-// 16384-wide and 8192-wide tiles), 24 = 12 + 12 (11.1 vs 10.2 per-strip),
+// (tuner, sum form, profiles/r02_joint): 20 = 12 + 8 from 24576 columns
+// (32768^2 10.9 vs 10.7 T cells/s for 8 + 12 and 10.0 per-strip 10 + 10), else
+// 8 + 12 (2-3% ahead on the 16384- and 8192-wide tiles), 24 = 12 + 12 (11.1 vs
+// 10.2 per-strip),
 // 28 = 12 + 16 (11.5), 32 = 16 + 16 (11.8; PF = 3).
 // fp64 (wide-lane body, 4 doubles per lane: the same 256-column strips): the
 // sum form's S = 16 as 8 + 8, 944 vs 896 columns per group.
@@ -59,46 +60,49 @@ template <typename T, int S>
 constexpr int joint_s0() {
   return sizeof(T) == 8 ? S / 2 : (S >= 32 ? 16 : 12);
 }
+// Below 24576 columns S = 20 runs 8 + 12 (928 columns per group): 2-3% ahead of
+// 12 + 8 on the 16384- and 8192-wide tiles, 2% behind on 32768^2.
+constexpr index_t kJointWide = 24576;
 
-template <typename T, int S, bool WRAP, bool SUM, bool JOINT = false>
+// JS0: 0 = per-strip layout (pipe_s0 split), else joint windows with S0 = JS0.
+template <typename T, int S, bool WRAP, bool SUM, int JS0 = 0>
 constexpr auto pipe_kernel() {
-  if constexpr (JOINT)
-    return stencil5_stream_pipe_kernel<joint_s0<T, S>(), S - joint_s0<T, S>(), pipe_pf<T, S>(), WRAP, 0, T, SUM,
-                                       kWavesPerBlock, false, true>;
+  if constexpr (JS0 > 0)
+    return stencil5_stream_pipe_kernel<JS0, S - JS0, pipe_pf<T, S>(), WRAP, 0, T, SUM, kWavesPerBlock, false, true>;
   else
     return stencil5_stream_pipe_kernel<pipe_s0<T, S, SUM>(), S - pipe_s0<T, S, SUM>(), pipe_pf<T, S>(), WRAP, 0, T,
                                        SUM>;
 }
 
-template <typename T, int S, bool WRAP, bool SUM, bool JOINT = false>
+template <typename T, int S, bool WRAP, bool SUM, int JS0 = 0>
 int pipe_blocks() {
   static int blocks = 0;
   if (blocks == 0) {
     int occ = 0;
     MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &occ, reinterpret_cast<const void*>(pipe_kernel<T, S, WRAP, SUM, JOINT>()), 2 * kBlock, 0));
+        &occ, reinterpret_cast<const void*>(pipe_kernel<T, S, WRAP, SUM, JS0>()), 2 * kBlock, 0));
     blocks = std::max(occ, 1) * device_cu_count();
   }
   return std::max(1, blocks / gpu_share());
 }
 
-template <typename T, int S, bool WRAP, bool SUM, bool JOINT = false>
+template <typename T, int S, bool WRAP, bool SUM, int JS0 = 0>
 index_t pipe_share(index_t x0, index_t x1, index_t y0, index_t y1) {
   constexpr int OW = StripShape<T, S, true>::OW;
-  constexpr int OWG = JointShape<joint_s0<T, S>(), S - joint_s0<T, S>(), kWavesPerBlock>::OWG;
+  constexpr int OWG = JointShape<(JS0 > 0 ? JS0 : S / 2), S - (JS0 > 0 ? JS0 : S / 2), kWavesPerBlock>::OWG;
   const index_t groups =
-      JOINT ? (x1 - x0 + OWG - 1) / OWG : ((x1 - x0 + OW - 1) / OW + kWavesPerBlock - 1) / kWavesPerBlock;
-  const int blocks = pipe_blocks<T, S, WRAP, SUM, JOINT>();
+      JS0 > 0 ? (x1 - x0 + OWG - 1) / OWG : ((x1 - x0 + OW - 1) / OW + kWavesPerBlock - 1) / kWavesPerBlock;
+  const int blocks = pipe_blocks<T, S, WRAP, SUM, JS0>();
   return (groups * (y1 - y0) + blocks - 1) / blocks;
 }
 
-template <typename T, int S, bool WRAP, bool SUM, bool JOINT>
+template <typename T, int S, bool WRAP, bool SUM, int JS0>
 void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0,
                       T c1, T sc, hipStream_t s) {
-  const index_t share = pipe_share<T, S, WRAP, SUM, JOINT>(x0, x1, y0, y1);
+  const index_t share = pipe_share<T, S, WRAP, SUM, JS0>(x0, x1, y0, y1);
   MXS_CHECK(std::min(share, y1 - y0) * g.pitch * index_t(sizeof(T)) < (index_t(1) << 31),
             "stencil5_tb: a pipeline chunk must stay under 2 GiB (buffer-descriptor stores)");
-  pipe_kernel<T, S, WRAP, SUM, JOINT>()<<<pipe_blocks<T, S, WRAP, SUM, JOINT>(), 2 * kBlock, 0, s>>>(
+  pipe_kernel<T, S, WRAP, SUM, JS0>()<<<pipe_blocks<T, S, WRAP, SUM, JS0>(), 2 * kBlock, 0, s>>>(
       in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, SUM ? sc : c0, c1);
   note_dispatch(SUM ? "stream_pipe_sum" : "stream_pipe");
 }
@@ -107,9 +111,14 @@ template <typename T, int S, bool WRAP, bool SUM>
 void launch_pipe_impl(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
                  T sc, hipStream_t s) {
   if constexpr (pipe_joint_ok<T, S>()) {
-    if (pipe_joint()) return launch_pipe_form<T, S, WRAP, SUM, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+    if (pipe_joint()) {
+      if constexpr (sizeof(T) == 4 && S == 20) {
+        if (x1 - x0 < kJointWide) return launch_pipe_form<T, S, WRAP, SUM, 8>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+      }
+      return launch_pipe_form<T, S, WRAP, SUM, joint_s0<T, S>()>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+    }
   }
-  launch_pipe_form<T, S, WRAP, SUM, false>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+  launch_pipe_form<T, S, WRAP, SUM, 0>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
 }
 
 // Whether the fp64 wide-lane pipeline can take [x0, x1) x [y0, y1) at depth S:

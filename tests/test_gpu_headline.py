@@ -286,7 +286,8 @@ def test_warm_and_prepare_leave_the_state_alone(gpu, backend, loopback):
 
 @pytest.mark.parametrize("w,h,steps,wrap,rect,dtype", [
     (8192, 4096, 24, True, None, "f32"),           # 32768^2's split (12 + 12), 9 joint groups + a partial one
-    (8192, 4096, 20, True, None, "f32"),           # 12 + 8
+    (8192, 4096, 20, True, None, "f32"),           # 8 + 12 (narrower than 24576 columns)
+    (24576, 512, 20, True, None, "f32"),           # 12 + 8 (the 32768^2 split)
     (2048, 1024, 32, True, None, "f32"),           # 16 + 16, PF = 3
     (2048, 1024, 28, True, None, "f32"),           # 12 + 16
     (300, 200, 24, True, None, "f32"),             # one partial group, modulo wrap
