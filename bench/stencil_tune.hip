@@ -458,6 +458,16 @@ int main(int argc, char** argv) {
     vs.push_back(n20);
     vs.push_back(joint_vs(pipe<8, 12, 6, false, 0, true, 4, false, true>(in, out, g), n20));
     vs.push_back(joint_vs(pipe<12, 12, 6, false, 0, true, 4, false, true>(in, out, g), n24));
+  } else if (focus && std::string(focus) == "joint2") {  // joint windows: fetch depth, XCD-major order, priority
+    vs.push_back(pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g));
+    vs.push_back(pipe<12, 8, 3, true, 0, true, 4, false, true>(in, out, g));
+    vs.push_back(pipe<12, 8, 9, true, 0, true, 4, false, true>(in, out, g));
+    vs.push_back(pipe<12, 8, 6, true, 0, true, 4, true, true>(in, out, g));
+    vs.push_back(pipe<12, 8, 6, true, 1, true, 4, false, true>(in, out, g));
+    vs.push_back(pipe<12, 8, 6, true, 2, true, 4, false, true>(in, out, g));
+    vs.push_back(pipe<8, 12, 6, true, 0, true, 4, false, true>(in, out, g));
+    vs.push_back(pipe<8, 12, 9, true, 0, true, 4, false, true>(in, out, g));
+    vs.push_back(pipe<8, 12, 6, true, 0, true, 4, true, true>(in, out, g));
   } else if (focus && std::string(focus) == "jointpmc") {  // counters: the S = 20 default, per-strip vs joint
     vs.push_back(pipe<10, 10, 6, true, 0, true>(in, out, g, tmp));
     vs.push_back(pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g));
