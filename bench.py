@@ -252,6 +252,7 @@ def main(argv=None) -> int:
         from cuda_mpi_scratch_amd import hip
 
         extras["stencil_kernel"] = hip().last_stencil_dispatch()
+        extras["pipe_joint_windows"] = bool(hip().pipe_joint())  # MXS_PIPE_JOINT=0 runs the per-strip layout
     del st
     if gpu:
         torch.cuda.empty_cache()
