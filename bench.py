@@ -256,6 +256,11 @@ def main(argv=None) -> int:
     del st
     if gpu:
         torch.cuda.empty_cache()
+    if ctx.is_root:
+        # The headline is measured; the extras below (dot, ping-pong, 8192^2 tiles)
+        # run after it. Log it now on stderr so a failure in an extra cannot lose it.
+        print(f"headline measured: {value:.3f} Gcells/s, {_ms(dt / args.steps)} ms/step, n_gpus={n}",
+              file=sys.stderr, flush=True)
 
     if not args.no_extras:
         try:
