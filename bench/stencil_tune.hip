@@ -196,19 +196,19 @@ Variant balanced(const float* in, float* out, const TileGeom& g, int per_cu, flo
 
 // Two-stage wave pipeline (S = S0 + S1 levels; 512-thread workgroups).
 template <int S0, int S1, int PF, bool WRAP = true, int PRIO = 0, bool SUM = false, int G = 4, bool XM = false,
-          bool JOINT = false>
+          bool JOINT = false, bool LAG1 = false>
 Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullptr) {
   int per_cu = 0, cus = 0;
   constexpr int threads = 2 * G * kWaveSize;
   MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu, reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM, JOINT>),
+      &per_cu, reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM, JOINT, LAG1>),
       threads, 0));
   MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const int blocks = std::max(1, per_cu * cus);
   char buf[128];
-  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s%s%s%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
+  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s%s%s%s%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
                 PRIO == 1 ? "_prio0" : (PRIO == 2 ? "_prio1" : ""), SUM ? "_sum" : "",
-                G == 4 ? "" : (G == 2 ? "_g2" : "_g1"), XM ? "_xcd" : "", JOINT ? "_joint" : "");
+                G == 4 ? "" : (G == 2 ? "_g2" : "_g1"), XM ? "_xcd" : "", JOINT ? "_joint" : "", LAG1 ? "_lag1" : "");
   const float c0 = SUM ? float(std::pow(0.2, S0 + S1)) : 0.2f;  // sum form: c0 carries c^S
   auto mk = [=](const float* I, float* O) {
     return [=](hipStream_t s) {
@@ -216,7 +216,7 @@ Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullpt
       constexpr int OWG = JointShape<S0, S1, G>::OWG;
       const index_t groups = JOINT ? (g.width + OWG - 1) / OWG : ((g.width + OW - 1) / OW + G - 1) / G;
       const index_t share = (groups * g.height + blocks - 1) / blocks;
-      stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM, JOINT><<<blocks, threads, 0, s>>>(
+      stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM, JOINT, LAG1><<<blocks, threads, 0, s>>>(
           I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, c0, 0.2f);
     };
   };
@@ -468,6 +468,28 @@ int main(int argc, char** argv) {
     vs.push_back(pipe<8, 12, 6, true, 0, true, 4, false, true>(in, out, g));
     vs.push_back(pipe<8, 12, 9, true, 0, true, 4, false, true>(in, out, g));
     vs.push_back(pipe<8, 12, 6, true, 0, true, 4, true, true>(in, out, g));
+  } else if (focus && std::string(focus) == "lag1") {  // ascending level order (1-row lag per level) vs descending
+    // Same arithmetic per cell: every LAG1 variant is checked BITWISE against the
+    // default-order kernel of the same shape.
+    auto vs_plain = [&](Variant v, const Variant& plain) {
+      v.ref = plain.launch;
+      v.tol = 0.f;
+      return v;
+    };
+    const Variant a = pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g);
+    const Variant b = pipe<8, 12, 6, true, 0, true, 4, false, true>(in, out, g);
+    const Variant c = pipe<12, 12, 6, true, 0, true, 4, false, true>(in, out, g);
+    const Variant n = pipe<8, 12, 6, false, 0, true, 4, false, true>(in, out, g);
+    vs.push_back(a);
+    vs.push_back(vs_plain(pipe<12, 8, 6, true, 0, true, 4, false, true, true>(in, out, g), a));
+    vs.push_back(b);
+    vs.push_back(vs_plain(pipe<8, 12, 6, true, 0, true, 4, false, true, true>(in, out, g), b));
+    vs.push_back(c);
+    vs.push_back(vs_plain(pipe<12, 12, 6, true, 0, true, 4, false, true, true>(in, out, g), c));
+    vs.push_back(n);
+    vs.push_back(vs_plain(pipe<8, 12, 6, false, 0, true, 4, false, true, true>(in, out, g), n));
+    vs.push_back(vs_plain(pipe<8, 12, 6, true, 0, false, 4, false, true, true>(in, out, g),
+                          pipe<8, 12, 6, true, 0, false, 4, false, true>(in, out, g)));
   } else if (focus && std::string(focus) == "jointpmc") {  // counters: the S = 20 default, per-strip vs joint
     vs.push_back(pipe<10, 10, 6, true, 0, true>(in, out, g, tmp));
     vs.push_back(pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g));

@@ -146,6 +146,14 @@ int gpu_share();
 // output). MXS_PIPE_JOINT=0 in the environment turns it off at start-up.
 void set_pipe_joint(bool on);
 bool pipe_joint();
+// Ascending level order (one row of lag per level) in the joint fp32 pipeline
+// where it measured faster: S = 20 on chunks of <= 768 rows (small and
+// multi-GPU tiles), S = 24 everywhere (stencil_pipe.hpp). Bitwise equal output.
+// MXS_PIPE_LAG1=0 in the environment turns it off at start-up.
+void set_pipe_lag1(bool on);
+bool pipe_lag1();
+// Whether the most recent stencil launch was a pipeline pass in that order.
+bool last_pipe_lag1();
 
 // Kernel form chosen by the most recent stencil launcher on this host process:
 // "stream_pipe" (the two-stage pipeline: fp32 blocks > 16 steps, the one the

@@ -56,7 +56,11 @@ constexpr int kLdsRows = 16;
 // Host-side record of the kernel form the last stencil launcher picked (the
 // tests assert that their shapes reach the kernel the benchmarks time).
 std::atomic<const char*> g_last_dispatch{"none"};
-inline void note(const char* k) { g_last_dispatch.store(k, std::memory_order_relaxed); }
+std::atomic<bool> g_last_lag1{false};  // the pipeline launcher sets it after note()
+inline void note(const char* k) {
+  g_last_dispatch.store(k, std::memory_order_relaxed);
+  g_last_lag1.store(false, std::memory_order_relaxed);
+}
 
 // Tuned on MI355X with bench/stencil_tune.hip (profiles/stencil_tuning/*.log):
 // short strips whose ROWS+2 row loads are all issued up front beat long rolling
@@ -345,13 +349,21 @@ std::atomic<bool> g_pipe_joint{[] {
   const char* e = std::getenv("MXS_PIPE_JOINT");
   return !(e && std::string(e) == "0");
 }()};
+std::atomic<bool> g_pipe_lag1{[] {
+  const char* e = std::getenv("MXS_PIPE_LAG1");
+  return !(e && std::string(e) == "0");
+}()};
 }  // namespace
 void set_gpu_share(int processes) { g_gpu_share.store(std::max(1, processes), std::memory_order_relaxed); }
 int gpu_share() { return g_gpu_share.load(std::memory_order_relaxed); }
 void set_pipe_joint(bool on) { g_pipe_joint.store(on, std::memory_order_relaxed); }
 bool pipe_joint() { return g_pipe_joint.load(std::memory_order_relaxed); }
+void set_pipe_lag1(bool on) { g_pipe_lag1.store(on, std::memory_order_relaxed); }
+bool pipe_lag1() { return g_pipe_lag1.load(std::memory_order_relaxed); }
+bool last_pipe_lag1() { return g_last_lag1.load(std::memory_order_relaxed); }
 namespace detail {
 void note_dispatch(const char* k) { note(k); }
+void note_pipe_lag1(bool lag1) { g_last_lag1.store(lag1, std::memory_order_relaxed); }
 }  // namespace detail
 
 #define MXS_INST_STENCIL(T)                                                                                    \

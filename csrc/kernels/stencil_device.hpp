@@ -1172,18 +1172,26 @@ struct JointShape {
   static_assert(OWG > 0, "time block too deep for a joint group");
 };
 
-template <typename B, int S0, int S1, int PF, bool WRAP, bool JOINT = false, int G = kWavesPerBlock>
+template <typename B, int S0, int S1, int PF, bool WRAP, bool JOINT = false, int G = kWavesPerBlock, bool LAG1 = false>
 __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in, typename B::T* __restrict__ out,
                                            index_t pitch, index_t core_off, index_t W, index_t H, index_t xw,
                                            index_t x_end, index_t ys, index_t ye, typename B::T c0, typename B::T c1,
                                            typename B::V* __restrict__ ring, int stage, int strip = 0) {
   static_assert(PF % 3 == 0, "the window rotates through 3 slots: PF must be a multiple of 3");
   using P = PipeShape<S0, S1, PF>;
-  constexpr int S = P::S, RING = P::RING, T1 = P::T1;
+  constexpr int S = P::S, RING = P::RING;
   using T = typename B::T;
   using V = typename B::V;
   using Sh = StripShape<T, S, true>;
   using J = JointShape<S0, S1, G>;
+  // Level order within a row iteration. Default: levels descend, so every
+  // level reads only rows of earlier iterations (S independent evaluations per
+  // row, level l lags 3 rows per level: a stage emits its first valid row at
+  // iteration 3 * levels - 1). LAG1: levels ascend and each reads the row its
+  // lower level made in the same iteration (a dependent chain per row), so a
+  // level lags one row and a stage emits its first row at iteration 2 * levels:
+  // S - 1 fewer fill iterations per chunk and stage. Same arithmetic per cell.
+  constexpr int E0 = LAG1 ? 2 * S0 : 3 * S0 - 1, E1 = LAG1 ? 2 * S1 : 3 * S1 - 1;
   constexpr int N = Sh::N, SA = Sh::SA, AL = SA / N;
   static_assert(!JOINT || N == 4, "joint windows assume 4-cell lanes");
   const int lane = threadIdx.x & (kWaveSize - 1);
@@ -1198,9 +1206,11 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
   // Stage 0 starts D rows early so that its ring writes start block-aligned
   // (row k is emitted at iteration 3*S0 - 1 + D + k, a multiple of PF for k = 0):
   // no per-row slot wrap. The lead rows only feed level-S0 rows before ys - S1.
-  constexpr int D = (PF - (3 * S0 - 1) % PF) % PF;
-  const index_t n_it0 = rows + 2 * S1 + 3 * S0 - 1 + D;  // stage 0: level-S0 rows [ys - S1, ye + S1)
-  const index_t n_it1 = rows + 3 * S1 - 1;           // stage 1: output rows [ys, ye)
+  constexpr int D = (PF - E0 % PF) % PF;
+  constexpr int T1 = (E0 + D) / PF + 1;  // stage-1 start block (P::T1 for the default order)
+  static_assert(LAG1 || T1 == P::T1, "stage-1 start block");
+  const index_t n_it0 = rows + 2 * S1 + E0 + D;  // stage 0: level-S0 rows [ys - S1, ye + S1)
+  const index_t n_it1 = rows + E1;               // stage 1: output rows [ys, ye)
   const index_t blocks0 = (n_it0 + PF - 1) / PF, blocks1 = T1 + (n_it1 + PF - 1) / PF;
   const index_t blocks = blocks0 > blocks1 ? blocks0 : blocks1;
   // This lane's slot in a ring row, and the ring's row stride (lane vectors).
@@ -1264,38 +1274,61 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
     for (int q = 0; q < 3; ++q)
 #pragma unroll
       for (int l = 0; l < S0; ++l) win[q][l] = B::zero();
-    constexpr int kWarm = (3 * (S0 - 1)) / PF * PF;  // see stream_chunk_rot: level l matters from iteration 3l + 2
+    // See stream_chunk_rot: level l matters from iteration 3l + 2 (LAG1: 2l).
+    constexpr int kWarm = LAG1 ? (2 * S0) / PF * PF : (3 * (S0 - 1)) / PF * PF;
 #pragma unroll 1
     for (int ib = 0; ib < kWarm; ib += PF) {
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
-        const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
-        const int b = (ib + k) / 3;
-        win[p2][0] = B::enter(pf[k]);
-        pf[k] = fetch();
+        if constexpr (LAG1) {
+          const int n = k % 3, o = (k + 1) % 3, m = (k + 2) % 3;  // rows of iterations j, j-2, j-1
+          const int b = (ib + k) / 2;
+          win[n][0] = B::enter(pf[k]);
+          pf[k] = fetch();
 #pragma unroll
-        for (int l = S0 - 2; l >= 0; --l)
-          if (l <= b) win[p0][l + 1] = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+          for (int l = 0; l < S0 - 1; ++l)
+            if (l < b) win[n][l + 1] = B::jac(win[o][l], win[m][l], win[n][l], c0, c1);
+        } else {
+          const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
+          const int b = (ib + k) / 3;
+          win[p2][0] = B::enter(pf[k]);
+          pf[k] = fetch();
+#pragma unroll
+          for (int l = S0 - 2; l >= 0; --l)
+            if (l <= b) win[p0][l + 1] = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+        }
       }
       __syncthreads();
     }
     // Ring slot of each block's first row k = i - (3*S0 - 1): a wave-uniform
     // counter stepping by PF modulo RING (a 64-bit modulo per block cost ~40
     // scalar instructions).
-    int base = ((kWarm - (3 * S0 - 1 + D)) % RING + RING) % RING;  // 0, PF or 2 PF
+    int base = ((kWarm - (E0 + D)) % RING + RING) % RING;  // 0, PF or 2 PF
 #pragma unroll 1
     for (index_t i = kWarm; i < blocks * PF; i += PF) {
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
-        const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
-        win[p2][0] = B::enter(pf[k]);
-        pf[k] = fetch();
         V top;
+        if constexpr (LAG1) {
+          const int n = k % 3, o = (k + 1) % 3, m = (k + 2) % 3;
+          win[n][0] = B::enter(pf[k]);
+          pf[k] = fetch();
 #pragma unroll
-        for (int l = S0 - 1; l >= 0; --l) {
-          const V o = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
-          if (l == S0 - 1) top = o;
-          else win[p0][l + 1] = o;
+          for (int l = 0; l < S0; ++l) {
+            const V v = B::jac(win[o][l], win[m][l], win[n][l], c0, c1);
+            if (l == S0 - 1) top = v;
+            else win[n][l + 1] = v;
+          }
+        } else {
+          const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
+          win[p2][0] = B::enter(pf[k]);
+          pf[k] = fetch();
+#pragma unroll
+          for (int l = S0 - 1; l >= 0; --l) {
+            const V o = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+            if (l == S0 - 1) top = o;
+            else win[p0][l + 1] = o;
+          }
         }
         // Row k = j - (3*S0 - 1 + D) of stage 1's input (rotated layout);
         // writes for k < 0 land in slots no reader touches before they are
@@ -1335,7 +1368,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
       for (int l = 0; l < S1; ++l) win[q][l] = B::zero();
 #pragma unroll 1
     for (int t = 0; t < T1; ++t) __syncthreads();  // stage 0 fills the ring
-    constexpr int kWarm = (3 * (S1 - 1)) / PF * PF;
+    constexpr int kWarm = LAG1 ? (2 * S1) / PF * PF : (3 * (S1 - 1)) / PF * PF;
 #pragma unroll 1
     for (int ib = 0; ib < kWarm; ib += PF) {
       V inrow[PF];
@@ -1344,12 +1377,21 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
       for (int k = 0; k < PF; ++k) inrow[k] = my[(base + k) * RSTRIDE];
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
-        const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
-        const int b = (ib + k) / 3;
-        win[p2][0] = inrow[k];
+        if constexpr (LAG1) {
+          const int n = k % 3, o = (k + 1) % 3, m = (k + 2) % 3;
+          const int b = (ib + k) / 2;
+          win[n][0] = inrow[k];
 #pragma unroll
-        for (int l = S1 - 2; l >= 0; --l)
-          if (l <= b) win[p0][l + 1] = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+          for (int l = 0; l < S1 - 1; ++l)
+            if (l < b) win[n][l + 1] = B::jac(win[o][l], win[m][l], win[n][l], c0, c1);
+        } else {
+          const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
+          const int b = (ib + k) / 3;
+          win[p2][0] = inrow[k];
+#pragma unroll
+          for (int l = S1 - 2; l >= 0; --l)
+            if (l <= b) win[p0][l + 1] = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+        }
       }
       __syncthreads();
     }
@@ -1363,16 +1405,27 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
         const index_t j = i + k;
-        const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
-        win[p2][0] = inrow[k];
         V top;
+        if constexpr (LAG1) {
+          const int n = k % 3, o = (k + 1) % 3, m = (k + 2) % 3;
+          win[n][0] = inrow[k];
 #pragma unroll
-        for (int l = S1 - 1; l >= 0; --l) {
-          const V o = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
-          if (l == S1 - 1) top = o;
-          else win[p0][l + 1] = o;
+          for (int l = 0; l < S1; ++l) {
+            const V v = B::jac(win[o][l], win[m][l], win[n][l], c0, c1);
+            if (l == S1 - 1) top = v;
+            else win[n][l + 1] = v;
+          }
+        } else {
+          const int p0 = k % 3, p1 = (k + 1) % 3, p2 = (k + 2) % 3;
+          win[p2][0] = inrow[k];
+#pragma unroll
+          for (int l = S1 - 1; l >= 0; --l) {
+            const V o = B::jac(win[p0][l], win[p1][l], win[p2][l], c0, c1);
+            if (l == S1 - 1) top = o;
+            else win[p0][l + 1] = o;
+          }
         }
-        const index_t r = j - (3 * S1 - 1);
+        const index_t r = j - E1;
         const bool ok = store_lane && r >= 0 && r < rows;
         const unsigned off = ok ? lane_off + unsigned(r) * row_bytes : kDrop;
         B::store(top, orsrc, off, c0);
@@ -1395,7 +1448,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 // read the same 2S apron rows, share that XCD's L2.
 // JOINT: joint stage-1 windows (JointShape), OWG output columns per group.
 template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float, bool SUM = false,
-          int G = kWavesPerBlock, bool XM = false, bool JOINT = false>
+          int G = kWavesPerBlock, bool XM = false, bool JOINT = false, bool LAG1 = false>
 __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
@@ -1426,11 +1479,11 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
     const index_t grp = a / rows, r0 = a - grp * rows;
     const index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
     if constexpr (JOINT) {
-      pipe_chunk<B, S0, S1, PF, WRAP, true, G>(in, out, pitch, core_off, W, H, x_begin + grp * OWG, x_end,
+      pipe_chunk<B, S0, S1, PF, WRAP, true, G, LAG1>(in, out, pitch, core_off, W, H, x_begin + grp * OWG, x_end,
                                                y_begin + r0, y_begin + r1, c0, c1, ring, stage, strip);
     } else {
       const index_t xw = x_begin + (grp * G + strip) * OW;
-      pipe_chunk<B, S0, S1, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1,
+      pipe_chunk<B, S0, S1, PF, WRAP, false, G, LAG1>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0, c1,
                                       ring + strip * P::RING * kWaveSize, stage);
     }
     a += r1 - r0;

@@ -16,6 +16,7 @@ namespace kernels {
 namespace detail {
 
 void note_dispatch(const char* kernel);  // stencil.hip: last_stencil_dispatch() record
+void note_pipe_lag1(bool lag1);          // stencil.hip: last_pipe_lag1() record
 
 // fp64 depths the wide-lane pipeline takes (S0 = S/2, S1 = S - S0 <= 8 levels
 // per stage: the windows fit 2 waves/SIMD without spilling).
@@ -60,15 +61,26 @@ template <typename T, int S>
 constexpr int joint_s0() {
   return sizeof(T) == 8 ? S / 2 : (S >= 32 ? 16 : 12);
 }
-// Below 24576 columns S = 20 runs 8 + 12 (928 columns per group): 2-3% ahead of
-// 12 + 8 on the 16384- and 8192-wide tiles, 2% behind on 32768^2.
-constexpr index_t kJointWide = 24576;
+// Level order (LAG1, stencil_device.hpp pipe_chunk): ascending levels lag one
+// row per level instead of three, so a chunk fills its pipeline S - 1 rows
+// sooner per stage, at the cost of a dependent chain of levels per row. It pays
+// on short chunks (tuner focus lag1, 21 interleaved rounds, profiles/r02_lag1):
+// S = 20 on 8192^2 (288-row chunks) 8 + 12: 8.88 -> 9.49 T cells/s, on the
+// 8-GPU tile 16384 x 8192 (576 rows) 12 + 8: 10.21 -> 10.52; with 1152-row
+// chunks (16384^2) and longer the descending order wins (12 + 8: 11.04 vs 10.58;
+// 32768^2: 10.84 vs 10.50). S = 24 (12 + 12) takes LAG1 everywhere (+1.3% on
+// 32768^2, +6-9% on the smaller tiles).
+constexpr index_t kLag1MaxChunk = 768;
+// With LAG1 (short chunks) S = 20 runs 8 + 12 below 12288 columns (8192^2:
+// 9.49 vs 9.36 for 12 + 8), else 12 + 8.
+constexpr index_t kJointWide = 12288;
 
 // JS0: 0 = per-strip layout (pipe_s0 split), else joint windows with S0 = JS0.
-template <typename T, int S, bool WRAP, bool SUM, int JS0 = 0>
+template <typename T, int S, bool WRAP, bool SUM, int JS0 = 0, bool LAG1 = false>
 constexpr auto pipe_kernel() {
   if constexpr (JS0 > 0)
-    return stencil5_stream_pipe_kernel<JS0, S - JS0, pipe_pf<T, S>(), WRAP, 0, T, SUM, kWavesPerBlock, false, true>;
+    return stencil5_stream_pipe_kernel<JS0, S - JS0, pipe_pf<T, S>(), WRAP, 0, T, SUM, kWavesPerBlock, false, true,
+                                       LAG1>;
   else
     return stencil5_stream_pipe_kernel<pipe_s0<T, S, SUM>(), S - pipe_s0<T, S, SUM>(), pipe_pf<T, S>(), WRAP, 0, T,
                                        SUM>;
@@ -96,15 +108,17 @@ index_t pipe_share(index_t x0, index_t x1, index_t y0, index_t y1) {
   return (groups * (y1 - y0) + blocks - 1) / blocks;
 }
 
-template <typename T, int S, bool WRAP, bool SUM, int JS0>
+template <typename T, int S, bool WRAP, bool SUM, int JS0, bool LAG1 = false>
 void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0,
                       T c1, T sc, hipStream_t s) {
   const index_t share = pipe_share<T, S, WRAP, SUM, JS0>(x0, x1, y0, y1);
   MXS_CHECK(std::min(share, y1 - y0) * g.pitch * index_t(sizeof(T)) < (index_t(1) << 31),
             "stencil5_tb: a pipeline chunk must stay under 2 GiB (buffer-descriptor stores)");
-  pipe_kernel<T, S, WRAP, SUM, JS0>()<<<pipe_blocks<T, S, WRAP, SUM, JS0>(), 2 * kBlock, 0, s>>>(
+  // Same workgroup count as the descending-order kernel (one per CU), so `share` holds.
+  pipe_kernel<T, S, WRAP, SUM, JS0, LAG1>()<<<pipe_blocks<T, S, WRAP, SUM, JS0>(), 2 * kBlock, 0, s>>>(
       in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, SUM ? sc : c0, c1);
   note_dispatch(SUM ? "stream_pipe_sum" : "stream_pipe");
+  note_pipe_lag1(LAG1);
 }
 
 template <typename T, int S, bool WRAP, bool SUM>
@@ -113,7 +127,13 @@ void launch_pipe_impl(const T* in, T* out, const TileGeom& g, index_t x0, index_
   if constexpr (pipe_joint_ok<T, S>()) {
     if (pipe_joint()) {
       if constexpr (sizeof(T) == 4 && S == 20) {
-        if (x1 - x0 < kJointWide) return launch_pipe_form<T, S, WRAP, SUM, 8>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+        if (pipe_lag1() && pipe_share<T, S, WRAP, SUM, 12>(x0, x1, y0, y1) <= kLag1MaxChunk) {
+          if (x1 - x0 < kJointWide)
+            return launch_pipe_form<T, S, WRAP, SUM, 8, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+          return launch_pipe_form<T, S, WRAP, SUM, 12, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+        }
+      } else if constexpr (sizeof(T) == 4 && S == 24) {
+        if (pipe_lag1()) return launch_pipe_form<T, S, WRAP, SUM, 12, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
       }
       return launch_pipe_form<T, S, WRAP, SUM, joint_s0<T, S>()>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
     }

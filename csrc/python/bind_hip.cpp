@@ -177,6 +177,11 @@ PYBIND11_MODULE(_mxs_hip, m) {
   m.def("set_pipe_joint", &kernels::set_pipe_joint, py::arg("on"),
         "joint stage-1 windows in the fp32 two-stage pipeline (default on; bitwise equal output)");
   m.def("pipe_joint", &kernels::pipe_joint);
+  m.def("set_pipe_lag1", &kernels::set_pipe_lag1, py::arg("on"),
+        "ascending level order in the joint fp32 pipeline where it pays (default on; bitwise equal output)");
+  m.def("pipe_lag1", &kernels::pipe_lag1);
+  m.def("last_pipe_lag1", &kernels::last_pipe_lag1,
+        "whether the most recent stencil launch was a pipeline pass in ascending level order");
   m.def(
       "stencil5_tb",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0,

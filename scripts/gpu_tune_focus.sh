@@ -9,7 +9,7 @@ mkdir -p gpurun_out/tune_$focus
 for tag in "$@"; do
   shape=$(echo $tag | tr x ' ')
   log=gpurun_out/tune_$focus/${tuner}_$tag.log
-  TUNE_FOCUS=$focus timeout -k 10 400 build/bin/$tuner $shape 7 > $log 2>&1 \
+  TUNE_FOCUS=$focus timeout -k 10 400 build/bin/$tuner $shape ${TUNE_ROUNDS:-7} > $log 2>&1 \
     || { echo "$tuner $tag failed"; tail -20 $log; exit 1; }
   echo "== $tuner $tag"; grep -v mismatches $log | grep -v '"copy_float4\|"lds_th\|"roll_\|"tb1_'
   grep mismatches $log
