@@ -58,17 +58,19 @@ std::function<void(const double*, double*, hipStream_t)> balanced_fn(const TileG
   };
 }
 
-template <int S0, int S1, int PF, bool WRAP, bool SUM = false>
+template <int S0, int S1, int PF, bool WRAP, bool SUM = false, bool JOINT = false, bool LAG1 = false>
 std::function<void(const double*, double*, hipStream_t)> pipe_fn(const TileGeom& g, int* per_cu = nullptr) {
-  const int blocks =
-      resident(reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, 0, double, SUM>), 512);
+  const int blocks = resident(
+      reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, 0, double, SUM, 4, false, JOINT, LAG1>),
+      512);
   if (per_cu) *per_cu = blocks / 256;
   const double c0 = SUM ? std::pow(0.2, S0 + S1) : 0.2;  // sum form: c0 carries c^S
   return [=](const double* I, double* O, hipStream_t s) {
     constexpr int OW = StripShape<double, S0 + S1, true>::OW;
-    const index_t groups = ((g.width + OW - 1) / OW + 3) / 4;
+    constexpr int OWG = JointShape<S0, S1, 4>::OWG;
+    const index_t groups = JOINT ? (g.width + OWG - 1) / OWG : ((g.width + OW - 1) / OW + 3) / 4;
     const index_t share = (groups * g.height + blocks - 1) / blocks;
-    stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, 0, double, SUM><<<blocks, 512, 0, s>>>(
+    stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, 0, double, SUM, 4, false, JOINT, LAG1><<<blocks, 512, 0, s>>>(
         I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, c0, 0.2);
   };
 }
@@ -101,14 +103,14 @@ Variant balanced(const TileGeom& g, double* tmp) {
   return v;
 }
 
-template <int S0, int S1, int PF, bool WRAP, bool SUM = false>
+template <int S0, int S1, int PF, bool WRAP, bool SUM = false, bool JOINT = false, bool LAG1 = false>
 Variant pipe(const TileGeom& g, double* tmp) {
   int per_cu = 0;
   Variant v;
-  v.launch = pipe_fn<S0, S1, PF, WRAP, SUM>(g, &per_cu);
+  v.launch = pipe_fn<S0, S1, PF, WRAP, SUM, JOINT, LAG1>(g, &per_cu);
   char buf[128];
-  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
-                SUM ? "_sum" : "");
+  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
+                SUM ? "_sum" : "", JOINT ? "_joint" : "", LAG1 ? "_lag1" : "");
   v.name = buf;
   v.steps = S0 + S1;
   v.ref = ref_fn<S0 + S1, WRAP>(g, tmp);
@@ -169,6 +171,20 @@ int main(int argc, char** argv) {
     vs.push_back(pipe<7, 7, 6, true>(g, tmp));
     vs.push_back(pipe<8, 6, 3, true>(g, tmp));
     vs.push_back(pipe<8, 8, 3, true>(g, tmp));
+  }
+  if (f == "lag1") {  // ascending level order on the joint sum-form default (8 + 8), bitwise vs descending
+    Variant a = pipe<8, 8, 3, true, true, true>(g, tmp);
+    Variant b = pipe<8, 8, 3, true, true, true, true>(g, tmp);
+    b.ref = a.launch;
+    b.tol = 0.0;
+    Variant c = pipe<6, 6, 3, true, false, false>(g, tmp);
+    Variant d = pipe<6, 6, 3, true, false, false, true>(g, tmp);
+    d.ref = c.launch;
+    d.tol = 0.0;
+    vs.push_back(a);
+    vs.push_back(b);
+    vs.push_back(c);
+    vs.push_back(d);
   }
   if (f == "split") {  // around the 6 + 6 winner of the first pass (profiles/r02_f64)
     vs.push_back(balanced<12, true, false>(g, tmp));

@@ -71,6 +71,9 @@ constexpr int joint_s0() {
 // 32768^2: 10.84 vs 10.50). S = 24 (12 + 12) takes LAG1 everywhere (+1.3% on
 // 32768^2, +6-9% on the smaller tiles).
 constexpr index_t kLag1MaxChunk = 768;
+// fp64 (S = 16 as 8 + 8, wide lanes): 8192^2 (288-row chunks) 3.88 -> 4.00 T
+// cells/s; 576- and 1152-row chunks within +-1.5% (profiles/r02_lag1/*64*).
+constexpr index_t kLag1MaxChunkF64 = 384;
 // With LAG1 (short chunks) S = 20 runs 8 + 12 below 12288 columns (8192^2:
 // 9.49 vs 9.36 for 12 + 8), else 12 + 8.
 constexpr index_t kJointWide = 12288;
@@ -134,6 +137,9 @@ void launch_pipe_impl(const T* in, T* out, const TileGeom& g, index_t x0, index_
         }
       } else if constexpr (sizeof(T) == 4 && S == 24) {
         if (pipe_lag1()) return launch_pipe_form<T, S, WRAP, SUM, 12, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+      } else if constexpr (sizeof(T) == 8 && S == 16) {
+        if (pipe_lag1() && pipe_share<T, S, WRAP, SUM, 8>(x0, x1, y0, y1) <= kLag1MaxChunkF64)
+          return launch_pipe_form<T, S, WRAP, SUM, 8, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
       }
       return launch_pipe_form<T, S, WRAP, SUM, joint_s0<T, S>()>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
     }

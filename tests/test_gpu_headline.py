@@ -326,22 +326,26 @@ def test_pipe_joint_windows_bitwise_vs_per_strip(gpu, w, h, steps, wrap, rect, d
     assert bool((got[mask] == -3.0).all()) and bool((got[~mask] != -3.0).all())
 
 
-@pytest.mark.parametrize("w,h,steps,wrap,rect,lag1", [
-    (8192, 4096, 20, True, None, True),            # short chunks (144 rows), 8 + 12 below 12288 columns
-    (16384, 2048, 20, True, None, True),           # 12 + 8 (the 8-GPU tile's split)
-    (16384, 2048, 20, False, None, True),          # ghost-ring tile (multi-GPU schedule)
-    (8192, 4096, 24, True, None, True),            # S = 24: ascending order at every chunk length
-    (4096, 2048, 24, False, (8, 4088, 24, 2024), True),  # interior rectangle
-    (4096, 49152, 20, True, None, False),          # 960-row chunks: descending order
+@pytest.mark.parametrize("w,h,steps,wrap,rect,dtype,lag1", [
+    (8192, 4096, 20, True, None, "f32", True),     # short chunks (144 rows), 8 + 12 below 12288 columns
+    (16384, 2048, 20, True, None, "f32", True),    # 12 + 8 (the 8-GPU tile's split)
+    (16384, 2048, 20, False, None, "f32", True),   # ghost-ring tile (multi-GPU schedule)
+    (8192, 4096, 24, True, None, "f32", True),     # S = 24: ascending order at every chunk length
+    (4096, 2048, 24, False, (8, 4088, 24, 2024), "f32", True),  # interior rectangle
+    (4096, 49152, 20, True, None, "f32", False),   # 960-row chunks: descending order
+    (4096, 2048, 16, True, None, "f64", True),     # fp64 wide lanes, 8 + 8, short chunks
+    (2048, 1024, 16, False, (8, 2040, 16, 1008), "f64", True),
+    (2048, 40000, 16, True, None, "f64", False),   # 469-row chunks: descending order
 ])
 @pytest.mark.parametrize("sum_form", [True, False])
-def test_pipe_level_order_bitwise(gpu, w, h, steps, wrap, rect, lag1, sum_form):
+def test_pipe_level_order_bitwise(gpu, w, h, steps, wrap, rect, dtype, lag1, sum_form):
     """Ascending level order (one row of lag per level, chosen for short chunks)
     gives the same output bit for bit as the descending order, writes nothing
     outside the rectangle, and is dispatched exactly where the launcher says."""
-    g = core().TileGeom.aligned(w, h, 1 if wrap else steps, 1 if wrap else steps, 4)
+    tdt = torch.float32 if dtype == "f32" else torch.float64
+    g = core().TileGeom.aligned(w, h, 1 if wrap else steps, 1 if wrap else steps, tdt.itemsize)
     gen = torch.Generator(device=gpu).manual_seed(w + 5 * steps)
-    src = torch.rand(g.alloc_elems(), generator=gen, device=gpu, dtype=torch.float32)
+    src = torch.rand(g.alloc_elems(), generator=gen, device=gpu, dtype=torch.float64).to(tdt)
     x0, x1, y0, y1 = rect or (0, w, 0, h)
     outs, used = [], []
     old = hip().pipe_lag1()
@@ -349,7 +353,7 @@ def test_pipe_level_order_bitwise(gpu, w, h, steps, wrap, rect, lag1, sum_form):
         for on in (True, False):
             hip().set_pipe_lag1(on)
             dst = torch.full_like(src, -3.0)
-            hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, x0, x1, y0, y1, 0.2, 0.2, wrap, "f32",
+            hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, x0, x1, y0, y1, 0.2, 0.2, wrap, dtype,
                               torch.cuda.current_stream().cuda_stream, "auto", sum_form)
             assert hip().last_stencil_dispatch() == _expect("stream_pipe", sum_form)
             used.append(hip().last_pipe_lag1())
