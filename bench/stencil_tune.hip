@@ -196,7 +196,7 @@ Variant balanced(const float* in, float* out, const TileGeom& g, int per_cu, flo
 
 // Two-stage wave pipeline (S = S0 + S1 levels; 512-thread workgroups).
 template <int S0, int S1, int PF, bool WRAP = true, int PRIO = 0, bool SUM = false, int G = 4, bool XM = false,
-          bool JOINT = false, bool LAG1 = false>
+          bool JOINT = false, int LAG1 = 0>
 Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullptr) {
   int per_cu = 0, cus = 0;
   constexpr int threads = 2 * G * kWaveSize;
@@ -208,7 +208,7 @@ Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullpt
   char buf[128];
   std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s%s%s%s%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
                 PRIO == 1 ? "_prio0" : (PRIO == 2 ? "_prio1" : ""), SUM ? "_sum" : "",
-                G == 4 ? "" : (G == 2 ? "_g2" : "_g1"), XM ? "_xcd" : "", JOINT ? "_joint" : "", LAG1 ? "_lag1" : "");
+                G == 4 ? "" : (G == 2 ? "_g2" : "_g1"), XM ? "_xcd" : "", JOINT ? "_joint" : "", LAG1 == 3 ? "_lag1" : (LAG1 == 2 ? "_lag1s1" : (LAG1 == 1 ? "_lag1s0" : "")));
   const float c0 = SUM ? float(std::pow(0.2, S0 + S1)) : 0.2f;  // sum form: c0 carries c^S
   auto mk = [=](const float* I, float* O) {
     return [=](hipStream_t s) {
@@ -481,15 +481,45 @@ int main(int argc, char** argv) {
     const Variant c = pipe<12, 12, 6, true, 0, true, 4, false, true>(in, out, g);
     const Variant n = pipe<8, 12, 6, false, 0, true, 4, false, true>(in, out, g);
     vs.push_back(a);
-    vs.push_back(vs_plain(pipe<12, 8, 6, true, 0, true, 4, false, true, true>(in, out, g), a));
+    vs.push_back(vs_plain(pipe<12, 8, 6, true, 0, true, 4, false, true, 3>(in, out, g), a));
     vs.push_back(b);
-    vs.push_back(vs_plain(pipe<8, 12, 6, true, 0, true, 4, false, true, true>(in, out, g), b));
+    vs.push_back(vs_plain(pipe<8, 12, 6, true, 0, true, 4, false, true, 3>(in, out, g), b));
     vs.push_back(c);
-    vs.push_back(vs_plain(pipe<12, 12, 6, true, 0, true, 4, false, true, true>(in, out, g), c));
+    vs.push_back(vs_plain(pipe<12, 12, 6, true, 0, true, 4, false, true, 3>(in, out, g), c));
     vs.push_back(n);
-    vs.push_back(vs_plain(pipe<8, 12, 6, false, 0, true, 4, false, true, true>(in, out, g), n));
-    vs.push_back(vs_plain(pipe<8, 12, 6, true, 0, false, 4, false, true, true>(in, out, g),
+    vs.push_back(vs_plain(pipe<8, 12, 6, false, 0, true, 4, false, true, 3>(in, out, g), n));
+    vs.push_back(vs_plain(pipe<8, 12, 6, true, 0, false, 4, false, true, 3>(in, out, g),
                           pipe<8, 12, 6, true, 0, false, 4, false, true>(in, out, g)));
+  } else if (focus && std::string(focus) == "lag2") {  // per-stage level order (LAG1 mask), bitwise vs descending
+    auto vs_plain = [&](Variant v, const Variant& plain) {
+      v.ref = plain.launch;
+      v.tol = 0.f;
+      return v;
+    };
+    const Variant a = pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g);
+    const Variant b = pipe<8, 12, 6, true, 0, true, 4, false, true>(in, out, g);
+    const Variant c = pipe<12, 12, 6, true, 0, true, 4, false, true>(in, out, g);
+    vs.push_back(a);
+    vs.push_back(vs_plain(pipe<12, 8, 6, true, 0, true, 4, false, true, 1>(in, out, g), a));
+    vs.push_back(vs_plain(pipe<12, 8, 6, true, 0, true, 4, false, true, 2>(in, out, g), a));
+    vs.push_back(vs_plain(pipe<12, 8, 6, true, 0, true, 4, false, true, 3>(in, out, g), a));
+    vs.push_back(b);
+    vs.push_back(vs_plain(pipe<8, 12, 6, true, 0, true, 4, false, true, 2>(in, out, g), b));
+    vs.push_back(vs_plain(pipe<8, 12, 6, true, 0, true, 4, false, true, 3>(in, out, g), b));
+    vs.push_back(c);
+    vs.push_back(vs_plain(pipe<12, 12, 6, true, 0, true, 4, false, true, 2>(in, out, g), c));
+    vs.push_back(vs_plain(pipe<12, 12, 6, true, 0, true, 4, false, true, 3>(in, out, g), c));
+  } else if (focus && std::string(focus) == "lag2head") {  // long-chunk tiles: the S = 20 / 24 candidates
+    const Variant a = pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g);
+    Variant b = pipe<8, 12, 6, true, 0, true, 4, false, true, 2>(in, out, g);
+    b.ref = a.launch;  // same arithmetic per cell whatever the split and order: bitwise
+    b.tol = 0.f;
+    Variant c = pipe<12, 12, 6, true, 0, true, 4, false, true, 2>(in, out, g);
+    vs.push_back(a);
+    vs.push_back(b);
+    vs.push_back(pipe<8, 12, 6, true, 0, true, 4, false, true>(in, out, g));
+    vs.push_back(c);
+    vs.push_back(pipe<12, 12, 6, true, 0, true, 4, false, true, 3>(in, out, g));
   } else if (focus && std::string(focus) == "jointpmc") {  // counters: the S = 20 default, per-strip vs joint
     vs.push_back(pipe<10, 10, 6, true, 0, true>(in, out, g, tmp));
     vs.push_back(pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g));

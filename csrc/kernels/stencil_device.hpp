@@ -1172,7 +1172,7 @@ struct JointShape {
   static_assert(OWG > 0, "time block too deep for a joint group");
 };
 
-template <typename B, int S0, int S1, int PF, bool WRAP, bool JOINT = false, int G = kWavesPerBlock, bool LAG1 = false>
+template <typename B, int S0, int S1, int PF, bool WRAP, bool JOINT = false, int G = kWavesPerBlock, int LAG1 = 0>
 __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in, typename B::T* __restrict__ out,
                                            index_t pitch, index_t core_off, index_t W, index_t H, index_t xw,
                                            index_t x_end, index_t ys, index_t ye, typename B::T c0, typename B::T c1,
@@ -1191,7 +1191,9 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
   // lower level made in the same iteration (a dependent chain per row), so a
   // level lags one row and a stage emits its first row at iteration 2 * levels:
   // S - 1 fewer fill iterations per chunk and stage. Same arithmetic per cell.
-  constexpr int E0 = LAG1 ? 2 * S0 : 3 * S0 - 1, E1 = LAG1 ? 2 * S1 : 3 * S1 - 1;
+  // LAG1 is a stage mask: bit 0 = stage 0 ascends, bit 1 = stage 1 ascends.
+  constexpr bool ASC0 = (LAG1 & 1) != 0, ASC1 = (LAG1 & 2) != 0;
+  constexpr int E0 = ASC0 ? 2 * S0 : 3 * S0 - 1, E1 = ASC1 ? 2 * S1 : 3 * S1 - 1;
   constexpr int N = Sh::N, SA = Sh::SA, AL = SA / N;
   static_assert(!JOINT || N == 4, "joint windows assume 4-cell lanes");
   const int lane = threadIdx.x & (kWaveSize - 1);
@@ -1208,7 +1210,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
   // no per-row slot wrap. The lead rows only feed level-S0 rows before ys - S1.
   constexpr int D = (PF - E0 % PF) % PF;
   constexpr int T1 = (E0 + D) / PF + 1;  // stage-1 start block (P::T1 for the default order)
-  static_assert(LAG1 || T1 == P::T1, "stage-1 start block");
+  static_assert(ASC0 || T1 == P::T1, "stage-1 start block");
   const index_t n_it0 = rows + 2 * S1 + E0 + D;  // stage 0: level-S0 rows [ys - S1, ye + S1)
   const index_t n_it1 = rows + E1;               // stage 1: output rows [ys, ye)
   const index_t blocks0 = (n_it0 + PF - 1) / PF, blocks1 = T1 + (n_it1 + PF - 1) / PF;
@@ -1275,12 +1277,12 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 #pragma unroll
       for (int l = 0; l < S0; ++l) win[q][l] = B::zero();
     // See stream_chunk_rot: level l matters from iteration 3l + 2 (LAG1: 2l).
-    constexpr int kWarm = LAG1 ? (2 * S0) / PF * PF : (3 * (S0 - 1)) / PF * PF;
+    constexpr int kWarm = ASC0 ? (2 * S0) / PF * PF : (3 * (S0 - 1)) / PF * PF;
 #pragma unroll 1
     for (int ib = 0; ib < kWarm; ib += PF) {
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
-        if constexpr (LAG1) {
+        if constexpr (ASC0) {
           const int n = k % 3, o = (k + 1) % 3, m = (k + 2) % 3;  // rows of iterations j, j-2, j-1
           const int b = (ib + k) / 2;
           win[n][0] = B::enter(pf[k]);
@@ -1309,7 +1311,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
         V top;
-        if constexpr (LAG1) {
+        if constexpr (ASC0) {
           const int n = k % 3, o = (k + 1) % 3, m = (k + 2) % 3;
           win[n][0] = B::enter(pf[k]);
           pf[k] = fetch();
@@ -1368,7 +1370,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
       for (int l = 0; l < S1; ++l) win[q][l] = B::zero();
 #pragma unroll 1
     for (int t = 0; t < T1; ++t) __syncthreads();  // stage 0 fills the ring
-    constexpr int kWarm = LAG1 ? (2 * S1) / PF * PF : (3 * (S1 - 1)) / PF * PF;
+    constexpr int kWarm = ASC1 ? (2 * S1) / PF * PF : (3 * (S1 - 1)) / PF * PF;
 #pragma unroll 1
     for (int ib = 0; ib < kWarm; ib += PF) {
       V inrow[PF];
@@ -1377,7 +1379,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
       for (int k = 0; k < PF; ++k) inrow[k] = my[(base + k) * RSTRIDE];
 #pragma unroll
       for (int k = 0; k < PF; ++k) {
-        if constexpr (LAG1) {
+        if constexpr (ASC1) {
           const int n = k % 3, o = (k + 1) % 3, m = (k + 2) % 3;
           const int b = (ib + k) / 2;
           win[n][0] = inrow[k];
@@ -1406,7 +1408,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
       for (int k = 0; k < PF; ++k) {
         const index_t j = i + k;
         V top;
-        if constexpr (LAG1) {
+        if constexpr (ASC1) {
           const int n = k % 3, o = (k + 1) % 3, m = (k + 2) % 3;
           win[n][0] = inrow[k];
 #pragma unroll
@@ -1448,7 +1450,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 // read the same 2S apron rows, share that XCD's L2.
 // JOINT: joint stage-1 windows (JointShape), OWG output columns per group.
 template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float, bool SUM = false,
-          int G = kWavesPerBlock, bool XM = false, bool JOINT = false, bool LAG1 = false>
+          int G = kWavesPerBlock, bool XM = false, bool JOINT = false, int LAG1 = 0>
 __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {

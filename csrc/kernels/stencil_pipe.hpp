@@ -71,6 +71,7 @@ constexpr int joint_s0() {
 // 32768^2: 10.84 vs 10.50). S = 24 (12 + 12) takes LAG1 everywhere (+1.3% on
 // 32768^2, +6-9% on the smaller tiles).
 constexpr index_t kLag1MaxChunk = 768;
+constexpr int kLagBoth = 3;  // LAG1 stage mask: both stages ascend
 // fp64 (S = 16 as 8 + 8, wide lanes): 8192^2 (288-row chunks) 3.88 -> 4.00 T
 // cells/s; 576- and 1152-row chunks within +-1.5% (profiles/r02_lag1/*64*).
 constexpr index_t kLag1MaxChunkF64 = 384;
@@ -79,7 +80,7 @@ constexpr index_t kLag1MaxChunkF64 = 384;
 constexpr index_t kJointWide = 12288;
 
 // JS0: 0 = per-strip layout (pipe_s0 split), else joint windows with S0 = JS0.
-template <typename T, int S, bool WRAP, bool SUM, int JS0 = 0, bool LAG1 = false>
+template <typename T, int S, bool WRAP, bool SUM, int JS0 = 0, int LAG1 = 0>
 constexpr auto pipe_kernel() {
   if constexpr (JS0 > 0)
     return stencil5_stream_pipe_kernel<JS0, S - JS0, pipe_pf<T, S>(), WRAP, 0, T, SUM, kWavesPerBlock, false, true,
@@ -111,7 +112,7 @@ index_t pipe_share(index_t x0, index_t x1, index_t y0, index_t y1) {
   return (groups * (y1 - y0) + blocks - 1) / blocks;
 }
 
-template <typename T, int S, bool WRAP, bool SUM, int JS0, bool LAG1 = false>
+template <typename T, int S, bool WRAP, bool SUM, int JS0, int LAG1 = 0>
 void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0,
                       T c1, T sc, hipStream_t s) {
   const index_t share = pipe_share<T, S, WRAP, SUM, JS0>(x0, x1, y0, y1);
@@ -121,7 +122,7 @@ void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_
   pipe_kernel<T, S, WRAP, SUM, JS0, LAG1>()<<<pipe_blocks<T, S, WRAP, SUM, JS0>(), 2 * kBlock, 0, s>>>(
       in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, SUM ? sc : c0, c1);
   note_dispatch(SUM ? "stream_pipe_sum" : "stream_pipe");
-  note_pipe_lag1(LAG1);
+  note_pipe_lag1(LAG1 != 0);
 }
 
 template <typename T, int S, bool WRAP, bool SUM>
@@ -132,14 +133,14 @@ void launch_pipe_impl(const T* in, T* out, const TileGeom& g, index_t x0, index_
       if constexpr (sizeof(T) == 4 && S == 20) {
         if (pipe_lag1() && pipe_share<T, S, WRAP, SUM, 12>(x0, x1, y0, y1) <= kLag1MaxChunk) {
           if (x1 - x0 < kJointWide)
-            return launch_pipe_form<T, S, WRAP, SUM, 8, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
-          return launch_pipe_form<T, S, WRAP, SUM, 12, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+            return launch_pipe_form<T, S, WRAP, SUM, 8, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+          return launch_pipe_form<T, S, WRAP, SUM, 12, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
         }
       } else if constexpr (sizeof(T) == 4 && S == 24) {
-        if (pipe_lag1()) return launch_pipe_form<T, S, WRAP, SUM, 12, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+        if (pipe_lag1()) return launch_pipe_form<T, S, WRAP, SUM, 12, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
       } else if constexpr (sizeof(T) == 8 && S == 16) {
         if (pipe_lag1() && pipe_share<T, S, WRAP, SUM, 8>(x0, x1, y0, y1) <= kLag1MaxChunkF64)
-          return launch_pipe_form<T, S, WRAP, SUM, 8, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+          return launch_pipe_form<T, S, WRAP, SUM, 8, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
       }
       return launch_pipe_form<T, S, WRAP, SUM, joint_s0<T, S>()>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
     }
