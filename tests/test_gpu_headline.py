@@ -367,3 +367,21 @@ def test_pipe_level_order_bitwise(gpu, w, h, steps, wrap, rect, dtype, lag1, sum
     mask = torch.ones(h, w, dtype=torch.bool, device=gpu)
     mask[y0:y1, x0:x1] = False
     assert bool((got[mask] == -3.0).all()) and bool((got[~mask] != -3.0).all())
+
+
+def test_8192_rate_floor_bottom_up(gpu):
+    """BASELINE config 2 (8192^2 fp32, 1 GPU) as bench.py's extra times it: auto
+    S = 20 on 288-row chunks takes the bottom-up level order (8 + 12). Tuner
+    9.49 T cells/s, bench extra 9.23-9.50 (top-down order: 8.4-8.9)."""
+    st = Stencil2D(StencilConfig(global_width=8192, global_height=8192, dims="1x1", dtype="f32"))
+    assert st.time_block == 20
+    st.run(20)
+    st.prepare(480)
+    st.synchronize()
+    t0 = time.perf_counter()
+    st.run(480)
+    st.synchronize()
+    rate = st.cells_per_step * 480 / (time.perf_counter() - t0) / 1e9
+    assert hip().last_stencil_dispatch() == "stream_pipe_sum"
+    assert hip().last_pipe_lag1()
+    assert rate > 7500, f"{rate:.0f} Gcells/s"
