@@ -253,6 +253,8 @@ def main(argv=None) -> int:
 
         extras["stencil_kernel"] = hip().last_stencil_dispatch()
         extras["pipe_joint_windows"] = bool(hip().pipe_joint())  # MXS_PIPE_JOINT=0 runs the per-strip layout
+        # Level order of the last pipeline pass (bottom-up on short chunks, MXS_PIPE_LAG1=0 disables it).
+        extras["pipe_level_order"] = "bottom-up" if hip().last_pipe_lag1() else "top-down"
     del st
     if gpu:
         torch.cuda.empty_cache()
