@@ -192,6 +192,9 @@ def main(argv=None) -> int:
                    help="per-step evaluation in the time-blocked kernels (bitwise equal to S single steps; "
                         "default: the sum form, c^S applied once per pass, for the equal default coefficients)")
     p.add_argument("--no-overlap", action="store_true")
+    p.add_argument("--no-frame-overlap", action="store_true",
+                   help="multi-GPU: exchange the halo before each pass (serial) instead of under the pass "
+                        "(frame-first overlap, the default)")
     p.add_argument("--overlap", action="store_true", help="force the interior/exchange overlap schedule")
     p.add_argument("--loopback", action="store_true",
                    help="1 GPU: route the self-neighbour halos through RCCL (exercises the multi-GPU schedule)")
@@ -233,18 +236,25 @@ def main(argv=None) -> int:
                         overlap=False if args.no_overlap else (True if args.overlap else None),
                         graph=not args.no_graph,
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback,
-                        sum_form=not args.no_sum_form)
+                        sum_form=not args.no_sum_form, frame_overlap=not args.no_frame_overlap)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3)
+    timed_blocks = st.last_run_blocks()  # the super-steps the timed window executed
     value = st.cells_per_step * args.steps / dt / 1e9
     halo = st.halo_mode()
     exchange = ("none: 1x1 periodic self-exchange fused into the kernel addressing"
                 if st.solver is not None and st.solver.fused_periodic()
                 else f"{st.backend} point-to-point per neighbour")
+    sum_used = st.sum_form_active
     extras: dict = {"backend": st.backend, "halo": halo, "halo_exchange": exchange, "graph": st.graph_status(),
                     "time_block": st.time_block,
+                    # What the K timed steps ran: S-step passes (one exchange each), e.g. [[20, 1]]
+                    # for a 20-step window on a tile whose block is 24.
+                    "timed_super_steps": [list(b) for b in timed_blocks],
+                    "sum_form_used": sum_used,
                     "evaluation": ("sum form: 5-point sums per level, c^S applied once per pass (c_center == "
-                                   "c_neighbor = 0.2)" if st.sum_form else "per step: fma(c_n, (n+s)+(w+e), c_c*c)"),
+                                   "c_neighbor = 0.2; range-guarded: 5|c| <= 1, max|u| 5^S < FLT_MAX/4)"
+                                   if sum_used else "per step: fma(c_n, (n+s)+(w+e), c_c*c)"),
                     "clock_warmup_ms": args.clock_warmup_ms,
                     "tile": f"{st.decomp.width}x{st.decomp.height}",
                     "process_grid": f"{rows} rows x {cols} cols of ranks"}
@@ -255,6 +265,9 @@ def main(argv=None) -> int:
         extras["pipe_joint_windows"] = bool(hip().pipe_joint())  # MXS_PIPE_JOINT=0 runs the per-strip layout
         # Level order of the last pipeline pass (bottom-up on short chunks, MXS_PIPE_LAG1=0 disables it).
         extras["pipe_level_order"] = "bottom-up" if hip().last_pipe_lag1() else "top-down"
+        extras["pipe_balanced_shares"] = bool(hip().pipe_balanced())  # MXS_PIPE_BALANCED=0: equal row shares
+        if st.solver is not None and not st.solver.fused_periodic():
+            extras["frame_overlap"] = bool(timed_blocks and st.solver.frame_overlap(timed_blocks[0][0]))
     del st
     if gpu:
         torch.cuda.empty_cache()
@@ -272,6 +285,14 @@ def main(argv=None) -> int:
         _sync()
         ctx.barrier()
         if gpu:
+            torch.cuda.empty_cache()
+        if n == 1 and gpu and args.global_ == "32768x32768" and not args.no_sum_form:
+            # The general rate on record: the same 20-step window in the per-step
+            # form (valid for any coefficients; the headline's sum form needs
+            # c_center == c_neighbor).
+            extras["stencil_32768sq_f32_per_step_gcells_per_s"] = round(
+                stencil_rate(ctx, 32768, 32768, "f32", args.steps, args.warmup, args.clock_warmup_ms / 1e3,
+                             time_block=args.time_block, sum_form=False), 2)
             torch.cuda.empty_cache()
         if n == 1 and gpu:
             # 480 steps: a multiple of the fp32 (20) and fp64 (16) default blocks,

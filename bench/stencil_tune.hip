@@ -17,7 +17,7 @@
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
 #include "mxs/runtime/hip_utils.hpp"
-#include "../csrc/kernels/stencil_device.hpp"
+#include "../csrc/kernels/stencil_pipe.hpp"
 
 using namespace mxs;
 using namespace mxs::kernels::detail;
@@ -216,8 +216,13 @@ Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullpt
       constexpr int OWG = JointShape<S0, S1, G>::OWG;
       const index_t groups = JOINT ? (g.width + OWG - 1) / OWG : ((g.width + OW - 1) / OW + G - 1) / G;
       const index_t share = (groups * g.height + blocks - 1) / blocks;
+      // The production shares (fill-aware starts unless MXS_PIPE_BALANCED=0; XM
+      // permutes workgroups, so it keeps equal shares).
+      PipeShares shares = PipeShares::equal(share);
+      if (!XM && G == kWavesPerBlock && pipe_balanced() && blocks <= kMaxShareBlocks)
+        pipe_starts(groups, g.height, blocks, pipe_fill_rows<S0, S1, PF, LAG1>(), &shares);
       stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM, JOINT, LAG1><<<blocks, threads, 0, s>>>(
-          I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, c0, 0.2f);
+          I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, shares, c0, 0.2f);
     };
   };
   Variant v{buf, mk(in, out)};

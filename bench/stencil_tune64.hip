@@ -21,7 +21,7 @@
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
 #include "mxs/runtime/hip_utils.hpp"
-#include "../csrc/kernels/stencil_device.hpp"
+#include "../csrc/kernels/stencil_pipe.hpp"
 
 using namespace mxs;
 using namespace mxs::kernels::detail;
@@ -70,8 +70,11 @@ std::function<void(const double*, double*, hipStream_t)> pipe_fn(const TileGeom&
     constexpr int OWG = JointShape<S0, S1, 4>::OWG;
     const index_t groups = JOINT ? (g.width + OWG - 1) / OWG : ((g.width + OW - 1) / OW + 3) / 4;
     const index_t share = (groups * g.height + blocks - 1) / blocks;
+    PipeShares shares = PipeShares::equal(share);
+    if (pipe_balanced() && blocks <= kMaxShareBlocks)
+      pipe_starts(groups, g.height, blocks, pipe_fill_rows<S0, S1, PF, LAG1>(), &shares);
     stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, 0, double, SUM, 4, false, JOINT, LAG1><<<blocks, 512, 0, s>>>(
-        I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, share, c0, 0.2);
+        I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, shares, c0, 0.2);
   };
 }
 

@@ -41,6 +41,14 @@ namespace mxs {
 // rank order.
 using HostAllgather = std::function<std::vector<std::string>(const std::string&)>;
 
+// Collective. The IPC halos (this transport and halo/ipc_direct.hpp) write a
+// neighbour's memory with device stores and hand it over with flags; that is
+// verified for ranks sharing one GPU (tests/test_gpu_multirank.py), not yet
+// across GPUs over xGMI. Ranks on different devices therefore refuse unless
+// MXS_IPC_CROSS_DEVICE=1 opts in (then a warning is printed). Returns whether
+// some peer is on another device.
+bool ipc_check_devices(const HostAllgather& allgather, int rank, const char* what);
+
 template <typename T>
 class IpcHaloTransport {
  public:

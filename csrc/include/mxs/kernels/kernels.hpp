@@ -13,7 +13,10 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <cstdint>
+
 #include "mxs/grid/layout.hpp"
+#include "mxs/kernels/frame_schedule.hpp"
 
 namespace mxs {
 namespace kernels {
@@ -127,6 +130,47 @@ template <typename T>
 void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0, index_t y1,
                  Stencil5Coeffs c, bool wrap, hipStream_t s, StencilVariant v = StencilVariant::Auto);
 
+// --------------------------------------- overlapped multi-GPU pass (frame first)
+// The S-step pass over the whole core of a ghost-ring tile (no wrap) on the
+// two-stage pipeline, with the workgroups' chunks ordered by a FrameSchedule
+// (kernels/frame_schedule.hpp): the chunks that produce the S-deep output
+// frame run first, each workgroup adds 1 to *counter once its frame chunks are
+// stored (agent-scope release), and `comm_wgs` frame-only workgroups exit
+// early so the halo exchange's kernels get CUs while the pass continues.
+// Bitwise identical to stencil5_tb over the same core (same per-cell
+// arithmetic, same kernel body; only the chunk order differs).
+struct FramePassShape {
+  int steps = 0;
+  bool sum = false;   // sum form (c_center == c_neighbor and allowed)
+  int js0 = 0;        // stage-0 levels of the joint windows
+  int lag1 = 0;       // level-order mask (stencil_pipe.hpp)
+  int blocks = 0;     // resident workgroups (one per CU)
+  index_t groups = 0;  // column groups of OWG output columns over the core width
+  index_t owg = 0;
+  index_t fill = 0;    // pipeline-fill row iterations per chunk
+};
+// False when `steps` has no frame-first form here (fp32 S = 20 / 24, fp64
+// S = 16 on whole lane vectors; other depths keep the serial schedule). The
+// caller still has to keep every chunk of its schedule under 2 GiB (rows x
+// pitch: the kernel's buffer-descriptor stores).
+template <typename T>
+bool frame_pass_shape(const TileGeom& g, int steps, const Stencil5Coeffs& c, FramePassShape* out);
+// table: shape.blocks x entries chunks in device memory (FrameSchedule::table).
+template <typename T>
+void stencil5_frame_pass(const T* in, T* out, const TileGeom& g, const Stencil5Coeffs& c, const FramePassShape& shape,
+                         const FrameChunk* table, int entries, unsigned* counter, hipStream_t s);
+// One lane spins (device deadline of `timeout_ticks` wall-clock ticks, then
+// *status = 1) until *counter >= target, then resets *counter to 0: the comm
+// stream's wait for a frame_pass running on another stream.
+void wait_counter(unsigned* counter, unsigned target, std::uint64_t timeout_ticks, unsigned* status, hipStream_t s);
+// Device wall-clock ticks per second (the deadline unit above).
+double wall_clock_hz();
+
+// max |x[i]| over n elements into *out (device pointer, overwritten; NaN if
+// any element is NaN): the range check of the sum form.
+template <typename T>
+void absmax(const T* x, index_t n, T* out, hipStream_t s);
+
 // Update an arbitrary core rectangle [x0, x1) x [y0, y1) (scalar path; used for the
 // boundary columns of the overlapped schedule and for tiny tiles).
 template <typename T>
@@ -154,6 +198,12 @@ void set_pipe_lag1(bool on);
 bool pipe_lag1();
 // Whether the most recent stencil launch was a pipeline pass in that order.
 bool last_pipe_lag1();
+// Fill-aware workgroup shares of the pipeline passes (frame_schedule.hpp:
+// balanced_starts; default on): a share that crosses a column-group boundary
+// pays a second pipeline fill, and with equal row shares those workgroups set
+// the pass time. MXS_PIPE_BALANCED=0 restores equal shares. Bitwise equal output.
+void set_pipe_balanced(bool on);
+bool pipe_balanced_on();
 
 // Kernel form chosen by the most recent stencil launcher on this host process:
 // "stream_pipe" (the two-stage pipeline: fp32 blocks > 16 steps, the one the

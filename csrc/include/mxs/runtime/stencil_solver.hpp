@@ -40,14 +40,43 @@
 // grid fuses the self-exchange into the kernel's wrap-around addressing
 // (`fuse_periodic_self`).
 //
+// Frame-first overlap (`frame_overlap`, the multi-GPU default): with remote
+// peers over RCCL and a depth that has a frame form (fp32 S = 20 / 24, fp64
+// S = 16: kernels::frame_pass_shape), a super-step is one pass on the side
+// stream whose chunk order (kernels/frame_schedule.hpp) stores the S-deep output
+// frame first and signals a device counter; the main stream waits for that
+// counter and exchanges the NEXT super-step's halo (pack -> RCCL -> unpack of
+// nxt) while the pass finishes the interior:
+//
+//   side stream : wait(fork) -> frame-first pass cur -> nxt -> record(done)
+//   main stream : record(fork) -> wait_counter -> pack(nxt) -> RCCL -> unpack(nxt)
+//                 -> wait(done)
+//
+// so cur's ghost ring is fresh whenever a pass starts (the first pass of a run
+// is preceded by one exchange when it is not: construction, field_changed(), a
+// serial super-step). The pass is submitted before the counter wait, so even
+// streams that share a hardware queue cannot deadlock (the wait then just runs
+// after the pass). These super-steps are launched eagerly, not from a graph,
+// for the same reason: a graph's branches are dispatched in an order the host
+// does not choose.
+//
+// Sum-form guard: the sum form sums S levels unscaled (magnitudes up to
+// 5^S max|u|) and scales by c^S once. It runs only when 5 |c| <= 1 (the
+// operator is a max-norm contraction, so max|u| never grows), c^S is a normal
+// number of T and max|u| 5^S < max(T) / 4; max|u| is measured (absmax kernel)
+// before the first run and again after field_changed(). Otherwise every pass
+// takes the per-step form.
+//
 // `use_graph`: `graph_supersteps` consecutive super-steps (auto: ~1 ms of work)
 // are captured once per buffer orientation into a hipGraph and replayed
 // (launch-bound inner loops, Guideline 9). If capture fails
 // (e.g. an RCCL build without graph support) the solver falls back to eager launches.
 #pragma once
 
+#include <cstdint>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "mxs/halo/exchange.hpp"
@@ -86,6 +115,13 @@ struct SolverConfig {
   // neighbours' ghost rings and publishes a ready counter; the next pass waits
   // for the neighbours' counters. Replaces pack -> put -> wait -> unpack.
   bool direct_halo = false;
+  // Frame-first overlap of the RCCL halo with the pass (see above).
+  bool frame_overlap = true;
+  // Frame-only workgroups that exit early and leave their CUs to the exchange
+  // (-1: MXS_FRAME_COMM_WGS or 8), and the frame chunk height (0: MXS_FRAME_ROWS
+  // or auto, kernels::make_frame_schedule).
+  int frame_comm_wgs = -1;
+  int frame_rows = 0;
 };
 
 template <typename T>
@@ -113,6 +149,13 @@ class StencilSolver {
   void warm(int iters, int passes);
   void exchange_only();   // enqueue a halo exchange of the current tile (no update)
   void synchronize();     // wait for everything enqueued so far
+  // The caller wrote the field (checkpoint load, initial data, any direct
+  // write): the next run re-exchanges the ghost ring before its first
+  // frame-first pass and re-checks the sum form's range.
+  void field_changed() {
+    ghost_fresh_ = false;
+    range_checked_ = false;
+  }
 
   T* current() const { return cur_; }
   T* other() const { return nxt_; }
@@ -124,6 +167,17 @@ class StencilSolver {
   bool fused_periodic() const { return fused_; }
   bool direct_halo() const { return direct_ != nullptr; }
   bool overlapped() const { return cfg_.overlap; }
+  // Whether super-steps of depth S run the frame-first overlapped schedule.
+  bool frame_overlap(int S) const;
+  // Whether the passes currently take the sum form (coefficients, user choice
+  // and the measured range all allow it).
+  bool sum_form_active() const { return cfg_.coeffs.sum_form && kernels::uses_sum_form(cfg_.coeffs); }
+  // Why the sum form is off when the coefficients are equal ("" when on).
+  const std::string& sum_form_note() const { return sum_note_; }
+  // (S, count) of the super-steps the last run() enqueued.
+  std::vector<std::pair<int, int>> last_run_blocks() const { return last_blocks_; }
+  // Frame schedule of depth S (building it if needed); nullptr: serial.
+  const kernels::FrameSchedule* frame_schedule(int S);
   int time_block() const { return block_; }
   int graph_supersteps() const { return chain_; }
   index_t cells_per_iteration() const { return tile_.width * tile_.height; }
@@ -151,6 +205,29 @@ class StencilSolver {
   };
   void split(int iters, Group out[2]) const;
   void run_group(int S, int count);
+
+  // Frame-first pass of depth S: shape + schedule + device table.
+  struct FramePass {
+    int S = 0;
+    kernels::FramePassShape shape;
+    kernels::FrameSchedule sched;
+    DeviceBuffer<kernels::FrameChunk> table;
+  };
+  FramePass* frame_pass(int S, bool build);  // nullptr: serial schedule for S
+  void ensure_range();                       // sum-form range check (host sync)
+  void begin_run();                          // range check + prime
+  bool frame_allowed_ = false;               // config / backend / peers allow the overlap
+  std::vector<std::unique_ptr<FramePass>> frames_;
+  std::vector<int> no_frame_;                // depths without a frame form
+  DeviceBuffer<unsigned> frame_ctl_;         // [0] frame counter, [1] wait deadline status
+  std::uint64_t frame_timeout_ticks_ = 0;
+  bool ghost_fresh_ = false;                 // cur_'s ghost ring holds the neighbours' current bands
+  bool range_checked_ = false;
+  bool user_sum_ = true;                     // the caller allows the sum form
+  bool sum_coeffs_ok_ = false;               // 5|c| <= 1 and c^S normal
+  std::string sum_note_;
+  DeviceBuffer<T> absmax_;
+  std::vector<std::pair<int, int>> last_blocks_;
 
   TileGeom tile_;
   SolverConfig cfg_;

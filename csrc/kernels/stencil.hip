@@ -39,6 +39,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <string>
+#include <vector>
 
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
@@ -353,6 +354,10 @@ std::atomic<bool> g_pipe_lag1{[] {
   const char* e = std::getenv("MXS_PIPE_LAG1");
   return !(e && std::string(e) == "0");
 }()};
+std::atomic<bool> g_pipe_balanced{[] {
+  const char* e = std::getenv("MXS_PIPE_BALANCED");
+  return !(e && std::string(e) == "0");
+}()};
 }  // namespace
 void set_gpu_share(int processes) { g_gpu_share.store(std::max(1, processes), std::memory_order_relaxed); }
 int gpu_share() { return g_gpu_share.load(std::memory_order_relaxed); }
@@ -361,7 +366,28 @@ bool pipe_joint() { return g_pipe_joint.load(std::memory_order_relaxed); }
 void set_pipe_lag1(bool on) { g_pipe_lag1.store(on, std::memory_order_relaxed); }
 bool pipe_lag1() { return g_pipe_lag1.load(std::memory_order_relaxed); }
 bool last_pipe_lag1() { return g_last_lag1.load(std::memory_order_relaxed); }
+void set_pipe_balanced(bool on) { g_pipe_balanced.store(on, std::memory_order_relaxed); }
+bool pipe_balanced_on() { return g_pipe_balanced.load(std::memory_order_relaxed); }
 namespace detail {
+bool pipe_balanced() { return g_pipe_balanced.load(std::memory_order_relaxed); }
+void pipe_starts(index_t groups, index_t rows, int blocks, index_t fill, PipeShares* out) {
+  struct Entry {
+    index_t groups, rows, fill;
+    int blocks;
+    std::vector<std::int64_t> start;
+  };
+  thread_local std::vector<Entry> cache;
+  const Entry* hit = nullptr;
+  for (const auto& e : cache)
+    if (e.groups == groups && e.rows == rows && e.fill == fill && e.blocks == blocks) hit = &e;
+  if (!hit) {
+    if (cache.size() >= 16) cache.erase(cache.begin());
+    cache.push_back(Entry{groups, rows, fill, blocks, balanced_starts(groups, rows, blocks, fill)});
+    hit = &cache.back();
+  }
+  out->n = blocks;
+  for (int w = 0; w <= blocks; ++w) out->start[w] = int(hit->start[size_t(w)]);
+}
 void note_dispatch(const char* k) { note(k); }
 void note_pipe_lag1(bool lag1) { g_last_lag1.store(lag1, std::memory_order_relaxed); }
 }  // namespace detail

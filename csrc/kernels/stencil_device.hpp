@@ -1449,11 +1449,28 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 // congruent mod 8) take consecutive shares, so vertically adjacent chunks, which
 // read the same 2S apron rows, share that XCD's L2.
 // JOINT: joint stage-1 windows (JointShape), OWG output columns per group.
+// Workgroup ranges of the linear (group x rows) space: equal shares of `share`
+// rows (n == 0), or explicit fill-aware starts (kernels/frame_schedule.hpp:
+// balanced_starts), start[w] .. start[w + 1] for workgroup w — passed by value
+// in the kernel arguments (2 KB), so a launch needs no device table and stays
+// graph-capturable.
+constexpr int kMaxShareBlocks = 512;
+struct PipeShares {
+  index_t share = 0;
+  int n = 0;
+  int start[kMaxShareBlocks + 1];
+  static PipeShares equal(index_t share) {
+    PipeShares p;
+    p.share = share;
+    return p;
+  }
+};
+
 template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float, bool SUM = false,
           int G = kWavesPerBlock, bool XM = false, bool JOINT = false, int LAG1 = 0>
 __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
-    index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
+    index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, const PipeShares shares, T c0, T c1) {
   using P = PipeShape<S0, S1, PF>;
   using B = typename FastBody<T, SUM>::type;
   constexpr int OW = StripShape<T, P::S, true>::OW;
@@ -1474,8 +1491,14 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
   if constexpr (XM) {
     if (gridDim.x % kNumXcds == 0) slot = (blockIdx.x % kNumXcds) * (gridDim.x / kNumXcds) + blockIdx.x / kNumXcds;
   }
-  index_t a = slot * share;
-  const index_t b = a + share < total ? a + share : total;
+  index_t a, b;
+  if (shares.n > 0) {
+    a = shares.start[slot];
+    b = shares.start[slot + 1];
+  } else {
+    a = slot * shares.share;
+    b = a + shares.share < total ? a + shares.share : total;
+  }
 #pragma unroll 1
   while (a < b) {  // workgroup-uniform: all 8 waves take every chunk (barriers inside)
     const index_t grp = a / rows, r0 = a - grp * rows;
@@ -1489,6 +1512,44 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
                                       ring + strip * P::RING * kWaveSize, stage);
     }
     a += r1 - r0;
+  }
+}
+
+// Frame-first pass of the overlapped multi-GPU schedule (kernels/frame_schedule.hpp):
+// the joint-window pipeline of stencil5_stream_pipe_kernel (ghost-ring tile, no
+// wrap) over an explicit chunk list per workgroup instead of an equal share.
+// After a chunk flagged kFrameSignal the workgroup publishes what it stored —
+// every storing wave drains its stores, the workgroup meets, one lane releases
+// at agent scope and adds 1 to `counter` (MI355X_MICROARCH.md, producer form)
+// — so the halo exchange of those cells can start while the pass goes on.
+template <int S0, int S1, int PF, typename T, bool SUM, int LAG1>
+__global__ __launch_bounds__(2 * kWavesPerBlock * kWaveSize) void stencil5_pipe_frame_kernel(
+    const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
+    index_t x_begin, index_t x_end, index_t y_begin, const FrameChunk* __restrict__ table, int entries,
+    unsigned* __restrict__ counter, T c0, T c1) {
+  constexpr int G = kWavesPerBlock;
+  using P = PipeShape<S0, S1, PF>;
+  using B = typename FastBody<T, SUM>::type;
+  constexpr int OWG = JointShape<S0, S1, G>::OWG;
+  __shared__ typename B::V ring[G * P::RING * kWaveSize];
+  const int wave = threadIdx.x / kWaveSize;
+  const int strip = wave % G, stage = wave / G;
+  const FrameChunk* __restrict__ mine = table + index_t(blockIdx.x) * entries;
+#pragma unroll 1
+  for (int e = 0; e < entries; ++e) {  // workgroup-uniform
+    const FrameChunk c = mine[e];
+    if (c.r1 <= c.r0) break;  // lists are packed from slot 0
+    pipe_chunk<B, S0, S1, PF, false, true, G, LAG1>(in, out, pitch, core_off, W, H, x_begin + index_t(c.group) * OWG,
+                                                   x_end, y_begin + c.r0, y_begin + c.r1, c0, c1, ring, stage, strip);
+    if (c.flags & kFrameSignal) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
   }
 }
 

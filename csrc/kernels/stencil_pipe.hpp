@@ -112,15 +112,45 @@ index_t pipe_share(index_t x0, index_t x1, index_t y0, index_t y1) {
   return (groups * (y1 - y0) + blocks - 1) / blocks;
 }
 
+// Row iterations a chunk of R rows costs beyond R (pipe_chunk: the longer of
+// the two stages' block counts, rounded up to a block).
+template <int S0, int S1, int PF, int LAG1>
+constexpr index_t pipe_fill_rows() {
+  constexpr bool A0 = (LAG1 & 1) != 0, A1 = (LAG1 & 2) != 0;
+  constexpr int E0 = A0 ? 2 * S0 : 3 * S0 - 1, E1 = A1 ? 2 * S1 : 3 * S1 - 1;
+  constexpr int D = (PF - E0 % PF) % PF;
+  constexpr int T1 = (E0 + D) / PF + 1;
+  constexpr int a = 2 * S1 + E0 + D, b = T1 * PF + E1;
+  return (a > b ? a : b) + PF - 1;
+}
+
+// Fill-aware shares (balanced_starts), memoised per shape: the binary search
+// costs ~10 us of host time, a launch must not.
+void pipe_starts(index_t groups, index_t rows, int blocks, index_t fill, PipeShares* out);
+
+// MXS_PIPE_BALANCED=0: equal row shares (the round-2 rule), for comparison.
+bool pipe_balanced();
+
 template <typename T, int S, bool WRAP, bool SUM, int JS0, int LAG1 = 0>
 void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0,
                       T c1, T sc, hipStream_t s) {
   const index_t share = pipe_share<T, S, WRAP, SUM, JS0>(x0, x1, y0, y1);
-  MXS_CHECK(std::min(share, y1 - y0) * g.pitch * index_t(sizeof(T)) < (index_t(1) << 31),
+  const int blocks = pipe_blocks<T, S, WRAP, SUM, JS0>();
+  PipeShares shares = PipeShares::equal(share);
+  index_t chunk = std::min(share, y1 - y0);
+  if (pipe_balanced() && blocks <= kMaxShareBlocks) {
+    constexpr int S0 = JS0 > 0 ? JS0 : pipe_s0<T, S, SUM>();
+    constexpr int OW = StripShape<T, S, true>::OW;
+    constexpr int OWG = JointShape<(JS0 > 0 ? JS0 : S / 2), S - (JS0 > 0 ? JS0 : S / 2), kWavesPerBlock>::OWG;
+    const index_t groups =
+        JS0 > 0 ? (x1 - x0 + OWG - 1) / OWG : ((x1 - x0 + OW - 1) / OW + kWavesPerBlock - 1) / kWavesPerBlock;
+    pipe_starts(groups, y1 - y0, blocks, pipe_fill_rows<S0, S - S0, pipe_pf<T, S>(), LAG1>(), &shares);
+    for (int w = 0; w < shares.n; ++w) chunk = std::max<index_t>(chunk, std::min<index_t>(y1 - y0, shares.start[w + 1] - shares.start[w]));
+  }
+  MXS_CHECK(chunk * g.pitch * index_t(sizeof(T)) < (index_t(1) << 31),
             "stencil5_tb: a pipeline chunk must stay under 2 GiB (buffer-descriptor stores)");
-  // Same workgroup count as the descending-order kernel (one per CU), so `share` holds.
-  pipe_kernel<T, S, WRAP, SUM, JS0, LAG1>()<<<pipe_blocks<T, S, WRAP, SUM, JS0>(), 2 * kBlock, 0, s>>>(
-      in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, SUM ? sc : c0, c1);
+  pipe_kernel<T, S, WRAP, SUM, JS0, LAG1>()<<<blocks, 2 * kBlock, 0, s>>>(
+      in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, shares, SUM ? sc : c0, c1);
   note_dispatch(SUM ? "stream_pipe_sum" : "stream_pipe");
   note_pipe_lag1(LAG1 != 0);
 }

@@ -9,6 +9,7 @@
 #include "mxs/grid/layout.hpp"
 #include "mxs/grid/regions.hpp"
 #include "mxs/halo/plan.hpp"
+#include "mxs/kernels/frame_schedule.hpp"
 #include "mxs/topo/cart.hpp"
 
 namespace py = pybind11;
@@ -153,4 +154,39 @@ PYBIND11_MODULE(_mxs_core, m) {
       .def_readonly("recv_elems", &HaloPlan::recv_elems);
   m.def("make_halo_plan", &make_halo_plan, py::arg("topo"), py::arg("rank"), py::arg("tile"),
         py::arg("corners") = true, py::arg("loopback_self") = false);
+
+  m.def("balanced_starts", &kernels::balanced_starts, py::arg("groups"), py::arg("rows"), py::arg("blocks"),
+        py::arg("fill"), "fill-aware linear starts of the pipeline workgroups' shares (blocks + 1 entries)");
+  // Frame-first schedule of the overlapped multi-GPU pass (kernels/frame_schedule.hpp).
+  m.def(
+      "frame_schedule",
+      [](std::int64_t groups, std::int64_t rows, int blocks, std::int64_t fill, std::int64_t frame_rows, int comm_wgs,
+         int edge_left, int edge_right) {
+        const auto s =
+            kernels::make_frame_schedule(groups, rows, blocks, fill, frame_rows, comm_wgs, edge_left, edge_right);
+        py::list table;
+        for (int w = 0; w < s.blocks; ++w) {
+          py::list l;
+          for (int e = 0; e < s.entries; ++e) {
+            const auto& c = s.at(w, e);
+            if (c.r1 > c.r0) l.append(py::make_tuple(c.group, c.r0, c.r1, c.flags));
+          }
+          table.append(l);
+        }
+        py::dict d;
+        d["blocks"] = s.blocks;
+        d["entries"] = s.entries;
+        d["signals"] = s.signals;
+        d["comm_wgs"] = s.comm_wgs;
+        d["frame_rows"] = s.frame_rows;
+        d["frame_cost"] = s.frame_cost;
+        d["bulk_cost"] = s.bulk_cost;
+        d["table"] = table;
+        d["check"] = kernels::check_frame_schedule(s, groups, rows, std::min<std::int64_t>(rows, 32), edge_left,
+                                                   edge_right);
+        return d;
+      },
+      py::arg("groups"), py::arg("rows"), py::arg("blocks"), py::arg("fill"), py::arg("frame_rows") = 0,
+      py::arg("comm_wgs") = 8, py::arg("edge_left") = 1, py::arg("edge_right") = 1,
+      "per-workgroup chunk lists (group, r0, r1, flags) + the coverage check ('' = ok)");
 }

@@ -180,6 +180,27 @@ PYBIND11_MODULE(_mxs_hip, m) {
   m.def("set_pipe_lag1", &kernels::set_pipe_lag1, py::arg("on"),
         "ascending level order in the joint fp32 pipeline where it pays (default on; bitwise equal output)");
   m.def("pipe_lag1", &kernels::pipe_lag1);
+  m.def("set_pipe_balanced", &kernels::set_pipe_balanced, py::arg("on"),
+        "fill-aware workgroup shares in the pipeline passes (default on; bitwise equal output)");
+  m.def("pipe_balanced", &kernels::pipe_balanced_on);
+  m.def(
+      "absmax",
+      [](std::uintptr_t x, index_t n, const std::string& dt) {
+        double r = 0;
+        if (parse_dtype(dt) == DType::F32) {
+          DeviceBuffer<float> o(1);
+          kernels::absmax<float>(ptr<float>(x), n, o.get(), nullptr);
+          float h = 0;
+          MXS_HIP_CHECK(hipMemcpy(&h, o.get(), sizeof(float), hipMemcpyDeviceToHost));
+          r = h;
+        } else {
+          DeviceBuffer<double> o(1);
+          kernels::absmax<double>(ptr<double>(x), n, o.get(), nullptr);
+          MXS_HIP_CHECK(hipMemcpy(&r, o.get(), sizeof(double), hipMemcpyDeviceToHost));
+        }
+        return r;
+      },
+      py::arg("x"), py::arg("n"), py::arg("dtype") = "f32", "max |x[i]| (device reduction; NaN if any is NaN)");
   m.def("last_pipe_lag1", &kernels::last_pipe_lag1,
         "whether the most recent stencil launch was a pipeline pass in ascending level order");
   m.def(
@@ -333,8 +354,12 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        const RcclComm* comm, const std::string& dt, HaloBackend backend, bool overlap,
                        bool use_graph, bool loopback_self, StencilKind kind, double c0, double c1, int box_radius,
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
-                       py::object bootstrap, int graph_supersteps, bool sum_form, bool direct_halo) {
+                       py::object bootstrap, int graph_supersteps, bool sum_form, bool direct_halo, bool frame_overlap,
+                       int frame_comm_wgs, int frame_rows) {
              SolverConfig cfg;
+             cfg.frame_overlap = frame_overlap;
+             cfg.frame_comm_wgs = frame_comm_wgs;
+             cfg.frame_rows = frame_rows;
              cfg.bootstrap = wrap_allgather(bootstrap);
              cfg.graph_supersteps = graph_supersteps;
              cfg.direct_halo = direct_halo;
@@ -364,7 +389,33 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("box_radius") = 1, py::arg("box_weights") = std::vector<float>{}, py::arg("variant") = "auto",
            py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
            py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = false,
+           py::arg("frame_overlap") = true, py::arg("frame_comm_wgs") = -1, py::arg("frame_rows") = 0,
            py::keep_alive<1, 7>())
+      .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
+           "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")
+      .def(
+          "frame_overlap", [](SolverHandle& h, int S) { return h.visit([S](auto& s) { return s.frame_overlap(S); }); },
+          py::arg("S"), "whether super-steps of depth S run the frame-first overlapped schedule")
+      .def("sum_form_active", [](SolverHandle& h) { return h.visit([](auto& s) { return s.sum_form_active(); }); })
+      .def("sum_form_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.sum_form_note(); }); })
+      .def("last_run_blocks", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_blocks(); }); },
+           "(S, count) super-steps the last run() enqueued")
+      .def(
+          "frame_schedule",
+          [](SolverHandle& h, int S) -> py::object {
+            const kernels::FrameSchedule* f = h.visit([S](auto& s) { return s.frame_schedule(S); });
+            if (!f) return py::none();
+            py::dict d;
+            d["blocks"] = f->blocks;
+            d["entries"] = f->entries;
+            d["signals"] = f->signals;
+            d["comm_wgs"] = f->comm_wgs;
+            d["frame_rows"] = f->frame_rows;
+            d["frame_cost"] = f->frame_cost;
+            d["bulk_cost"] = f->bulk_cost;
+            return d;
+          },
+          py::arg("S"), "frame-first schedule of depth S (None: serial schedule)")
       .def("step", [](SolverHandle& h) { h.visit([](auto& s) { s.step(); }); })
       .def("direct_halo", [](SolverHandle& h) { return h.visit([](auto& s) { return s.direct_halo(); }); },
            "whether halos are pushed tile-to-tile by the device (IPC backend, direct mode)")

@@ -180,6 +180,7 @@ IpcDirectHalo<T>::IpcDirectHalo(const CartTopology& topo, int rank, const TileGe
     : impl_(std::make_unique<Impl>()) {
   Impl& I = *impl_;
   MXS_CHECK(bool(allgather), "IpcDirectHalo needs a host allgather bootstrap");
+  (void)ipc_check_devices(allgather, rank, "direct IPC halo");
   I.a = buf_a;
   I.b = buf_b;
   I.world = topo.size();

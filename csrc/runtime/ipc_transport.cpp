@@ -1,5 +1,8 @@
 #include "mxs/halo/ipc_transport.hpp"
 
+#include <cstdio>
+#include <cstdlib>
+
 #include <algorithm>
 #include <cstdint>
 #include <cstring>
@@ -190,6 +193,26 @@ double wall_clock_hz() {
 
 }  // namespace
 
+bool ipc_check_devices(const HostAllgather& allgather, int rank, const char* what) {
+  int dev = 0;
+  MXS_HIP_CHECK(hipGetDevice(&dev));
+  hipUUID u{};
+  MXS_HIP_CHECK(hipDeviceGetUuid(&u, dev));
+  const std::string mine(u.bytes, sizeof(u.bytes));
+  const std::vector<std::string> all = allgather(mine);
+  bool cross = false;
+  for (const auto& d : all) cross = cross || d != mine;
+  if (!cross) return false;
+  const char* opt = std::getenv("MXS_IPC_CROSS_DEVICE");
+  MXS_CHECK(opt && std::string(opt) == "1",
+            what << ": ranks on different GPUs. The IPC halo is verified only for ranks sharing one GPU; use the "
+                    "RCCL backend, or set MXS_IPC_CROSS_DEVICE=1 to opt in to the unverified cross-device path");
+  if (rank == 0)
+    std::fprintf(stderr, "warning: %s between different GPUs (MXS_IPC_CROSS_DEVICE=1): coherence of device-written "
+                         "peer memory over xGMI is not verified by the test suite\n", what);
+  return true;
+}
+
 template <typename T>
 struct IpcHaloTransport<T>::Impl {
   CtrlLayout L{};
@@ -215,6 +238,7 @@ IpcHaloTransport<T>::IpcHaloTransport(const HaloPlan& plan, const T* send, T* re
   MXS_CHECK(int(plan.sends.size()) <= kMaxMsgs && int(plan.recvs.size()) <= kMaxMsgs,
             "IPC halo: more than " << kMaxMsgs << " peers");
   MXS_CHECK(bool(allgather), "IPC halo backend needs a host allgather bootstrap");
+  (void)ipc_check_devices(allgather, rank, "IPC halo backend");
   MXS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&I.ctrl), I.L.words() * sizeof(u64)));
   MXS_HIP_CHECK(hipMemset(I.ctrl, 0, I.L.words() * sizeof(u64)));
   I.timeout_ticks = u64(timeout_s * wall_clock_hz());

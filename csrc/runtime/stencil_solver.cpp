@@ -2,6 +2,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <limits>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -64,6 +66,31 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   constexpr int N = 16 / int(sizeof(T));
   fused_ = cfg_.fuse_periodic_self && all_self && cfg_.kind == StencilKind::Jacobi5 && tile_.width % N == 0 &&
            kernels::stencil5_periodic_supported<T>(tile_);
+  // Frame-first overlap: RCCL with a wire transfer, the tuned kernel forms,
+  // every edge a neighbour's (time blocking), the thin-strip overlap off.
+  frame_allowed_ = cfg_.frame_overlap && cfg_.backend == HaloBackend::Rccl && !plan.sends.empty() && !fused_ &&
+                   cfg_.kind == StencilKind::Jacobi5 && cfg_.variant == kernels::StencilVariant::Auto &&
+                   block_ > 1 && !cfg_.overlap;
+  if (frame_allowed_) {
+    frame_ctl_.reset(2);
+    MXS_HIP_CHECK(hipMemsetAsync(frame_ctl_.get(), 0, 2 * sizeof(unsigned), main_.get()));
+    const double limit = comm_timeout() > 0 ? comm_timeout() : 600.0;
+    frame_timeout_ticks_ = std::uint64_t(limit * kernels::wall_clock_hz());
+  }
+  // Sum-form guard, coefficient part (the range part runs before the first pass).
+  user_sum_ = cfg_.coeffs.sum_form;
+  if (user_sum_ && cfg_.coeffs.center == cfg_.coeffs.neighbor && cfg_.kind == StencilKind::Jacobi5) {
+    const double c = std::fabs(cfg_.coeffs.neighbor);
+    const T cs = T(std::pow(c, double(block_)));
+    if (!(5.0 * c <= 1.0 + 1e-6)) {
+      sum_note_ = "sum form off: 5 |c| > 1 (the S-level sums would not be bounded by the field)";
+    } else if (!(cs >= std::numeric_limits<T>::min())) {
+      sum_note_ = "sum form off: c^S is below the normal range of the element type";
+    } else {
+      sum_coeffs_ok_ = true;
+    }
+  }
+  cfg_.coeffs.sum_form = user_sum_ && sum_coeffs_ok_;
 }
 
 template <typename T>
@@ -113,6 +140,20 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
     direct_->wait(m);
     update(cur, nxt, S, 0, w, 0, h, m);
     direct_->push(nxt, m);
+    return;
+  }
+  if (FramePass* fp = frame_pass(S, false)) {
+    // Frame-first pass on the side stream; the main stream exchanges nxt's
+    // halo as soon as the frame is stored. Submission order matters: the pass
+    // is enqueued before the counter wait (see the header).
+    fork_.record(m);
+    fork_.wait_on(side);
+    kernels::stencil5_frame_pass<T>(cur, nxt, tile_, cfg_.coeffs, fp->shape, fp->table.get(), fp->sched.entries,
+                                    frame_ctl_.get(), side);
+    interior_.record(side);
+    kernels::wait_counter(frame_ctl_.get(), unsigned(fp->sched.signals), frame_timeout_ticks_, frame_ctl_.get() + 1, m);
+    ex_->exchange(nxt, m);
+    interior_.wait_on(m);
     return;
   }
   if (!cfg_.overlap) {
@@ -214,7 +255,12 @@ typename StencilSolver<T>::GraphSet* StencilSolver<T>::graphs_for(int S, int cou
   if (!cfg_.use_graph) return nullptr;
   for (auto& gs : graphs_)
     if (gs->S == S) return gs->ok ? gs.get() : nullptr;
-  if (int(graphs_.size()) >= kMaxGraphSets) graphs_.erase(graphs_.begin());
+  if (int(graphs_.size()) >= kMaxGraphSets) {
+    // run() is asynchronous: launches of the evicted executables may still be queued.
+    main_.sync();
+    side_.sync();
+    graphs_.erase(graphs_.begin());
+  }
   auto gs = std::make_unique<GraphSet>();
   gs->S = S;
   gs->chain = std::max(1, std::min(chain_for(S), count));  // a short first run gets a short chain
@@ -240,6 +286,19 @@ void StencilSolver<T>::split(int iters, Group out[2]) const {
 template <typename T>
 void StencilSolver<T>::run_group(int S, int count) {
   if (count <= 0) return;
+  last_blocks_.emplace_back(S, count);
+  if (frame_pass(S, true)) {
+    // Post-exchange super-steps: cur's ghost ring must be fresh before the
+    // first one; each leaves the next one's fresh. Eager launches (header).
+    if (!ghost_fresh_) ex_->exchange(cur_, main_.get());
+    for (int i = 0; i < count; ++i) {
+      enqueue_block(cur_, nxt_, S);
+      std::swap(cur_, nxt_);
+    }
+    ghost_fresh_ = true;
+    return;
+  }
+  ghost_fresh_ = false;  // a serial super-step exchanges first and leaves the new ghost ring stale
   int i = 0;
   if (GraphSet* gs = graphs_for(S, count)) {
     for (; i + gs->chain <= count; i += gs->chain) {
@@ -264,23 +323,119 @@ void StencilSolver<T>::prime() {
 }
 
 template <typename T>
+void StencilSolver<T>::ensure_range() {
+  if (range_checked_) return;
+  range_checked_ = true;
+  if (!(user_sum_ && sum_coeffs_ok_)) return;
+  // max|u| over the whole current buffer (core and ghost ring): with
+  // 5 |c| <= 1 no later pass can exceed it, so one check per field change.
+  if (!absmax_.get()) absmax_.reset(1);
+  kernels::absmax<T>(cur_, tile_.alloc_elems(), absmax_.get(), main_.get());
+  T m = T(0);
+  MXS_HIP_CHECK(hipMemcpyAsync(&m, absmax_.get(), sizeof(T), hipMemcpyDeviceToHost, main_.get()));
+  main_.sync();
+  const double bound = double(std::numeric_limits<T>::max()) / 4.0 / std::pow(5.0, double(block_));
+  const bool ok = std::isfinite(double(m)) && double(m) < bound;
+  if (ok == cfg_.coeffs.sum_form) return;
+  cfg_.coeffs.sum_form = ok;
+  sum_note_ = ok ? "" : "sum form off: max|u| * 5^S would overflow the element type (per-step form)";
+  // Captured graphs and frame shapes were built for the other form.
+  main_.sync();
+  side_.sync();
+  graphs_.clear();
+  frames_.clear();
+  no_frame_.clear();
+  warmed_.clear();
+}
+
+template <typename T>
+void StencilSolver<T>::begin_run() {
+  ensure_range();
+  prime();
+}
+
+template <typename T>
 void StencilSolver<T>::run(int iters) {
   MXS_TRACE_RANGE("stencil.run");
-  if (iters > 0) prime();
+  last_blocks_.clear();
+  if (iters <= 0) return;
+  begin_run();
   Group gr[2];
   split(iters, gr);
   for (const Group& g : gr) run_group(g.S, g.count);
 }
 
 template <typename T>
+typename StencilSolver<T>::FramePass* StencilSolver<T>::frame_pass(int S, bool build) {
+  if (!frame_allowed_) return nullptr;
+  for (auto& f : frames_)
+    if (f->S == S) return f.get();
+  if (!build || std::find(no_frame_.begin(), no_frame_.end(), S) != no_frame_.end()) return nullptr;
+  kernels::FramePassShape shape;
+  if (!kernels::frame_pass_shape<T>(tile_, S, cfg_.coeffs, &shape)) {
+    no_frame_.push_back(S);
+    return nullptr;
+  }
+  auto env_int = [](const char* k, int dflt) {
+    const char* e = std::getenv(k);
+    return e && *e ? std::atoi(e) : dflt;
+  };
+  const int comm = cfg_.frame_comm_wgs >= 0 ? cfg_.frame_comm_wgs : env_int("MXS_FRAME_COMM_WGS", 8);
+  const int rows = cfg_.frame_rows > 0 ? cfg_.frame_rows : env_int("MXS_FRAME_ROWS", 0);
+  // Edge groups: those holding output columns of the S-wide left / right bands.
+  const int left = int(std::min<index_t>(shape.groups, (S + shape.owg - 1) / shape.owg));
+  const index_t last_w = tile_.width - (shape.groups - 1) * shape.owg;
+  const int right = last_w >= S ? 1 : 2;
+  auto fp = std::make_unique<FramePass>();
+  fp->S = S;
+  fp->shape = shape;
+  try {
+    fp->sched = kernels::make_frame_schedule(shape.groups, tile_.height, shape.blocks, shape.fill,
+                                             rows > 0 ? std::max<index_t>(rows, S) : 0, comm, left, right);
+  } catch (const std::invalid_argument&) {
+    no_frame_.push_back(S);  // more frame chunks than workgroups: serial
+    return nullptr;
+  }
+  index_t longest = 0;
+  for (const auto& c : fp->sched.table) longest = std::max<index_t>(longest, c.r1 - c.r0);
+  if (longest * tile_.pitch * index_t(sizeof(T)) >= (index_t(1) << 31)) {
+    no_frame_.push_back(S);  // a chunk past the 2 GiB buffer-descriptor range
+    return nullptr;
+  }
+  fp->table.reset(index_t(fp->sched.table.size()));
+  MXS_HIP_CHECK(hipMemcpy(fp->table.get(), fp->sched.table.data(), fp->table.bytes(), hipMemcpyHostToDevice));
+  frames_.push_back(std::move(fp));
+  return frames_.back().get();
+}
+
+template <typename T>
+bool StencilSolver<T>::frame_overlap(int S) const {
+  for (const auto& f : frames_)
+    if (f->S == S) return true;
+  if (!frame_allowed_) return false;
+  return std::find(no_frame_.begin(), no_frame_.end(), S) == no_frame_.end() &&
+         kernels::frame_pass_shape<T>(tile_, S, cfg_.coeffs, nullptr);
+}
+
+template <typename T>
+const kernels::FrameSchedule* StencilSolver<T>::frame_schedule(int S) {
+  FramePass* f = frame_pass(S, true);
+  return f ? &f->sched : nullptr;
+}
+
+template <typename T>
 void StencilSolver<T>::prepare(int iters) {
   MXS_TRACE_RANGE("stencil.prepare");
-  prime();
+  begin_run();
   Group gr[2];
   split(iters, gr);
   for (const Group& g : gr) {
     if (g.count <= 0) continue;
-    (void)graphs_for(g.S, g.count);
+    if (frame_pass(g.S, true) && !ghost_fresh_) {
+      ex_->exchange(cur_, main_.get());
+      ghost_fresh_ = true;
+    }
+    if (!frame_pass(g.S, false)) (void)graphs_for(g.S, g.count);
     if (std::find(warmed_.begin(), warmed_.end(), g.S) != warmed_.end()) continue;
     // One untimed launch of every kernel of this super-step size: cur -> nxt
     // without swapping (nxt is scratch; the exchange rewrites cur's ghost ring
@@ -295,9 +450,14 @@ void StencilSolver<T>::prepare(int iters) {
 template <typename T>
 void StencilSolver<T>::warm(int iters, int passes) {
   MXS_TRACE_RANGE("stencil.warm");
-  prime();
+  begin_run();
   Group gr[2];
   split(iters, gr);
+  for (const Group& g : gr)
+    if (g.count > 0 && frame_pass(g.S, true) && !ghost_fresh_) {
+      ex_->exchange(cur_, main_.get());
+      ghost_fresh_ = true;
+    }
   for (int p = 0; p < passes; ++p)
     for (const Group& g : gr)
       if (g.count > 0) enqueue_block(cur_, nxt_, g.S);  // cur -> nxt, no swap: state unchanged
@@ -313,6 +473,7 @@ void StencilSolver<T>::step() {
 template <typename T>
 void StencilSolver<T>::exchange_only() {
   ex_->exchange(cur_, main_.get());
+  ghost_fresh_ = true;
 }
 
 template <typename T>
@@ -327,6 +488,11 @@ void StencilSolver<T>::synchronize() {
   side_.sync();
   ex_->check();  // IPC backend: device-side waits carry their own deadline
   if (direct_) direct_->check();
+  if (frame_allowed_) {
+    unsigned st = 0;
+    MXS_HIP_CHECK(hipMemcpy(&st, frame_ctl_.get() + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+    MXS_CHECK(st == 0, "frame-first pass: the halo exchange's wait for the pass's frame counter hit its deadline");
+  }
 }
 
 template class StencilSolver<float>;

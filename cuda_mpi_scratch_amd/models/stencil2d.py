@@ -73,8 +73,16 @@ class StencilConfig:
     graph_supersteps: int = 0        # super-steps per hipGraph launch (0 = auto, ~1 ms of work)
     # IPC backend: device-initiated halo — each pass's output bands are pushed
     # tile-to-tile into the neighbours' ghost rings (no pack / unpack launches).
-    # None = on whenever the backend is ipc.
+    # None = on whenever the backend is ipc. The IPC backend refuses ranks on
+    # different GPUs unless MXS_IPC_CROSS_DEVICE=1 (verified only for ranks
+    # sharing one GPU: halo/ipc_transport.hpp ipc_check_devices).
     direct_halo: bool | None = None
+    # RCCL backend with remote peers: frame-first overlap — each pass stores its
+    # S-deep output frame first and the next halo exchange (pack -> RCCL ->
+    # unpack) runs under the rest of the pass (runtime/stencil_solver.hpp).
+    frame_overlap: bool = True
+    frame_comm_wgs: int = -1         # frame-only workgroups leaving CUs to the exchange (-1 = default)
+    frame_rows: int = 0              # frame chunk height (0 = auto)
 
     @property
     def halo(self) -> int:
@@ -160,7 +168,8 @@ class Stencil2D:
                                           cfg.dtype, be, overlap, cfg.graph, cfg.loopback, kind, cfg.c_center,
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
-                                          backend == "ipc" and cfg.direct_halo is not False)
+                                          backend == "ipc" and cfg.direct_halo is not False,
+                                          cfg.frame_overlap, cfg.frame_comm_wgs, cfg.frame_rows)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
@@ -243,9 +252,32 @@ class Stencil2D:
 
     # ---------------------------------------------------------------- state
     def current(self) -> torch.Tensor:
+        """The tensor holding the current field. The caller may write it, so the
+        native solver re-exchanges the ghost ring and re-checks the sum form's
+        range before its next pass (one extra exchange; see field_changed())."""
         if self.solver is not None:
+            self.solver.field_changed()
             return self.a if self.solver.current() == self.a.data_ptr() else self.b
         return self._cur
+
+    def field_changed(self):
+        """Tell the native solver that the field was written from outside."""
+        if self.solver is not None:
+            self.solver.field_changed()
+
+    @property
+    def sum_form_active(self) -> bool:
+        """Whether the passes run the sum form right now (coefficients, the
+        user's choice and the measured field range all allow it)."""
+        if self.solver is not None:
+            return bool(self.solver.sum_form_active())
+        return False
+
+    def last_run_blocks(self) -> list[tuple[int, int]]:
+        """(S, count) of the super-steps the last run() executed."""
+        if self.solver is not None:
+            return [tuple(x) for x in self.solver.last_run_blocks()]
+        return [(1, 0)]
 
     def full_view(self) -> torch.Tensor:
         """(total_height, total_width) logical view: core + ghost ring."""
@@ -304,6 +336,9 @@ class Stencil2D:
             return "fused-periodic (1x1 self-exchange in the kernel addressing)" + blk
         if self.solver.direct_halo():
             return "ipc direct (device-initiated push of each pass's edge bands into the neighbours' tiles)" + blk
+        if tb > 1 and self.solver.frame_overlap(tb):
+            return (f"{self.backend} + frame-first overlap (each pass stores its {tb}-deep output frame first; "
+                    f"the next halo's pack -> RCCL send/recv -> unpack runs under the rest of the pass)" + blk)
         return f"{self.backend}" + (" + overlap" if self.solver.overlapped() else "") + blk
 
     # ----------------------------------------------------------------- dump

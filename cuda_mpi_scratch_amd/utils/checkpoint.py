@@ -104,6 +104,7 @@ def load(stencil, path: str) -> GridHeader:
     stencil.core_view().copy_(torch.from_numpy(block))
     if stencil.device.type == "cuda":
         torch.cuda.synchronize()  # the copy ran on torch's stream, not the solver's
+    stencil.field_changed()  # ghost ring and sum-form range are re-established before the next pass
     stencil.synchronize()
     stencil.iteration = header.iteration
     del arr
