@@ -9,7 +9,9 @@
 //   mpiexec -n 2 pingpong --transport mpi-staged --page-locked 1048576
 //
 // --transport rccl        ncclSend/ncclRecv between ranks 0 and 1 (xGMI); modes
-//                         blocking | async | overlap (async beside an HBM-streaming kernel)
+//                         blocking (host-timed round trips) | async (hipEvent-timed) |
+//                         overlap (async beside an ALU-bound kernel) | bidir (both ranks
+//                         send at once: both directions of the link, bidir_gbps)
 // --transport mpi-staged  D2H -> MPI (blocking Send/Recv, or Isend/Irecv with --mode async)
 //                         -> H2D; --page-locked uses hipHostMalloc buffers (host_allocator.h)
 // --transport loopback    1 rank: RCCL self send/recv; d2d / pinned / pageable: local paths
@@ -169,8 +171,10 @@ int main(int argc, char** argv) {
     PingPongStats st;
     if (!active) continue;
     if (transport == "rccl" || transport == "loopback") {
-      const PingPongMode m = mode == "async" ? PingPongMode::Async
-                           : mode == "overlap" ? PingPongMode::Overlap : PingPongMode::Blocking;
+      const PingPongMode m = mode == "async"     ? PingPongMode::Async
+                           : mode == "overlap" ? PingPongMode::Overlap
+                           : mode == "bidir"   ? PingPongMode::Bidirectional
+                                               : PingPongMode::Blocking;
       const int peer = transport == "loopback" ? env.rank() : 1 - env.rank();
       st = pingpong_rccl(*comm, peer, dsend.get(), drecv.get(), bytes, warmup, reps, m, stream.get());
     } else if (transport == "ipc") {
@@ -217,6 +221,8 @@ int main(int argc, char** argv) {
        << ", \"rtt_min_us\": " << app::fmt(st.min_rtt_us) << ", \"latency_us\": " << app::fmt(st.latency_us())
        << ", \"gbps\": " << app::fmt(st.bandwidth_gbps()) << ", \"reps\": " << st.reps
        << ", \"passed\": " << (st.verified ? "true" : "false");
+    js << ", \"timing\": \"" << (mode == "blocking" ? "host" : "device") << "\"";
+    if (mode == "bidir") js << ", \"bidir_gbps\": " << app::fmt(st.bidir_gbps());
     if (mode == "overlap")
       js << ", \"compute_alone_us\": " << app::fmt(st.compute_alone_us) << ", \"comm_alone_us\": "
          << app::fmt(st.comm_alone_us) << ", \"overlapped_us\": " << app::fmt(st.overlapped_us);

@@ -134,14 +134,15 @@ def pingpong_extras(ctx, extras: dict, max_bytes: int, with_ipc: bool = False) -
     from cuda_mpi_scratch_amd.models.pingpong import PingPong
 
     sweep = []
-    gpu_plan = (("rccl", ("blocking", "async", "overlap")),) + ((("ipc", ("device",)),) if with_ipc else ())
+    gpu_plan = (("rccl", ("blocking", "async", "overlap", "bidir")),) + ((("ipc", ("device",)),) if with_ipc else ())
     plan = gpu_plan if torch.cuda.is_available() else (("torch", ("blocking",)),)  # CPU rehearsal: gloo send/recv
     for transport, modes in plan:
         try:
             sizes = [b for b in PINGPONG_SIZES if b <= max_bytes]
             pp = PingPong(ctx, transport, sizes[-1])
             for mode in modes:
-                for nb in sizes:
+                # Bidirectional: the large-message end only (the per-link bound).
+                for nb in (sizes if mode != "bidir" else [b for b in sizes if b >= (1 << 20)]):
                     reps = 50 if nb <= (1 << 20) else (10 if nb <= (32 << 20) else 5)
                     rec = pp.run(nb, "async" if mode == "device" else mode, 3, reps)
                     rec["mode"] = mode
@@ -157,10 +158,17 @@ def pingpong_extras(ctx, extras: dict, max_bytes: int, with_ipc: bool = False) -
     for rec in sweep:
         key = f"pingpong_{rec['transport']}_{rec['mode']}"
         if rec["bytes"] == 8:
-            extras[f"{key}_8B_latency_us"] = round(rec["latency_us"], 2)
+            if rec.get("timing") == "host":
+                # Blocking mode is timed by the host around launch + stream sync:
+                # a host round-trip figure, not the transport's latency.
+                extras[f"{key}_8B_host_rtt_us"] = round(rec["rtt_us"], 2)
+            else:
+                extras[f"{key}_8B_latency_us"] = round(rec["latency_us"], 2)  # hipEvent-timed, RTT / 2
         for label, nb in SUMMARY_SIZES.items():
             if rec["bytes"] == nb:
                 extras[f"{key}_{label}_gbps"] = round(rec["gbps"], 2)
+                if "bidir_gbps" in rec:
+                    extras[f"{key}_{label}_both_directions_gbps"] = round(rec["bidir_gbps"], 2)
         if rec["mode"] == "overlap" and rec["bytes"] == SUMMARY_SIZES["256MiB"]:
             alone = rec.get("compute_alone_us", 0.0) + rec.get("comm_alone_us", 0.0)
             if rec.get("overlapped_us"):
@@ -192,9 +200,13 @@ def main(argv=None) -> int:
                    help="per-step evaluation in the time-blocked kernels (bitwise equal to S single steps; "
                         "default: the sum form, c^S applied once per pass, for the equal default coefficients)")
     p.add_argument("--no-overlap", action="store_true")
-    p.add_argument("--no-frame-overlap", action="store_true",
-                   help="multi-GPU: exchange the halo before each pass (serial) instead of under the pass "
-                        "(frame-first overlap, the default)")
+    p.add_argument("--no-fuse-periodic", action="store_true",
+                   help="N = 1: explicit self-exchange (copies into the ghost ring) + the ghost-ring pass instead "
+                        "of the wrap-around addressing")
+    p.add_argument("--frame-overlap", action="store_true",
+                   help="multi-GPU: exchange the next halo under the pass (frame-first overlap) instead of "
+                        "before it (serial, the default; docs/PERF.md)")
+    p.add_argument("--no-frame-overlap", action="store_true", help=argparse.SUPPRESS)
     p.add_argument("--overlap", action="store_true", help="force the interior/exchange overlap schedule")
     p.add_argument("--loopback", action="store_true",
                    help="1 GPU: route the self-neighbour halos through RCCL (exercises the multi-GPU schedule)")
@@ -236,7 +248,8 @@ def main(argv=None) -> int:
                         overlap=False if args.no_overlap else (True if args.overlap else None),
                         graph=not args.no_graph,
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback,
-                        sum_form=not args.no_sum_form, frame_overlap=not args.no_frame_overlap)
+                        sum_form=not args.no_sum_form, frame_overlap=args.frame_overlap and not args.no_frame_overlap,
+                        fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3)
     timed_blocks = st.last_run_blocks()  # the super-steps the timed window executed

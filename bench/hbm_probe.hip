@@ -56,6 +56,27 @@ __global__ __launch_bounds__(256) void read_u(const v4f* __restrict__ a, float* 
   if (acc == 12345.678f) out[0] = acc;  // keep the loads alive
 }
 
+// The dot kernel's pattern (kernels/dot.hip): one workgroup per CU, every lane
+// issues U non-temporal 16-byte loads before any use (U x 1 KiB per wave
+// instruction group in flight), grid-stride over whole chunks. dot.hip reads at
+// 7.1 TB/s this way (profiles/r02_dot); the plain-load read_u above at 8-32
+// workgroups per CU topped out at 6.3-6.4 TB/s.
+template <int U>
+__global__ __launch_bounds__(256) void read_nt(const v4f* __restrict__ a, float* __restrict__ out, index_t n) {
+  const index_t stride = index_t(gridDim.x) * 256 * U;
+  v4f acc = {0.f, 0.f, 0.f, 0.f};
+  index_t base = index_t(blockIdx.x) * 256 * U + threadIdx.x;
+  for (; base + (U - 1) * 256 < n; base += stride) {
+    v4f v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(a + base + u * 256);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += v[u];
+  }
+  for (; base < n; base += 256) acc += a[base];
+  if (acc.x + acc.y + acc.z + acc.w == 12345.678f) out[0] = acc.x;  // keep the loads alive
+}
+
 template <bool NTS>
 __global__ __launch_bounds__(256) void write_only(v4f* __restrict__ b, index_t n) {
   const index_t stride = index_t(gridDim.x) * 256;
@@ -95,6 +116,14 @@ int main(int argc, char** argv) {
     vs.push_back({"read_u8_g" + std::to_string(grid), rb, [=](hipStream_t s) { read_u<8><<<grid, 256, 0, s>>>(pa, ps, n); }});
     vs.push_back({"write_g" + std::to_string(grid), rb, [=](hipStream_t s) { write_only<false><<<grid, 256, 0, s>>>(pb, n); }});
     vs.push_back({"write_nts_g" + std::to_string(grid), rb, [=](hipStream_t s) { write_only<true><<<grid, 256, 0, s>>>(pb, n); }});
+  }
+  const int cus = device_cu_count();
+  for (int per_cu : {1, 2, 4}) {
+    const int grid = per_cu * cus;
+    vs.push_back({"read_nt_u8_g" + std::to_string(grid), rb, [=](hipStream_t s) { read_nt<8><<<grid, 256, 0, s>>>(pa, ps, n); }});
+    vs.push_back({"read_nt_u16_g" + std::to_string(grid), rb, [=](hipStream_t s) { read_nt<16><<<grid, 256, 0, s>>>(pa, ps, n); }});
+    add_copy("copy_u8_nts_ntl", grid, copy_u<8, true, true>);
+    add_copy("copy_u8_nts", grid, copy_u<8, true, false>);
   }
   vs.push_back({"hipMemcpyDtoD", cb, [=](hipStream_t s) { MXS_HIP_CHECK(hipMemcpyAsync(pb, pa, abytes, hipMemcpyDeviceToDevice, s)); }});
   Stream st;

@@ -17,7 +17,7 @@
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
 #include "mxs/runtime/hip_utils.hpp"
-#include "../csrc/kernels/stencil_pipe.hpp"
+#include "tune_kernels.hpp"
 
 using namespace mxs;
 using namespace mxs::kernels::detail;

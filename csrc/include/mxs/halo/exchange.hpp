@@ -80,6 +80,9 @@ class HaloExchanger {
   size_t wire_bytes() const { return size_t(plan_.send_elems) * sizeof(T); }
   // Raises if a device-side wait of the Ipc backend timed out (stream idle).
   void check() const;
+  // Threads per workgroup of the pack / unpack launches (0 = default 256;
+  // 64 = one-wave workgroups that run beside a pipeline pass).
+  void set_copy_block(int threads) { copy_block_ = threads; }
 
  private:
   HaloPlan plan_;
@@ -88,6 +91,7 @@ class HaloExchanger {
   HaloCopyPrograms progs_;
   DeviceBuffer<T> send_, recv_;
   std::unique_ptr<IpcHaloTransport<T>> ipc_;
+  int copy_block_ = 0;
 };
 
 }  // namespace mxs

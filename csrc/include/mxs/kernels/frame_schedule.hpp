@@ -153,26 +153,33 @@ inline FrameSchedule make_frame_schedule(std::int64_t groups, std::int64_t rows,
   s.blocks = blocks;
   // Frame chunks. Edge groups: whole height in chunks of ~hf rows; middle
   // groups: top and bottom hf rows (the whole group when it is that short).
+  // More chunks than workgroups: taller chunks until they fit.
   std::vector<FrameChunk> frame;
-  auto cut = [&](std::int32_t g, std::int64_t r0, std::int64_t r1) {
-    const std::int64_t n = std::max<std::int64_t>(1, (r1 - r0 + hf - 1) / hf);
-    for (std::int64_t i = 0; i < n; ++i)
-      frame.push_back(FrameChunk{g, std::int32_t(r0 + (r1 - r0) * i / n), std::int32_t(r0 + (r1 - r0) * (i + 1) / n),
-                                 kFrameSignal});
-  };
   std::vector<detail::Run> bulk;
-  for (std::int64_t g = 0; g < groups; ++g) {
-    if (g < edge_left || g >= groups - edge_right || rows <= 2 * hf) {
-      cut(std::int32_t(g), 0, rows);
-    } else {
-      frame.push_back(FrameChunk{std::int32_t(g), 0, std::int32_t(hf), kFrameSignal});
-      frame.push_back(FrameChunk{std::int32_t(g), std::int32_t(rows - hf), std::int32_t(rows), kFrameSignal});
-      bulk.push_back(detail::Run{std::int32_t(g), hf, rows - hf});
+  for (;;) {
+    frame.clear();
+    bulk.clear();
+    auto cut = [&](std::int32_t g, std::int64_t r0, std::int64_t r1) {
+      const std::int64_t n = std::max<std::int64_t>(1, (r1 - r0 + hf - 1) / hf);
+      for (std::int64_t i = 0; i < n; ++i)
+        frame.push_back(FrameChunk{g, std::int32_t(r0 + (r1 - r0) * i / n),
+                                   std::int32_t(r0 + (r1 - r0) * (i + 1) / n), kFrameSignal});
+    };
+    for (std::int64_t g = 0; g < groups; ++g) {
+      if (g < edge_left || g >= groups - edge_right || rows <= 2 * hf) {
+        cut(std::int32_t(g), 0, rows);
+      } else {
+        frame.push_back(FrameChunk{std::int32_t(g), 0, std::int32_t(hf), kFrameSignal});
+        frame.push_back(FrameChunk{std::int32_t(g), std::int32_t(rows - hf), std::int32_t(rows), kFrameSignal});
+        bulk.push_back(detail::Run{std::int32_t(g), hf, rows - hf});
+      }
     }
+    if (std::int64_t(frame.size()) <= blocks || hf >= rows) break;
+    hf = std::min(rows, hf + hf / 4 + 1);
   }
   if (std::int64_t(frame.size()) > blocks)
     throw std::invalid_argument("make_frame_schedule: " + std::to_string(frame.size()) + " frame chunks for " +
-                                std::to_string(blocks) + " workgroups (raise frame_rows)");
+                                std::to_string(blocks) + " workgroups");
   // Frame chunk i goes to workgroup i; the first comm_wgs of them (blocks b
   // and b + 8 share an XCD: the first 8 spread over all eight) take nothing else.
   const int nf = int(frame.size());

@@ -160,8 +160,9 @@ template <typename T>
 void stencil5_frame_pass(const T* in, T* out, const TileGeom& g, const Stencil5Coeffs& c, const FramePassShape& shape,
                          const FrameChunk* table, int entries, unsigned* counter, hipStream_t s);
 // One lane spins (device deadline of `timeout_ticks` wall-clock ticks, then
-// *status = 1) until *counter >= target, then resets *counter to 0: the comm
-// stream's wait for a frame_pass running on another stream.
+// *status = 1, a system-scope store: `status` may be pinned host memory) until
+// *counter >= target, then resets *counter to 0: the comm stream's wait for a
+// frame_pass running on another stream.
 void wait_counter(unsigned* counter, unsigned target, std::uint64_t timeout_ticks, unsigned* status, hipStream_t s);
 // Device wall-clock ticks per second (the deadline unit above).
 double wall_clock_hz();
@@ -241,8 +242,11 @@ struct Copy2DBatch {
   Copy2D op[kMaxCopies];
 };
 // grid_x: workgroups per copy (0 = sized from the largest copy; tuning only).
+// block: threads per workgroup (0 = 256, or MXS_HALO_BLOCK). One-wave (64)
+// workgroups are the ones the hardware places beside a running pipeline
+// workgroup (the frame-first schedule's copies); 256 is faster alone.
 template <typename T>
-void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x = 0);
+void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x = 0, int block = 0);
 
 // ---------------------------------------------------------------- dot (K2-K8)
 enum class DotReduce : int {

@@ -9,6 +9,11 @@
 //              with hipEvents (device-observed RTT, the floor of the transport).
 //   Overlap  : Async, while a compute kernel (an HBM-streaming triad) runs on a
 //              second stream; reports how much of the transfer was hidden.
+//   Bidirectional : both ranks send `bytes` to each other at once (one grouped
+//              send + recv per side, back to back, event-timed): one "round
+//              trip" sample is one such exchange, so the link carries 2 x bytes
+//              per sample (bidir_gbps); checks the per-link bound in both
+//              directions of one xGMI link at once.
 // The ping side is the lower rank; with peer == own rank (1-rank communicator)
 // each "round trip" is a grouped self send+recv, which lets one GPU exercise and
 // time the RCCL path.
@@ -22,15 +27,22 @@
 
 namespace mxs {
 
-enum class PingPongMode : int { Blocking = 0, Async = 1, Overlap = 2 };
+enum class PingPongMode : int { Blocking = 0, Async = 1, Overlap = 2, Bidirectional = 3 };
 
 struct PingPongStats {
   size_t bytes = 0;
   int reps = 0;
   double min_rtt_us = 0, median_rtt_us = 0, max_rtt_us = 0;
   // One-way latency = RTT / 2; unidirectional bandwidth = bytes / (RTT / 2).
-  double latency_us() const { return median_rtt_us / 2.0; }
-  double bandwidth_gbps() const { return median_rtt_us > 0 ? double(bytes) / (median_rtt_us * 0.5e-6) / 1e9 : 0; }
+  // Bidirectional mode: a sample is one simultaneous exchange, each direction
+  // moves `bytes` in it: per-direction bandwidth = bytes / sample time.
+  bool bidirectional = false;
+  double latency_us() const { return bidirectional ? median_rtt_us : median_rtt_us / 2.0; }
+  double bandwidth_gbps() const {
+    if (median_rtt_us <= 0) return 0;
+    return double(bytes) / (median_rtt_us * (bidirectional ? 1e-6 : 0.5e-6)) / 1e9;
+  }
+  double bidir_gbps() const { return bidirectional ? 2.0 * bandwidth_gbps() : 0.0; }
   // Overlap mode: time of compute alone, comm alone and both together (us).
   double compute_alone_us = 0, comm_alone_us = 0, overlapped_us = 0;
   bool verified = false;

@@ -115,13 +115,22 @@ struct SolverConfig {
   // neighbours' ghost rings and publishes a ready counter; the next pass waits
   // for the neighbours' counters. Replaces pack -> put -> wait -> unpack.
   bool direct_halo = false;
-  // Frame-first overlap of the RCCL halo with the pass (see above).
-  bool frame_overlap = true;
+  // Frame-first overlap of the RCCL halo with the pass (see above). Off by
+  // default: on one GPU (RCCL loopback, 16384 x 8192 tile) it measured 3-8%
+  // slower than the serial schedule with eager launches (docs/PERF.md,
+  // "Frame-first overlap"); it is exact and tested, and stays opt-in until a
+  // multi-GPU run shows the wire time it hides is worth the copies' interference.
+  bool frame_overlap = false;
   // Frame-only workgroups that exit early and leave their CUs to the exchange
-  // (-1: MXS_FRAME_COMM_WGS or 8), and the frame chunk height (0: MXS_FRAME_ROWS
+  // (-1: MXS_FRAME_COMM_WGS or 16), and the frame chunk height (0: MXS_FRAME_ROWS
   // or auto, kernels::make_frame_schedule).
   int frame_comm_wgs = -1;
   int frame_rows = 0;
+  // Super-steps estimated longer than this (us, at ~9 T cell-steps/s) are
+  // launched eagerly instead of from a hipGraph: on the 8-GPU tile (0.24 ms
+  // passes) a 20-step RCCL-loopback window took 0.276 ms eager vs 0.285 from
+  // the graph, 240 steps 3.23 vs 3.34 ms (profiles/r03_window5). 0 = always graphs.
+  double graph_max_superstep_us = 150.0;
 };
 
 template <typename T>
@@ -219,7 +228,10 @@ class StencilSolver {
   bool frame_allowed_ = false;               // config / backend / peers allow the overlap
   std::vector<std::unique_ptr<FramePass>> frames_;
   std::vector<int> no_frame_;                // depths without a frame form
-  DeviceBuffer<unsigned> frame_ctl_;         // [0] frame counter, [1] wait deadline status
+  DeviceBuffer<unsigned> frame_ctl_;         // frame counter (device memory)
+  // Wait-deadline status in coherent pinned host memory: synchronize() reads it
+  // without a device-to-host copy inside the caller's timed window.
+  PinnedBuffer<unsigned> frame_status_;
   std::uint64_t frame_timeout_ticks_ = 0;
   bool ghost_fresh_ = false;                 // cur_'s ghost ring holds the neighbours' current bands
   bool range_checked_ = false;

@@ -24,7 +24,7 @@ __global__ void wait_counter_kernel(unsigned* counter, unsigned target, std::uin
   const std::uint64_t t0 = wall_clock64();
   while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
     if (wall_clock64() - t0 > timeout_ticks) {
-      __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // pinned host word
       break;
     }
     __builtin_amdgcn_s_sleep(2);

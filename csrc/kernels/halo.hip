@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 
 #include "mxs/core/error.hpp"
 #include "mxs/kernels/kernels.hpp"
@@ -33,7 +34,12 @@ constexpr int kBlock = 256;
 // kInFlight elements per thread are loaded before any is stored: a pack of the
 // 8-GPU tile's 20-deep halo gives each thread 2-3 vectors, and one load ->
 // store round trip per element serialised them (6 us per launch, of which
-// ~4 us memory latency; profiles/r02_tile).
+// ~4 us memory latency; profiles/r02_tile). Each in-flight element keeps its
+// value and its destination pointer only (not its coordinates): the kernel
+// stays at <= 32 VGPRs, so a copy wave fits beside a pipeline workgroup
+// (2 waves x 240 VGPRs per SIMD) and the frame-first schedule's pack / unpack
+// run while the pass does (at 34 VGPRs -> 40 allocated they could not be
+// placed until the pass ended, profiles/r03_frame).
 constexpr int kInFlight = 4;
 
 template <typename V, typename Src, typename Dst>
@@ -44,12 +50,14 @@ __device__ __forceinline__ void copy_2d(index_t width, index_t height, Src&& src
   const index_t dy = stride / width, dx = stride - dy * width;
   while (y < height) {
     V v[kInFlight];
-    index_t xs[kInFlight], ys[kInFlight];
+    V* d[kInFlight];
 #pragma unroll
     for (int k = 0; k < kInFlight; ++k) {
-      xs[k] = x;
-      ys[k] = y;
-      if (y < height) v[k] = *src(x, y);
+      d[k] = nullptr;
+      if (y < height) {
+        v[k] = *src(x, y);
+        d[k] = dst(x, y);
+      }
       x += dx;
       y += dy;
       if (x >= width) {
@@ -59,13 +67,20 @@ __device__ __forceinline__ void copy_2d(index_t width, index_t height, Src&& src
     }
 #pragma unroll
     for (int k = 0; k < kInFlight; ++k)
-      if (ys[k] < height) *dst(xs[k], ys[k]) = v[k];
+      if (d[k]) *d[k] = v[k];
   }
 }
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void copy2d_batch_kernel(T* __restrict__ s0, T* __restrict__ s1,
-                                                              T* __restrict__ s2, Copy2DBatch b) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_vgpr(32))) void copy2d_batch_kernel(
+    T* __restrict__ s0, T* __restrict__ s1, T* __restrict__ s2, Copy2DBatch b) {
+  // Highest wave priority: in the frame-first schedule the pack / unpack run
+  // while the pipeline pass still fills every CU (a copy wave fits beside a
+  // pipeline workgroup: 20 VGPRs), and the pass's VALU-bound waves, which
+  // raise their own priority as they progress (stencil_device.hpp), otherwise
+  // win every issue slot: the pack crawled until the pass ended (140 us for
+  // 4 MB, profiles/r03_frame). A copy wave issues little: it mostly waits on memory.
+  __builtin_amdgcn_s_setprio(3);
   const Copy2D& op = b.op[blockIdx.y];
   // Wave-uniform selects (a runtime-indexed pointer array would go to scratch).
   const T* __restrict__ src = (op.src_slot == 0 ? s0 : (op.src_slot == 1 ? s1 : s2)) + op.src_off;
@@ -92,7 +107,7 @@ __global__ __launch_bounds__(kBlock) void copy2d_batch_kernel(T* __restrict__ s0
 }  // namespace
 
 template <typename T>
-void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x) {
+void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x, int block_req) {
   if (b.n <= 0) return;
   MXS_CHECK(b.n <= kMaxCopies, "copy2d_batch: too many copies " << b.n);
   index_t biggest = 0;
@@ -104,18 +119,25 @@ void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_
   // a 16384-wide tile = 1.3 MB per segment), and the earlier cap of 64
   // workgroups per segment moved them at ~0.4 TB/s (7 us per pack of the 8-GPU tile).
   constexpr index_t kVec = 16 / sizeof(T) > 0 ? 16 / sizeof(T) : 1;
-  const index_t want = (biggest + kBlock * kVec - 1) / (kBlock * kVec);
-  const index_t cap = std::max<index_t>(64, index_t(4) * device_cu_count() / b.n);
+  // MXS_HALO_BLOCK (tuning): threads per workgroup (64, 128 or 256).
+  static const int env_block = [] {
+    const char* e = std::getenv("MXS_HALO_BLOCK");
+    const int v = e && *e ? std::atoi(e) : kBlock;
+    return v == 64 || v == 128 ? v : kBlock;
+  }();
+  const int block = block_req == 64 || block_req == 128 || block_req == kBlock ? block_req : env_block;
+  const index_t want = (biggest + block * kVec - 1) / (block * kVec);
+  const index_t cap = std::max<index_t>(64, index_t(4 * kBlock / block) * device_cu_count() / b.n);
   const int gx = grid_x > 0 ? grid_x : int(std::min<index_t>(want, cap));
-  copy2d_batch_kernel<T><<<dim3(gx, b.n), kBlock, 0, s>>>(slot0, slot1, slot2, b);
+  copy2d_batch_kernel<T><<<dim3(gx, b.n), block, 0, s>>>(slot0, slot1, slot2, b);
   MXS_HIP_CHECK_LAUNCH();
 }
 
-template void copy2d_batch<float>(float*, float*, float*, const Copy2DBatch&, hipStream_t, int);
-template void copy2d_batch<double>(double*, double*, double*, const Copy2DBatch&, hipStream_t, int);
-template void copy2d_batch<int>(int*, int*, int*, const Copy2DBatch&, hipStream_t, int);
+template void copy2d_batch<float>(float*, float*, float*, const Copy2DBatch&, hipStream_t, int, int);
+template void copy2d_batch<double>(double*, double*, double*, const Copy2DBatch&, hipStream_t, int, int);
+template void copy2d_batch<int>(int*, int*, int*, const Copy2DBatch&, hipStream_t, int, int);
 template void copy2d_batch<unsigned char>(unsigned char*, unsigned char*, unsigned char*, const Copy2DBatch&,
-                                          hipStream_t, int);
+                                          hipStream_t, int, int);
 
 }  // namespace kernels
 }  // namespace mxs

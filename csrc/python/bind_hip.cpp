@@ -201,6 +201,49 @@ PYBIND11_MODULE(_mxs_hip, m) {
         return r;
       },
       py::arg("x"), py::arg("n"), py::arg("dtype") = "f32", "max |x[i]| (device reduction; NaN if any is NaN)");
+  m.def(
+      "stencil5_frame_pass",
+      [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, double c0, double c1,
+         const std::string& dt, int comm_wgs, int frame_rows, std::uintptr_t s, bool sum_form) -> py::object {
+        // One frame-first pass with its own schedule (tuning / tests): the
+        // table lives for the call, so the launch is synchronised before return.
+        kernels::Stencil5Coeffs c{c0, c1, sum_form};
+        auto run = [&](auto tag) -> py::object {
+          using T = decltype(tag);
+          kernels::FramePassShape sh;
+          if (!kernels::frame_pass_shape<T>(g, steps, c, &sh)) return py::none();
+          const auto sched = kernels::make_frame_schedule(sh.groups, g.height, sh.blocks, sh.fill, frame_rows,
+                                                          comm_wgs < 0 ? 8 : comm_wgs);
+          DeviceBuffer<kernels::FrameChunk> tab(index_t(sched.table.size()));
+          DeviceBuffer<unsigned> ctr(1);
+          MXS_HIP_CHECK(hipMemcpy(tab.get(), sched.table.data(), tab.bytes(), hipMemcpyHostToDevice));
+          MXS_HIP_CHECK(hipMemsetAsync(ctr.get(), 0, sizeof(unsigned), strm(s)));
+          Event e0(true), e1(true);
+          e0.record(strm(s));
+          kernels::stencil5_frame_pass<T>(ptr<T>(in), ptr<T>(out), g, c, sh, tab.get(), sched.entries, ctr.get(),
+                                          strm(s));
+          e1.record(strm(s));
+          MXS_HIP_CHECK(hipStreamSynchronize(strm(s)));
+          unsigned got = 0;
+          MXS_HIP_CHECK(hipMemcpy(&got, ctr.get(), sizeof(unsigned), hipMemcpyDeviceToHost));
+          py::dict d;
+          d["signals"] = sched.signals;
+          d["counter"] = got;
+          d["blocks"] = sched.blocks;
+          d["frame_cost"] = sched.frame_cost;
+          d["bulk_cost"] = sched.bulk_cost;
+          d["js0"] = sh.js0;
+          d["lag1"] = sh.lag1;
+          d["fill"] = sh.fill;
+          d["kernel_us"] = double(e1.since(e0)) * 1000.0;
+          return d;
+        };
+        return parse_dtype(dt) == DType::F32 ? run(float{}) : run(double{});
+      },
+      py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("steps"), py::arg("c_center") = 0.2,
+      py::arg("c_neighbor") = 0.2, py::arg("dtype") = "f32", py::arg("comm_wgs") = 8, py::arg("frame_rows") = 0,
+      py::arg("stream") = 0, py::arg("sum_form") = true,
+      "one frame-first pass over the core of a ghost-ring tile (None: no frame form for this depth)");
   m.def("last_pipe_lag1", &kernels::last_pipe_lag1,
         "whether the most recent stencil launch was a pipeline pass in ascending level order");
   m.def(
@@ -355,8 +398,9 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        bool use_graph, bool loopback_self, StencilKind kind, double c0, double c1, int box_radius,
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
                        py::object bootstrap, int graph_supersteps, bool sum_form, bool direct_halo, bool frame_overlap,
-                       int frame_comm_wgs, int frame_rows) {
+                       int frame_comm_wgs, int frame_rows, double graph_max_superstep_us) {
              SolverConfig cfg;
+             cfg.graph_max_superstep_us = graph_max_superstep_us;
              cfg.frame_overlap = frame_overlap;
              cfg.frame_comm_wgs = frame_comm_wgs;
              cfg.frame_rows = frame_rows;
@@ -389,7 +433,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("box_radius") = 1, py::arg("box_weights") = std::vector<float>{}, py::arg("variant") = "auto",
            py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
            py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = false,
-           py::arg("frame_overlap") = true, py::arg("frame_comm_wgs") = -1, py::arg("frame_rows") = 0,
+           py::arg("frame_overlap") = false, py::arg("frame_comm_wgs") = -1, py::arg("frame_rows") = 0,
+           py::arg("graph_max_superstep_us") = 150.0,
            py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")
@@ -452,7 +497,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
   py::enum_<PingPongMode>(m, "PingPongMode")
       .value("BLOCKING", PingPongMode::Blocking)
       .value("ASYNC", PingPongMode::Async)
-      .value("OVERLAP", PingPongMode::Overlap);
+      .value("OVERLAP", PingPongMode::Overlap)
+      .value("BIDIRECTIONAL", PingPongMode::Bidirectional);
   py::enum_<LocalPath>(m, "LocalPath")
       .value("DEVICE_COPY", LocalPath::DeviceCopy)
       .value("PINNED_STAGING", LocalPath::PinnedStaging)
@@ -468,7 +514,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def_readonly("overlapped_us", &PingPongStats::overlapped_us)
       .def_readonly("verified", &PingPongStats::verified)
       .def("latency_us", &PingPongStats::latency_us)
-      .def("bandwidth_gbps", &PingPongStats::bandwidth_gbps);
+      .def("bandwidth_gbps", &PingPongStats::bandwidth_gbps)
+      .def("bidir_gbps", &PingPongStats::bidir_gbps);
   m.def(
       "pingpong_rccl",
       [](const RcclComm& c, int peer, std::uintptr_t sb, std::uintptr_t rb, size_t bytes, int warmup, int reps,

@@ -1,6 +1,8 @@
 #include "mxs/halo/exchange.hpp"
 #include "mxs/core/trace.hpp"
 
+#include <cstdlib>
+
 namespace mxs {
 
 namespace {
@@ -80,10 +82,23 @@ void HaloExchanger<T>::check() const {
   if (ipc_) ipc_->check();
 }
 
+namespace {
+// Workgroups per copy segment of the pack / unpack launches (0 = sized from the
+// largest segment). MXS_HALO_GRID overrides it (tuning the frame-first overlap,
+// where the copies run beside the pipeline pass).
+int halo_grid() {
+  static const int g = [] {
+    const char* e = std::getenv("MXS_HALO_GRID");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  return g;
+}
+}  // namespace
+
 template <typename T>
 void HaloExchanger<T>::pack(T* tile, hipStream_t stream) {
   MXS_TRACE_RANGE("halo.pack");
-  kernels::copy2d_batch<T>(tile, send_.get(), recv_.get(), progs_.pack, stream);
+  kernels::copy2d_batch<T>(tile, send_.get(), recv_.get(), progs_.pack, stream, halo_grid(), copy_block_);
 }
 
 template <typename T>
@@ -104,7 +119,7 @@ void HaloExchanger<T>::transfer(hipStream_t stream) {
 template <typename T>
 void HaloExchanger<T>::unpack(T* tile, hipStream_t stream) {
   MXS_TRACE_RANGE("halo.unpack");
-  kernels::copy2d_batch<T>(tile, send_.get(), recv_.get(), progs_.unpack, stream);
+  kernels::copy2d_batch<T>(tile, send_.get(), recv_.get(), progs_.unpack, stream, halo_grid(), copy_block_);
   if (ipc_) ipc_->release(stream);  // receive buffer consumed: senders may write the next exchange
 }
 

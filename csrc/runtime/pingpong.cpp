@@ -73,6 +73,14 @@ void round_trip(const RcclComm& comm, int peer, void* sendbuf, void* recvbuf, si
   }
 }
 
+// Both sides send and receive at once (grouped, so neither blocks the other).
+void exchange(const RcclComm& comm, int peer, void* sendbuf, void* recvbuf, size_t bytes, hipStream_t s) {
+  comm.group_start();
+  comm.send<unsigned char>(static_cast<unsigned char*>(sendbuf), bytes, peer, s);
+  comm.recv<unsigned char>(static_cast<unsigned char*>(recvbuf), bytes, peer, s);
+  comm.group_end();
+}
+
 }  // namespace
 
 PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void* recvbuf, size_t bytes, int warmup,
@@ -82,6 +90,8 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
   st.bytes = bytes;
   MXS_CHECK(peer >= 0 && peer < comm.size(), "pingpong: bad peer " << peer);
   const bool ping = comm.rank() <= peer;
+  const bool bidir = mode == PingPongMode::Bidirectional;
+  st.bidirectional = bidir;
   // Every wait on the transfer stream goes through the communication watchdog
   // (--comm-timeout): a dead or hung peer fails the run instead of hanging it.
   auto drain = [&](const char* what) {
@@ -91,11 +101,15 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
   // Deterministic payload (the reference filled host_data[i] = i, mpi-pingpong-gpu.cpp:44).
   std::vector<unsigned char> pattern(bytes);
   for (size_t i = 0; i < bytes; ++i) pattern[i] = static_cast<unsigned char>((i * 131u + 7u) % 251u);
-  if (ping) MXS_HIP_CHECK(hipMemcpy(sendbuf, pattern.data(), bytes, hipMemcpyHostToDevice));
+  if (ping || bidir) MXS_HIP_CHECK(hipMemcpy(sendbuf, pattern.data(), bytes, hipMemcpyHostToDevice));
   MXS_HIP_CHECK(hipMemsetAsync(recvbuf, 0, bytes, stream));
   MXS_HIP_CHECK(hipStreamSynchronize(stream));
 
-  for (int i = 0; i < warmup; ++i) round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
+  auto trip = [&]() {
+    if (bidir) exchange(comm, peer, sendbuf, recvbuf, bytes, stream);
+    else round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
+  };
+  for (int i = 0; i < warmup; ++i) trip();
   drain("pingpong warm-up (RCCL)");
 
   std::vector<double> rtts;
@@ -115,7 +129,7 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
     Event e0(true), e1(true);
     for (int b = 0; b < batches; ++b) {
       e0.record(stream);
-      for (int i = 0; i < per; ++i) round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
+      for (int i = 0; i < per; ++i) trip();
       e1.record(stream);
       drain("pingpong batch (RCCL)");
       rtts.push_back(double(e1.since(e0)) * 1000.0 / per);
@@ -158,7 +172,7 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
   }
   fill_stats(st, rtts);
 
-  if (ping) {
+  if (ping || bidir) {  // bidirectional: each side received the other's copy of the pattern
     std::vector<unsigned char> back(bytes);
     MXS_HIP_CHECK(hipMemcpy(back.data(), recvbuf, bytes, hipMemcpyDeviceToHost));
     st.verified = std::equal(back.begin(), back.end(), pattern.begin());

@@ -72,8 +72,13 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
                    cfg_.kind == StencilKind::Jacobi5 && cfg_.variant == kernels::StencilVariant::Auto &&
                    block_ > 1 && !cfg_.overlap;
   if (frame_allowed_) {
-    frame_ctl_.reset(2);
-    MXS_HIP_CHECK(hipMemsetAsync(frame_ctl_.get(), 0, 2 * sizeof(unsigned), main_.get()));
+    // One-wave copy workgroups: they fit beside a pipeline workgroup (4-wave
+    // ones did not get placed until the pass ended, profiles/r03_window4).
+    ex_->set_copy_block(64);
+    frame_ctl_.reset(1);
+    MXS_HIP_CHECK(hipMemsetAsync(frame_ctl_.get(), 0, sizeof(unsigned), main_.get()));
+    frame_status_.reset(1, hipHostMallocCoherent | hipHostMallocMapped);
+    *frame_status_.get() = 0;
     const double limit = comm_timeout() > 0 ? comm_timeout() : 600.0;
     frame_timeout_ticks_ = std::uint64_t(limit * kernels::wall_clock_hz());
   }
@@ -151,7 +156,7 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
     kernels::stencil5_frame_pass<T>(cur, nxt, tile_, cfg_.coeffs, fp->shape, fp->table.get(), fp->sched.entries,
                                     frame_ctl_.get(), side);
     interior_.record(side);
-    kernels::wait_counter(frame_ctl_.get(), unsigned(fp->sched.signals), frame_timeout_ticks_, frame_ctl_.get() + 1, m);
+    kernels::wait_counter(frame_ctl_.get(), unsigned(fp->sched.signals), frame_timeout_ticks_, frame_status_.get(), m);
     ex_->exchange(nxt, m);
     interior_.wait_on(m);
     return;
@@ -253,6 +258,12 @@ bool StencilSolver<T>::capture(GraphSet& gs) {
 template <typename T>
 typename StencilSolver<T>::GraphSet* StencilSolver<T>::graphs_for(int S, int count) {
   if (!cfg_.use_graph) return nullptr;
+  // Long super-steps: eager launches beat the graph's replay (header).
+  const double est_us = double(tile_.width) * double(tile_.height) * S / 9e6;
+  if (cfg_.graph_max_superstep_us > 0 && est_us > cfg_.graph_max_superstep_us) {
+    graph_status_ = "eager (super-steps of ~" + std::to_string(int(est_us)) + " us)";
+    return nullptr;
+  }
   for (auto& gs : graphs_)
     if (gs->S == S) return gs->ok ? gs.get() : nullptr;
   if (int(graphs_.size()) >= kMaxGraphSets) {
@@ -380,7 +391,7 @@ typename StencilSolver<T>::FramePass* StencilSolver<T>::frame_pass(int S, bool b
     const char* e = std::getenv(k);
     return e && *e ? std::atoi(e) : dflt;
   };
-  const int comm = cfg_.frame_comm_wgs >= 0 ? cfg_.frame_comm_wgs : env_int("MXS_FRAME_COMM_WGS", 8);
+  const int comm = cfg_.frame_comm_wgs >= 0 ? cfg_.frame_comm_wgs : env_int("MXS_FRAME_COMM_WGS", 16);
   const int rows = cfg_.frame_rows > 0 ? cfg_.frame_rows : env_int("MXS_FRAME_ROWS", 0);
   // Edge groups: those holding output columns of the S-wide left / right bands.
   const int left = int(std::min<index_t>(shape.groups, (S + shape.owg - 1) / shape.owg));
@@ -489,8 +500,7 @@ void StencilSolver<T>::synchronize() {
   ex_->check();  // IPC backend: device-side waits carry their own deadline
   if (direct_) direct_->check();
   if (frame_allowed_) {
-    unsigned st = 0;
-    MXS_HIP_CHECK(hipMemcpy(&st, frame_ctl_.get() + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+    const unsigned st = __atomic_load_n(frame_status_.get(), __ATOMIC_ACQUIRE);
     MXS_CHECK(st == 0, "frame-first pass: the halo exchange's wait for the pass's frame counter hit its deadline");
   }
 }

@@ -10,9 +10,10 @@ and unidirectional bandwidth (bytes / (RTT/2)).
 Transports:
   ``rccl``   native RCCL send/recv between rank 0 and rank 1 (xGMI), modes
              blocking (host sync per round trip), async (stream-pipelined,
-             hipEvent-timed) and overlap (async beside an ALU-bound kernel on a
+             hipEvent-timed), overlap (async beside an ALU-bound kernel on a
              second stream, sized to the transfer time: compute alone, comm
-             alone and both together are reported);
+             alone and both together are reported) and bidir (both ranks send
+             at once: the link's two directions together, bidir_gbps);
   ``ipc``    device-initiated: HIP IPC mailboxes in each rank's HBM, one
              persistent kernel per rank writes the payload into the peer's
              mailbox over xGMI and spins on a system-scope flag for the echo
@@ -91,7 +92,7 @@ class PingPong:
             if not self.active:
                 return rec
             m = {"blocking": H.PingPongMode.BLOCKING, "async": H.PingPongMode.ASYNC,
-                 "overlap": H.PingPongMode.OVERLAP}[mode]
+                 "overlap": H.PingPongMode.OVERLAP, "bidir": H.PingPongMode.BIDIRECTIONAL}[mode]
             st = H.pingpong_rccl(self.comm, self.peer, self.send.data_ptr(), self.recv.data_ptr(), nbytes, warmup,
                                  reps, m, stream)
         elif self.transport in ("d2d", "pinned", "pageable"):
@@ -113,6 +114,12 @@ class PingPong:
             raise ValueError(self.transport)
         rec.update(rtt_us=st.median_rtt_us, rtt_min_us=st.min_rtt_us, rtt_max_us=st.max_rtt_us,
                    latency_us=st.latency_us(), gbps=st.bandwidth_gbps(), reps=st.reps, passed=st.verified)
+        # How the time was taken: "device" = hipEvents around back-to-back trips
+        # (the transport's own latency); "host" = host clock around each trip +
+        # stream synchronisation (blocking mode: launch + sync overhead included).
+        rec["timing"] = "host" if mode == "blocking" else "device"
+        if mode == "bidir":
+            rec["bidir_gbps"] = st.bidir_gbps()
         if mode == "overlap":
             rec.update(compute_alone_us=st.compute_alone_us, comm_alone_us=st.comm_alone_us,
                        overlapped_us=st.overlapped_us)
@@ -143,7 +150,7 @@ class PingPong:
         sm = summarize(times)
         ok = bool(torch.equal(r, s)) if self.ctx.rank == 0 else True
         rec.update(rtt_us=sm.median, rtt_min_us=sm.min, rtt_max_us=sm.max, latency_us=sm.median / 2,
-                   gbps=nbytes / (sm.median * 0.5e-6) / 1e9, reps=reps, passed=ok)
+                   gbps=nbytes / (sm.median * 0.5e-6) / 1e9, reps=reps, passed=ok, timing="host")
         return rec
 
 
@@ -165,7 +172,7 @@ def main(argv=None) -> int:
     p.add_argument("--sweep", default="8:268435456")
     p.add_argument("--transport", default="rccl",
                    choices=["rccl", "loopback", "ipc", "ipc-loopback", "torch", "d2d", "pinned", "pageable"])
-    p.add_argument("--mode", default="blocking", choices=["blocking", "async", "overlap"])
+    p.add_argument("--mode", default="blocking", choices=["blocking", "async", "overlap", "bidir"])
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--json", default=None)

@@ -80,9 +80,13 @@ class StencilConfig:
     # RCCL backend with remote peers: frame-first overlap — each pass stores its
     # S-deep output frame first and the next halo exchange (pack -> RCCL ->
     # unpack) runs under the rest of the pass (runtime/stencil_solver.hpp).
-    frame_overlap: bool = True
+    # Opt-in: on one GPU it measured slower than the serial schedule (docs/PERF.md).
+    frame_overlap: bool = False
     frame_comm_wgs: int = -1         # frame-only workgroups leaving CUs to the exchange (-1 = default)
     frame_rows: int = 0              # frame chunk height (0 = auto)
+    # Super-steps estimated longer than this run from eager launches, not a
+    # hipGraph (long passes: eager measured faster). 0 = always graphs.
+    graph_max_superstep_us: float = 150.0
 
     @property
     def halo(self) -> int:
@@ -169,7 +173,8 @@ class Stencil2D:
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
                                           backend == "ipc" and cfg.direct_halo is not False,
-                                          cfg.frame_overlap, cfg.frame_comm_wgs, cfg.frame_rows)
+                                          cfg.frame_overlap, cfg.frame_comm_wgs, cfg.frame_rows,
+                                          cfg.graph_max_superstep_us)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()

@@ -42,7 +42,9 @@ def test_bench_two_ranks_cpu_extras():
     assert ex["process_grid"] == "2 rows x 1 cols of ranks"
     assert ex["dot_8192_f64_verified"] is True
     # CPU rehearsal of the ping-pong sweep: gloo send/recv, 8 B .. 4 KiB.
-    assert ex["pingpong_torch_blocking_8B_latency_us"] > 0 and ex["pingpong_verified"] is True
+    # Host-timed round trips are labelled as such, not as a latency.
+    assert ex["pingpong_torch_blocking_8B_host_rtt_us"] > 0 and ex["pingpong_verified"] is True
+    assert "pingpong_torch_blocking_8B_latency_us" not in ex
     assert ex["pingpong_sweep_file"].endswith("bench_pingpong_n2.json")
 
 

@@ -26,6 +26,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _loopback(w, h, dtype="f32", **kw):
+    kw.setdefault("frame_overlap", True)  # opt-in (off by default, docs/PERF.md)
     return Stencil2D(StencilConfig(global_width=w, global_height=h, dims="1x1", dtype=dtype, backend="rccl",
                                    loopback=True, **kw))
 
@@ -46,8 +47,8 @@ def _frame_kernel(sum_form):
 def test_frame_overlap_bitwise_vs_serial(gpu, w, h, dtype, S, runs, sum_form):
     """The overlapped schedule changes only the order of the work: the field is
     bitwise the serial schedule's (pack -> RCCL -> unpack, then the pass)."""
-    a = _loopback(w, h, dtype, seed=w + h, sum_form=sum_form)
-    b = _loopback(w, h, dtype, seed=w + h, sum_form=sum_form, frame_overlap=False)
+    a = _loopback(w, h, dtype, seed=w + h, sum_form=sum_form, time_block=S)
+    b = _loopback(w, h, dtype, seed=w + h, sum_form=sum_form, frame_overlap=False, time_block=S)
     assert a.time_block == S and b.time_block == S
     assert a.solver.frame_overlap(S) and not b.solver.frame_overlap(S)
     assert "frame-first" in a.halo_mode() and "frame-first" not in b.halo_mode()
@@ -72,7 +73,7 @@ def test_rccl_solver_production_depth_per_step_bitwise(gpu, w, h, S, frame):
     """RCCL loopback at the production depths (20 / 24; 3 S steps = three full
     passes, graph chains on the serial path) in the per-step form equals as
     many single steps bit for bit."""
-    st = _loopback(w, h, seed=3, sum_form=False, frame_overlap=frame)
+    st = _loopback(w, h, seed=3, sum_form=False, frame_overlap=frame, time_block=S)
     assert st.time_block == S and st.solver.frame_overlap(S) == frame
     st.run(3 * S)
     st.synchronize()

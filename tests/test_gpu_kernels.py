@@ -189,7 +189,7 @@ def test_pingpong_local_paths(gpu):
         assert st.verified and st.median_rtt_us > 0
 
 
-@pytest.mark.parametrize("mode", ["BLOCKING", "ASYNC"])
+@pytest.mark.parametrize("mode", ["BLOCKING", "ASYNC", "BIDIRECTIONAL"])
 def test_pingpong_rccl_loopback(gpu, mode):
     H = pkg.hip()
     comm = H.RcclComm(H.RcclComm.make_unique_id(), 1, 0)
@@ -199,3 +199,6 @@ def test_pingpong_rccl_loopback(gpu, mode):
         st = H.pingpong_rccl(comm, 0, a.data_ptr(), b.data_ptr(), nb, 2, 10, getattr(H.PingPongMode, mode),
                              torch.cuda.current_stream().cuda_stream)
         assert st.verified and st.median_rtt_us > 0
+        if mode == "BIDIRECTIONAL":  # a sample is one exchange: both directions moved nb bytes
+            assert st.bidir_gbps() == pytest.approx(2 * st.bandwidth_gbps())
+            assert st.bandwidth_gbps() == pytest.approx(nb / (st.median_rtt_us * 1e-6) / 1e9)
