@@ -22,6 +22,12 @@
 // any non-periodic dimension therefore runs S = 1 (one exchange per iteration),
 // so every backend agrees with the S = 1 result.
 //
+// Per super-step (cur -> nxt), serial (the default): the pass on the main
+// stream, then the exchange of its output (pack(nxt) -> RCCL -> unpack(nxt)):
+// post-exchange, so a pass never waits for the host to enqueue the RCCL group
+// (the first pass of a run is preceded by one exchange when cur's ghost ring
+// is not fresh: construction, field_changed(), a thin-strip overlap step).
+//
 // Per super-step (cur -> nxt), with `overlap` on and S > 1:
 //
 //   main stream : record(fork) -> pack(cur) -> wire (RCCL send/recv or IPC put/wait)
@@ -223,6 +229,10 @@ class StencilSolver {
     DeviceBuffer<kernels::FrameChunk> table;
   };
   FramePass* frame_pass(int S, bool build);  // nullptr: serial schedule for S
+  // Super-steps exchange AFTER their pass (the ghost ring of the next pass's
+  // input): every schedule but the fused periodic, the direct IPC halo and the
+  // thin-strip overlap, which exchange first.
+  bool post_exchange() const { return !fused_ && !direct_ && !cfg_.overlap; }
   void ensure_range();                       // sum-form range check (host sync)
   void begin_run();                          // range check + prime
   bool frame_allowed_ = false;               // config / backend / peers allow the overlap

@@ -162,8 +162,12 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
     return;
   }
   if (!cfg_.overlap) {
-    ex_->exchange(cur, m);
+    // Post-exchange: the pass first (cur's ghost ring is fresh, run_group
+    // sees to it), then the exchange of its output. The pass is on the GPU
+    // before the host has enqueued the RCCL group (~25 us of host time that
+    // a pre-exchange super-step leaves the GPU idle for).
     update(cur, nxt, S, 0, w, 0, h, m);
+    ex_->exchange(nxt, m);
     return;
   }
   const index_t d = std::max(radius_, S);  // dependency depth of the super-step
@@ -298,10 +302,11 @@ template <typename T>
 void StencilSolver<T>::run_group(int S, int count) {
   if (count <= 0) return;
   last_blocks_.emplace_back(S, count);
-  if (frame_pass(S, true)) {
-    // Post-exchange super-steps: cur's ghost ring must be fresh before the
-    // first one; each leaves the next one's fresh. Eager launches (header).
-    if (!ghost_fresh_) ex_->exchange(cur_, main_.get());
+  // Post-exchange super-steps (frame-first and serial): cur's ghost ring must
+  // be fresh before the first one; each leaves the next one's fresh. The
+  // thin-strip overlap schedule exchanges first and leaves it stale.
+  if (post_exchange() && !ghost_fresh_) ex_->exchange(cur_, main_.get());
+  if (frame_pass(S, true)) {  // eager launches (header)
     for (int i = 0; i < count; ++i) {
       enqueue_block(cur_, nxt_, S);
       std::swap(cur_, nxt_);
@@ -309,7 +314,7 @@ void StencilSolver<T>::run_group(int S, int count) {
     ghost_fresh_ = true;
     return;
   }
-  ghost_fresh_ = false;  // a serial super-step exchanges first and leaves the new ghost ring stale
+  ghost_fresh_ = post_exchange();
   int i = 0;
   if (GraphSet* gs = graphs_for(S, count)) {
     for (; i + gs->chain <= count; i += gs->chain) {
@@ -442,7 +447,8 @@ void StencilSolver<T>::prepare(int iters) {
   split(iters, gr);
   for (const Group& g : gr) {
     if (g.count <= 0) continue;
-    if (frame_pass(g.S, true) && !ghost_fresh_) {
+    (void)frame_pass(g.S, true);
+    if (post_exchange() && !ghost_fresh_) {
       ex_->exchange(cur_, main_.get());
       ghost_fresh_ = true;
     }
@@ -464,11 +470,11 @@ void StencilSolver<T>::warm(int iters, int passes) {
   begin_run();
   Group gr[2];
   split(iters, gr);
-  for (const Group& g : gr)
-    if (g.count > 0 && frame_pass(g.S, true) && !ghost_fresh_) {
-      ex_->exchange(cur_, main_.get());
-      ghost_fresh_ = true;
-    }
+  for (const Group& g : gr) (void)frame_pass(g.S, g.count > 0);
+  if (post_exchange() && !ghost_fresh_) {
+    ex_->exchange(cur_, main_.get());
+    ghost_fresh_ = true;
+  }
   for (int p = 0; p < passes; ++p)
     for (const Group& g : gr)
       if (g.count > 0) enqueue_block(cur_, nxt_, g.S);  // cur -> nxt, no swap: state unchanged
