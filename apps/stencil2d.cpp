@@ -4,7 +4,9 @@
 // MPI is the control plane (ranks, Cartesian grid, RCCL bootstrap, timing);
 // device data moves by one of:
 //   --backend rccl        per-peer ncclSend/ncclRecv over xGMI (default when every
-//                         rank has its own GPU), compute/comm overlap + hipGraph;
+//                         rank has its own GPU): each pass, then the exchange of its
+//                         output (post-exchange); --frame-overlap runs the exchange
+//                         under a frame-first pass instead (opt-in, docs/PERF.md);
 //   --backend ipc         HIP IPC: direct writes into the peers' receive buffers,
 //                         device-side ready/free counters, overlap + hipGraph
 //                         (default when ranks share a GPU, where RCCL refuses);
@@ -19,6 +21,7 @@
 // Positional arguments keep the reference contract: [local width (= height) [stencil width]].
 // More options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
 // --iters N, --warmup N, --time-block S (default: measured per tile size and dtype), --no-overlap, --no-graph,
+// --frame-overlap,
 // --no-direct-halo (IPC backend: pack -> put -> unpack instead of the device-initiated push),
 // --c-center C --c-neighbor C (default 0.2 / 0.2), --no-sum-form (keep the per-step evaluation in the
 // time-blocked kernels: bitwise equal to the CPU app; default: sum form when the coefficients are equal),
@@ -119,6 +122,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   kernels::set_gpu_share(shared_gpu ? std::max(1, env.local_size() / std::max(1, dev.devices_used)) : 1);
   cfg.overlap = cli.flag("overlap") || (!cli.flag("no-overlap") && !shared_gpu && time_block == 1);
   cfg.use_graph = !cli.flag("no-graph");
+  cfg.frame_overlap = cli.flag("frame-overlap");
   cfg.loopback_self = loopback;
   cfg.coeffs = {c_center, c_neighbor, sum_form};
   cfg.time_block = time_block;
