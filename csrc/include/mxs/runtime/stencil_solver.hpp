@@ -54,9 +54,11 @@
 // counter and exchanges the NEXT super-step's halo (pack -> RCCL -> unpack of
 // nxt) while the pass finishes the interior:
 //
-//   side stream : wait(fork) -> frame-first pass cur -> nxt -> record(done)
+//   side stream : wait(fork) -> frame-first pass cur -> nxt
 //   main stream : record(fork) -> wait_counter -> pack(nxt) -> RCCL -> unpack(nxt)
-//                 -> wait(done)
+//
+// (the next super-step's fork is recorded after that unpack; the main stream
+// joins the side stream once, after the last super-step of a run)
 //
 // so cur's ghost ring is fresh whenever a pass starts (the first pass of a run
 // is preceded by one exchange when it is not: construction, field_changed(), a
@@ -236,6 +238,8 @@ class StencilSolver {
   void ensure_range();                       // sum-form range check (host sync)
   void begin_run();                          // range check + prime
   bool frame_allowed_ = false;               // config / backend / peers allow the overlap
+  bool side_pending_ = false;                // frame passes on the side stream not yet joined to main
+  void join_side();                          // main stream waits for the side stream's work
   std::vector<std::unique_ptr<FramePass>> frames_;
   std::vector<int> no_frame_;                // depths without a frame form
   DeviceBuffer<unsigned> frame_ctl_;         // frame counter (device memory)
