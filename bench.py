@@ -204,9 +204,9 @@ def main(argv=None) -> int:
                    help="N = 1: explicit self-exchange (copies into the ghost ring) + the ghost-ring pass instead "
                         "of the wrap-around addressing")
     p.add_argument("--frame-overlap", action="store_true",
-                   help="multi-GPU: exchange the next halo under the pass (frame-first overlap) instead of "
-                        "before it (serial, the default; docs/PERF.md)")
-    p.add_argument("--no-frame-overlap", action="store_true", help=argparse.SUPPRESS)
+                   help="multi-GPU: always exchange the next halo under the pass (frame-first overlap); default: "
+                        "prepare() times it against the serial schedule and keeps the faster (docs/PERF.md)")
+    p.add_argument("--no-frame-overlap", action="store_true", help="multi-GPU: always the serial schedule")
     p.add_argument("--overlap", action="store_true", help="force the interior/exchange overlap schedule")
     p.add_argument("--loopback", action="store_true",
                    help="1 GPU: route the self-neighbour halos through RCCL (exercises the multi-GPU schedule)")
@@ -248,7 +248,7 @@ def main(argv=None) -> int:
                         overlap=False if args.no_overlap else (True if args.overlap else None),
                         graph=not args.no_graph,
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback,
-                        sum_form=not args.no_sum_form, frame_overlap=args.frame_overlap and not args.no_frame_overlap,
+                        sum_form=not args.no_sum_form, frame_overlap=(True if args.frame_overlap else (False if args.no_frame_overlap else None)),
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3)
@@ -281,6 +281,10 @@ def main(argv=None) -> int:
         extras["pipe_balanced_shares"] = bool(hip().pipe_balanced())  # MXS_PIPE_BALANCED=0: equal row shares
         if st.solver is not None and not st.solver.fused_periodic():
             extras["frame_overlap"] = bool(timed_blocks and st.solver.frame_overlap(timed_blocks[0][0]))
+            choice, serial_ms, frame_ms = st.solver.frame_choice()
+            if choice:  # measured by prepare(): ms per super-step of each schedule
+                extras["schedule_choice"] = {"chosen": choice, "serial_ms": round(serial_ms, 4),
+                                             "frame_first_ms": round(frame_ms, 4)}
     del st
     if gpu:
         torch.cuda.empty_cache()

@@ -46,7 +46,8 @@
 // grid fuses the self-exchange into the kernel's wrap-around addressing
 // (`fuse_periodic_self`).
 //
-// Frame-first overlap (`frame_overlap`, the multi-GPU default): with remote
+// Frame-first overlap (`frame_overlap` forces it; `frame_auto`, the default, picks it
+// when prepare() measures it faster than the serial schedule): with remote
 // peers over RCCL and a depth that has a frame form (fp32 S = 20 / 24, fp64
 // S = 16: kernels::frame_pass_shape), a super-step is one pass on the side
 // stream whose chunk order (kernels/frame_schedule.hpp) stores the S-deep output
@@ -129,6 +130,10 @@ struct SolverConfig {
   // "Frame-first overlap"); it is exact and tested, and stays opt-in until a
   // multi-GPU run shows the wire time it hides is worth the copies' interference.
   bool frame_overlap = false;
+  // Auto: when frame_overlap is allowed here, prepare() times a few super-steps
+  // of each schedule (state-preserving, collective like prepare itself) and
+  // keeps the faster one; until then, and when no prepare() runs, serial.
+  bool frame_auto = true;
   // Frame-only workgroups that exit early and leave their CUs to the exchange
   // (-1: MXS_FRAME_COMM_WGS or 16), and the frame chunk height (0: MXS_FRAME_ROWS
   // or auto, kernels::make_frame_schedule).
@@ -186,6 +191,11 @@ class StencilSolver {
   bool overlapped() const { return cfg_.overlap; }
   // Whether super-steps of depth S run the frame-first overlapped schedule.
   bool frame_overlap(int S) const;
+  // The auto choice: "" before prepare() decided, else "frame" or "serial" and
+  // the median times (ms per super-step) of both.
+  const std::string& frame_choice() const { return frame_choice_; }
+  double frame_choice_serial_ms() const { return choice_ms_[0]; }
+  double frame_choice_frame_ms() const { return choice_ms_[1]; }
   // Whether the passes currently take the sum form (coefficients, user choice
   // and the measured range all allow it).
   bool sum_form_active() const { return cfg_.coeffs.sum_form && kernels::uses_sum_form(cfg_.coeffs); }
@@ -238,6 +248,10 @@ class StencilSolver {
   void ensure_range();                       // sum-form range check (host sync)
   void begin_run();                          // range check + prime
   bool frame_allowed_ = false;               // config / backend / peers allow the overlap
+  bool frame_on_ = false;                    // the frame-first schedule is in use (forced, or chosen)
+  std::string frame_choice_;
+  double choice_ms_[2] = {0, 0};
+  void choose_schedule(int S);               // frame_auto: time both, keep the faster
   bool side_pending_ = false;                // frame passes on the side stream not yet joined to main
   void join_side();                          // main stream waits for the side stream's work
   std::vector<std::unique_ptr<FramePass>> frames_;

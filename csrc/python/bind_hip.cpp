@@ -398,8 +398,9 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        bool use_graph, bool loopback_self, StencilKind kind, double c0, double c1, int box_radius,
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
                        py::object bootstrap, int graph_supersteps, bool sum_form, bool direct_halo, bool frame_overlap,
-                       int frame_comm_wgs, int frame_rows, double graph_max_superstep_us) {
+                       int frame_comm_wgs, int frame_rows, double graph_max_superstep_us, bool frame_auto) {
              SolverConfig cfg;
+             cfg.frame_auto = frame_auto;
              cfg.graph_max_superstep_us = graph_max_superstep_us;
              cfg.frame_overlap = frame_overlap;
              cfg.frame_comm_wgs = frame_comm_wgs;
@@ -434,13 +435,20 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
            py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = false,
            py::arg("frame_overlap") = false, py::arg("frame_comm_wgs") = -1, py::arg("frame_rows") = 0,
-           py::arg("graph_max_superstep_us") = 150.0,
+           py::arg("graph_max_superstep_us") = 150.0, py::arg("frame_auto") = true,
            py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")
       .def(
           "frame_overlap", [](SolverHandle& h, int S) { return h.visit([S](auto& s) { return s.frame_overlap(S); }); },
           py::arg("S"), "whether super-steps of depth S run the frame-first overlapped schedule")
+      .def("frame_choice",
+           [](SolverHandle& h) {
+             return h.visit([](auto& s) {
+               return py::make_tuple(s.frame_choice(), s.frame_choice_serial_ms(), s.frame_choice_frame_ms());
+             });
+           },
+           "auto schedule choice made by prepare(): (\"\" | \"serial\" | \"frame\", serial ms, frame ms per super-step)")
       .def("sum_form_active", [](SolverHandle& h) { return h.visit([](auto& s) { return s.sum_form_active(); }); })
       .def("sum_form_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.sum_form_note(); }); })
       .def("last_run_blocks", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_blocks(); }); },

@@ -68,13 +68,12 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
            kernels::stencil5_periodic_supported<T>(tile_);
   // Frame-first overlap: RCCL with a wire transfer, the tuned kernel forms,
   // every edge a neighbour's (time blocking), the thin-strip overlap off.
-  frame_allowed_ = cfg_.frame_overlap && cfg_.backend == HaloBackend::Rccl && !plan.sends.empty() && !fused_ &&
+  frame_allowed_ = (cfg_.frame_overlap || cfg_.frame_auto) && cfg_.backend == HaloBackend::Rccl &&
+                   !plan.sends.empty() && !fused_ &&
                    cfg_.kind == StencilKind::Jacobi5 && cfg_.variant == kernels::StencilVariant::Auto &&
                    block_ > 1 && !cfg_.overlap;
+  frame_on_ = frame_allowed_ && cfg_.frame_overlap;
   if (frame_allowed_) {
-    // One-wave copy workgroups: they fit beside a pipeline workgroup (4-wave
-    // ones did not get placed until the pass ended, profiles/r03_window4).
-    ex_->set_copy_block(64);
     frame_ctl_.reset(1);
     MXS_HIP_CHECK(hipMemsetAsync(frame_ctl_.get(), 0, sizeof(unsigned), main_.get()));
     frame_status_.reset(1, hipHostMallocCoherent | hipHostMallocMapped);
@@ -169,6 +168,9 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
       const char* e = std::getenv("MXS_FRAME_PROBE");
       return e && *e ? std::atoi(e) : 0;
     }();
+    // One-wave copy workgroups: they fit beside a pipeline workgroup (4-wave
+    // ones were not placed until the pass ended, profiles/r03_window4).
+    ex_->set_copy_block(64);
     if (probe == 0) {
       ex_->exchange(nxt, m);
     } else {
@@ -184,6 +186,7 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
     // before the host has enqueued the RCCL group (~25 us of host time that
     // a pre-exchange super-step leaves the GPU idle for).
     update(cur, nxt, S, 0, w, 0, h, m);
+    ex_->set_copy_block(0);  // alone on the GPU: the default (256-thread) copies
     ex_->exchange(nxt, m);
     return;
   }
@@ -401,7 +404,7 @@ void StencilSolver<T>::run(int iters) {
 
 template <typename T>
 typename StencilSolver<T>::FramePass* StencilSolver<T>::frame_pass(int S, bool build) {
-  if (!frame_allowed_) return nullptr;
+  if (!frame_on_) return nullptr;
   for (auto& f : frames_)
     if (f->S == S) return f.get();
   if (!build || std::find(no_frame_.begin(), no_frame_.end(), S) != no_frame_.end()) return nullptr;
@@ -444,11 +447,51 @@ typename StencilSolver<T>::FramePass* StencilSolver<T>::frame_pass(int S, bool b
 
 template <typename T>
 bool StencilSolver<T>::frame_overlap(int S) const {
+  if (!frame_on_) return false;
   for (const auto& f : frames_)
     if (f->S == S) return true;
-  if (!frame_allowed_) return false;
   return std::find(no_frame_.begin(), no_frame_.end(), S) == no_frame_.end() &&
          kernels::frame_pass_shape<T>(tile_, S, cfg_.coeffs, nullptr);
+}
+
+// frame_auto: median of 3 alternating timings of 2 state-preserving
+// super-steps (cur -> nxt, no swap) per schedule. Both schedules post-exchange
+// and issue the same RCCL groups in the same order, so ranks that choose
+// differently still match each other's sends and receives.
+template <typename T>
+void StencilSolver<T>::choose_schedule(int S) {
+  if (!frame_allowed_ || !cfg_.frame_auto || cfg_.frame_overlap || !frame_choice_.empty()) return;
+  frame_on_ = true;
+  const bool has_frame = frame_pass(S, true) != nullptr;
+  if (!has_frame) {
+    frame_on_ = false;
+    return;  // no frame form at this depth: nothing to choose (decided at the next prepare)
+  }
+  if (!ghost_fresh_) {
+    ex_->exchange(cur_, main_.get());
+    ghost_fresh_ = true;
+  }
+  std::vector<double> t[2];
+  Event e0(true), e1(true);
+  for (int rep = 0; rep < 4; ++rep)
+    for (int mode = 0; mode < 2; ++mode) {
+      frame_on_ = mode == 1;
+      join_side();
+      main_.sync();
+      side_.sync();
+      e0.record(main_.get());
+      for (int i = 0; i < 2; ++i) enqueue_block(cur_, nxt_, S);
+      join_side();
+      e1.record(main_.get());
+      e1.sync();
+      if (rep > 0) t[mode].push_back(double(e1.since(e0)) / 2.0);  // the first round warms both
+    }
+  for (int mode = 0; mode < 2; ++mode) {
+    std::sort(t[mode].begin(), t[mode].end());
+    choice_ms_[mode] = t[mode][t[mode].size() / 2];
+  }
+  frame_on_ = choice_ms_[1] < choice_ms_[0];
+  frame_choice_ = frame_on_ ? "frame" : "serial";
 }
 
 template <typename T>
@@ -471,6 +514,9 @@ void StencilSolver<T>::prepare(int iters) {
   begin_run();
   Group gr[2];
   split(iters, gr);
+  // frame_auto: decide the schedule at the depth of the larger group.
+  const Group& big = gr[0].count >= gr[1].count ? gr[0] : gr[1];
+  if (big.count > 0) choose_schedule(big.S);
   for (const Group& g : gr) {
     if (g.count <= 0) continue;
     (void)frame_pass(g.S, true);
@@ -533,7 +579,7 @@ void StencilSolver<T>::synchronize() {
   side_.sync();
   ex_->check();  // IPC backend: device-side waits carry their own deadline
   if (direct_) direct_->check();
-  if (frame_allowed_) {
+  if (frame_status_.get()) {
     const unsigned st = __atomic_load_n(frame_status_.get(), __ATOMIC_ACQUIRE);
     MXS_CHECK(st == 0, "frame-first pass: the halo exchange's wait for the pass's frame counter hit its deadline");
   }

@@ -80,8 +80,10 @@ class StencilConfig:
     # RCCL backend with remote peers: frame-first overlap — each pass stores its
     # S-deep output frame first and the next halo exchange (pack -> RCCL ->
     # unpack) runs under the rest of the pass (runtime/stencil_solver.hpp).
-    # Opt-in: on one GPU it measured slower than the serial schedule (docs/PERF.md).
-    frame_overlap: bool = False
+    # True forces it, False never, None (default) lets prepare() time both
+    # schedules and keep the faster (on one GPU through RCCL loopback: serial,
+    # docs/PERF.md).
+    frame_overlap: bool | None = None
     frame_comm_wgs: int = -1         # frame-only workgroups leaving CUs to the exchange (-1 = default)
     frame_rows: int = 0              # frame chunk height (0 = auto)
     # Super-steps estimated longer than this run from eager launches, not a
@@ -173,8 +175,8 @@ class Stencil2D:
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
                                           backend == "ipc" and cfg.direct_halo is not False,
-                                          cfg.frame_overlap, cfg.frame_comm_wgs, cfg.frame_rows,
-                                          cfg.graph_max_superstep_us)
+                                          bool(cfg.frame_overlap), cfg.frame_comm_wgs, cfg.frame_rows,
+                                          cfg.graph_max_superstep_us, cfg.frame_overlap is None)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
@@ -341,10 +343,14 @@ class Stencil2D:
             return "fused-periodic (1x1 self-exchange in the kernel addressing)" + blk
         if self.solver.direct_halo():
             return "ipc direct (device-initiated push of each pass's edge bands into the neighbours' tiles)" + blk
+        choice = self.solver.frame_choice()[0]
         if tb > 1 and self.solver.frame_overlap(tb):
             return (f"{self.backend} + frame-first overlap (each pass stores its {tb}-deep output frame first; "
                     f"the next halo's pack -> RCCL send/recv -> unpack runs under the rest of the pass)" + blk)
-        return f"{self.backend}" + (" + overlap" if self.solver.overlapped() else "") + blk
+        mode = " + overlap" if self.solver.overlapped() else ""
+        if not mode and tb > 1 and self.backend == "rccl" and choice == "serial":
+            mode = " (pass, then halo exchange; prepare() measured the frame-first overlap slower)"
+        return f"{self.backend}" + mode + blk
 
     # ----------------------------------------------------------------- dump
     def dump_text(self, stage_arrays: list[tuple[str, torch.Tensor]], device_id: int | None = None,

@@ -206,3 +206,24 @@ def test_balanced_shares_bitwise(gpu, w, h, steps, wrap, dtype):
     finally:
         hip().set_pipe_balanced(old)
     assert torch.equal(outs[0], outs[1])
+
+
+def test_auto_schedule_choice_is_recorded_and_exact(gpu):
+    """Default (frame_overlap=None): prepare() times both schedules on the real
+    path (here RCCL loopback) and keeps the faster; either way the field is
+    bitwise the serial schedule's."""
+    kw = dict(global_width=16384, global_height=8192, dims="1x1", dtype="f32", backend="rccl", loopback=True,
+              seed=31)
+    auto = Stencil2D(StencilConfig(**kw))
+    assert auto.solver.frame_choice()[0] == ""
+    auto.run(20)
+    auto.prepare(20)
+    choice, serial_ms, frame_ms = auto.solver.frame_choice()
+    assert choice in ("serial", "frame") and serial_ms > 0 and frame_ms > 0
+    assert (choice == "frame") == (frame_ms < serial_ms) == auto.solver.frame_overlap(20)
+    auto.run(40)
+    auto.synchronize()
+    serial = Stencil2D(StencilConfig(frame_overlap=False, **kw))
+    serial.run(60)
+    serial.synchronize()
+    assert torch.equal(auto.core_view(), serial.core_view())
