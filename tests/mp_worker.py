@@ -85,14 +85,20 @@ def task_gpu_solver(args):
     cfg = StencilConfig(global_width=args["w"], global_height=args["h"], dims=args["dims"],
                         dtype=args.get("dtype", "f32"), seed=args.get("seed", 5), backend=args.get("backend", "auto"),
                         overlap=args.get("overlap", True), graph=args.get("graph", True),
-                        time_block=args.get("time_block", 12), direct_halo=args.get("direct", None))
+                        time_block=args.get("time_block", 12), direct_halo=args.get("direct", None),
+                        sum_form=args.get("sum_form", True), frame_overlap=args.get("frame_overlap", None))
     st = Stencil2D(cfg, ctx)
+    if args.get("prepare"):
+        st.prepare(args["prepare"])
     for n in args.get("runs", [args["iters"]]):
         st.run(n)
     st.synchronize()
     g = st.gather_global()
     out = {"rank": ctx.rank, "backend": st.backend, "halo": st.halo_mode(), "graph": st.graph_status(),
-           "native": st.solver is not None}
+           "native": st.solver is not None, "time_block": st.time_block}
+    if st.solver is not None:
+        out["choice"] = list(st.solver.frame_choice())
+        out["frame"] = bool(st.solver.frame_overlap(st.time_block))
     if ctx.rank == 0:
         out["grid"] = g.double().tolist()
     ctx.barrier()
