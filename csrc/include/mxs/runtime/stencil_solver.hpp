@@ -26,7 +26,8 @@
 // stream, then the exchange of its output (pack(nxt) -> RCCL -> unpack(nxt)):
 // post-exchange, so a pass never waits for the host to enqueue the RCCL group
 // (the first pass of a run is preceded by one exchange when cur's ghost ring
-// is not fresh: construction, field_changed(), a thin-strip overlap step).
+// is not fresh: construction, field_changed(), a thin-strip overlap step; with
+// peers, every call, so that all ranks issue the same collectives).
 //
 // Per super-step (cur -> nxt), with `overlap` on and S > 1:
 //
@@ -63,7 +64,8 @@
 //
 // so cur's ghost ring is fresh whenever a pass starts (the first pass of a run
 // is preceded by one exchange when it is not: construction, field_changed(), a
-// serial super-step). The pass is submitted before the counter wait, so even
+// thin-strip overlap step; with peers, the first pass of every call, so that
+// all ranks issue the same collectives). The pass is submitted before the counter wait, so even
 // streams that share a hardware queue cannot deadlock (the wait then just runs
 // after the pass). These super-steps are launched eagerly, not from a graph,
 // for the same reason: a graph's branches are dispatched in an order the host
@@ -262,6 +264,7 @@ class StencilSolver {
   PinnedBuffer<unsigned> frame_status_;
   std::uint64_t frame_timeout_ticks_ = 0;
   bool ghost_fresh_ = false;                 // cur_'s ghost ring holds the neighbours' current bands
+  bool multi_rank_ = false;                  // peers: every run call primes (begin_run)
   bool range_checked_ = false;
   bool user_sum_ = true;                     // the caller allows the sum form
   bool sum_coeffs_ok_ = false;               // 5|c| <= 1 and c^S normal

@@ -50,6 +50,7 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   HaloBootstrap boot;
   boot.rank = rank;
   boot.world_size = topo.size();
+  multi_rank_ = topo.size() > 1;
   boot.allgather = cfg_.bootstrap;
   boot.timeout_s = comm_timeout() > 0 ? comm_timeout() : 60.0;
   ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm, &boot);
@@ -387,6 +388,11 @@ void StencilSolver<T>::ensure_range() {
 
 template <typename T>
 void StencilSolver<T>::begin_run() {
+  // Whether a run starts with a priming exchange must be the same on every
+  // rank (it is a collective). field_changed() is per rank (a caller may read
+  // or write one rank's field alone), so with peers every call primes: one
+  // exchange per run() / prepare() / warm() call, not per super-step.
+  if (multi_rank_) ghost_fresh_ = false;
   ensure_range();
   prime();
 }

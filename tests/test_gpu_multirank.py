@@ -68,3 +68,17 @@ def test_ipc_direct_halo_bitwise_vs_classic_exchange(gpu):
     classic = run_ranks("gpu_solver", 4, dict(args, direct=False), gpu=True)
     assert direct[0]["halo"].startswith("ipc direct") and not classic[0]["halo"].startswith("ipc direct")
     assert torch.equal(torch.tensor(direct[0]["grid"]), torch.tensor(classic[0]["grid"]))
+
+
+def test_one_rank_reading_its_field_keeps_ranks_in_step(gpu):
+    """Reading a field marks it changed on that rank only; the priming exchange
+    of the next run must still be issued by every rank (it is collective), so
+    ranks whose callers differ stay matched (post-exchange schedule, 3 runs)."""
+    w, h, seed, runs = 264, 200, 9, [20, 20, 13]
+    res = run_ranks("gpu_solver", 2, {"w": w, "h": h, "dims": "1x2", "iters": sum(runs), "runs": runs, "seed": seed,
+                                      "time_block": 20, "overlap": False, "direct": False, "rank0_reads": True},
+                    gpu=True)
+    assert all(r["native"] and r["backend"] == "ipc" for r in res), res
+    got = torch.tensor(res[0]["grid"], dtype=torch.float64)
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), sum(runs)).double()
+    assert (got - ref).abs().max().item() < 1e-5
