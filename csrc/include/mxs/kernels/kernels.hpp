@@ -89,6 +89,10 @@ constexpr int kMaxTimeBlock = 16;
 // between them and handed over through LDS). Needs fp32, x0 and x1 multiples
 // of 4 (whole vectors); see stencil5_deep_supported().
 constexpr int kMaxTimeBlockDeep = 32;
+// Largest chunk (rows x pitch bytes) one workgroup of the streaming kernels
+// stores through a single buffer descriptor: below 2^31 with room for the
+// drop offsets of stencil_device.hpp (a sum of two never wraps).
+constexpr index_t kMaxChunkBytes = 0x7F000000;
 // Measured default S for a w x h tile of `elem_bytes`-byte cells
 // (profiles/stencil_tuning/tunes_*, profiles/r02_deep/pipe*_*, profiles/r02_f64,
 // profiles/r02_sum): fp32 takes the two-stage pipeline at S = 20 (sum form,
@@ -151,7 +155,7 @@ struct FramePassShape {
 };
 // False when `steps` has no frame-first form here (fp32 S = 20 / 24, fp64
 // S = 16 on whole lane vectors; other depths keep the serial schedule). The
-// caller still has to keep every chunk of its schedule under 2 GiB (rows x
+// caller still has to keep every chunk of its schedule within kMaxChunkBytes (rows x
 // pitch: the kernel's buffer-descriptor stores).
 template <typename T>
 bool frame_pass_shape(const TileGeom& g, int steps, const Stencil5Coeffs& c, FramePassShape* out);

@@ -524,6 +524,20 @@ __device__ __forceinline__ double lane_shift<double, kDppWaveShl1>(double v) {
 // rotated, once per row each.
 __device__ __forceinline__ f32x4 rot_in(const f32x4& n) { return __builtin_shufflevector(n, n, 1, 2, 3, 0); }
 __device__ __forceinline__ f32x4 rot_out(const f32x4& r) { return __builtin_shufflevector(r, r, 3, 0, 1, 2); }
+// rot_in as two v_pk_mov_b32 into fresh registers. From the shufflevector the
+// backend often keeps the rotated row as halves of the loaded registers (the
+// op_sel of later adds reads them in place), so the next load into that
+// prefetch slot needs other registers and the loop back edge copies them back:
+// ~21 v_mov per 6 rows of the fetching stage, plus 4 v_mov instead of 2
+// v_pk_mov for some rotations (ISA of the S = 20 pipeline). Copying here ends
+// the loaded registers' lifetime at the rotation.
+__device__ __forceinline__ f32x4 rot_in_copy(const f32x4& n) {
+  const f32x2 lo = n.xy, hi = n.zw;
+  f32x2 a, b;
+  asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,0]" : "=v"(a) : "v"(lo), "v"(hi));  // (c1, c2)
+  asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,0]" : "=v"(b) : "v"(hi), "v"(lo));  // (c3, c0)
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3);
+}
 
 __device__ __forceinline__ f32x4 jac_rot4f(const f32x4& up, const f32x4& mid, const f32x4& dn, float c0, float c1) {
   const f32x2 am = mid.xy, bm = mid.zw;  // (c1, c2), (c3, c0)
@@ -581,7 +595,7 @@ struct BodyRotF32 {  // rotated-pair fp32 (jac_rot4f)
   static constexpr int N = 4;
   static __device__ __forceinline__ V zero() { return f32x4(0.f); }
   static __device__ __forceinline__ V load(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
-  static __device__ __forceinline__ V enter(const V& v) { return rot_in(v); }
+  static __device__ __forceinline__ V enter(const V& v) { return rot_in_copy(v); }
   static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, float c0, float c1) {
     return jac_rot4f(u, m, d, c0, c1);
   }
@@ -1260,9 +1274,15 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
     } else {
       store_lane = lane >= AL && lane < kWaveSize - AL && gx < x_end && xw < x_end;
     }
-    const unsigned lane_off = unsigned(lane) * unsigned(N * sizeof(T));
+    // Store offset = lane term + row term, both past the range when dropped: a
+    // dropped lane adds 2^31, a dropped row 0x7F000000 (chunks are at most
+    // kMaxChunkBytes = 0x7F000000 bytes, so no sum wraps past 2^32 and every
+    // sum with a dropped term is >= the range). The row term is wave-uniform
+    // (scalar select), so a row costs one v_add_u32 (a 64-bit v_cmp and a
+    // v_cndmask per row before).
+    const unsigned lane_term = store_lane ? unsigned(lane) * unsigned(N * sizeof(T)) : 0x80000000u;
     const unsigned row_bytes = unsigned(pitch) * unsigned(sizeof(T));
-    constexpr unsigned kDrop = 0x80000000u;
+    const int rows_i = int(rows);
     V win[3][S1];
 #pragma unroll
     for (int q = 0; q < 3; ++q)
@@ -1327,10 +1347,9 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
             else win[p0][l + 1] = o;
           }
         }
-        const index_t r = j - E1;
-        const bool ok = store_lane && r >= 0 && r < rows;
-        const unsigned off = ok ? lane_off + unsigned(r) * row_bytes : kDrop;
-        B::store(top, orsrc, off, c0);
+        const int r = int(j - E1);
+        const unsigned row_term = r >= 0 && r < rows_i ? unsigned(r) * row_bytes : unsigned(kMaxChunkBytes);
+        B::store(top, orsrc, lane_term + row_term, c0);
       }
       __syncthreads();
     }
@@ -1340,8 +1359,8 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 // Balanced persistent launch of the two-stage pipeline: 512-thread workgroups
 // (4 strips x 2 stages), equal shares of (4-strip group) x rows as in
 // stencil5_stream_balanced_kernel. T = float: rotated-pair layout; T = double:
-// wide-lane body (FastBody<T>). Needs x_end % 4 == 0 and a chunk under 2 GiB
-// (the output buffer descriptor).
+// wide-lane body (FastBody<T>). Needs x_end % 4 == 0 and a chunk of at most
+// kMaxChunkBytes (the output buffer descriptor and its drop offsets).
 // PRIO (tuning): 1 raises the fetching stage's wave priority, 2 the storing stage's.
 // G: strips per workgroup (2G waves; the barriers of one block of rows span the
 // workgroup, so smaller groups decouple the strips of a CU).

@@ -147,8 +147,8 @@ void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_
     pipe_starts(groups, y1 - y0, blocks, pipe_fill_rows<S0, S - S0, pipe_pf<T, S>(), LAG1>(), &shares);
     for (int w = 0; w < shares.n; ++w) chunk = std::max<index_t>(chunk, std::min<index_t>(y1 - y0, shares.start[w + 1] - shares.start[w]));
   }
-  MXS_CHECK(chunk * g.pitch * index_t(sizeof(T)) < (index_t(1) << 31),
-            "stencil5_tb: a pipeline chunk must stay under 2 GiB (buffer-descriptor stores)");
+  MXS_CHECK(chunk * g.pitch * index_t(sizeof(T)) <= kMaxChunkBytes,
+            "stencil5_tb: a pipeline chunk must stay within kMaxChunkBytes (buffer-descriptor stores)");
   pipe_kernel<T, S, WRAP, SUM, JS0, LAG1>()<<<blocks, 2 * kBlock, 0, s>>>(
       in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, shares, SUM ? sc : c0, c1);
   note_dispatch(SUM ? "stream_pipe_sum" : "stream_pipe");
@@ -180,7 +180,7 @@ void launch_pipe_impl(const T* in, T* out, const TileGeom& g, index_t x0, index_
 
 // Whether the fp64 wide-lane pipeline can take [x0, x1) x [y0, y1) at depth S:
 // whole 4-cell lane vectors (x0, x1 and, wrapping, the width multiples of 4),
-// the apron inside the row padding, and a chunk under 2 GiB.
+// the apron inside the row padding, and a chunk of at most kMaxChunkBytes.
 template <typename T, int S, bool WRAP>
 bool wide_pipe_ok_impl(const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1) {
   constexpr int SA = StripShape<T, S, true>::SA;
@@ -188,8 +188,8 @@ bool wide_pipe_ok_impl(const TileGeom& g, index_t x0, index_t x1, index_t y0, in
   if (WRAP && g.width % 4 != 0) return false;
   const index_t lead = g.x_origin + g.halo_x;
   if (!WRAP && (lead < SA || g.pitch < lead + (g.width + 3) / 4 * 4 + SA)) return false;
-  return std::min(pipe_share<T, S, WRAP, false>(x0, x1, y0, y1), y1 - y0) * g.pitch * index_t(sizeof(T)) <
-         (index_t(1) << 31);
+  return std::min(pipe_share<T, S, WRAP, false>(x0, x1, y0, y1), y1 - y0) * g.pitch * index_t(sizeof(T)) <=
+         kMaxChunkBytes;
 }
 
 

@@ -441,8 +441,8 @@ typename StencilSolver<T>::FramePass* StencilSolver<T>::frame_pass(int S, bool b
   }
   index_t longest = 0;
   for (const auto& c : fp->sched.table) longest = std::max<index_t>(longest, c.r1 - c.r0);
-  if (longest * tile_.pitch * index_t(sizeof(T)) >= (index_t(1) << 31)) {
-    no_frame_.push_back(S);  // a chunk past the 2 GiB buffer-descriptor range
+  if (longest * tile_.pitch * index_t(sizeof(T)) > kernels::kMaxChunkBytes) {
+    no_frame_.push_back(S);  // a chunk past the buffer-descriptor range
     return nullptr;
   }
   fp->table.reset(index_t(fp->sched.table.size()));

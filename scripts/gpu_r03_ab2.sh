@@ -1,0 +1,19 @@
+#!/bin/bash
+# Longer interleaved A/B (see gpu_r03_ab.sh): 8192^2 fp32 and the 20-step 32768^2 window.
+set -uo pipefail
+OUT=gpurun_out/r03_ab2
+mkdir -p "$OUT"
+export PYTHONUNBUFFERED=1
+run() {  # tag, script, args...
+  local tag=$1 script=$2; shift 2
+  timeout -k 10 240 python "$script" --no-extras "$@" > "$OUT/tmp.txt" 2>&1 || { echo "bench $tag failed"; tail -5 "$OUT/tmp.txt"; exit 1; }
+  echo "$tag $* $(grep '^{' "$OUT/tmp.txt" | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"])')" | tee -a "$OUT/ab.txt"
+}
+for rep in 1 2 3 4 5 6; do
+  for side in new old; do
+    s=bench.py; [ "$side" = old ] && s=ab_old/bench.py
+    run "$side" "$s" --global 8192x8192 --steps 960 --warmup 48
+    run "$side" "$s" --steps 20 --warmup 5
+  done
+done
+echo done
