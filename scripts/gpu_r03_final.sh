@@ -14,5 +14,6 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smo
 tail -1 "$OUT/smoke.txt"
 timeout -k 10 400 python bench.py --steps 20 --warmup 5 > "$OUT/bench_driver.txt" 2>&1 || { echo bench failed; tail -30 "$OUT/bench_driver.txt"; exit 1; }
 tail -1 "$OUT/bench_driver.txt"
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 > "$GRAFT_REPO_ROOT/$OUT/prof.txt" 2>&1 || { echo prof failed; tail "$GRAFT_REPO_ROOT/$OUT/prof.txt"; exit 1; }
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 20 --warmup 5 > "$GRAFT_REPO_ROOT/$OUT/prof.txt" 2>&1 || { echo prof failed; tail "$GRAFT_REPO_ROOT/$OUT/prof.txt"; exit 1; }
+find "$GRAFT_REPO_ROOT/$OUT/prof" -name "*kernel_trace.csv" -size +20M -delete
 echo done
