@@ -144,7 +144,9 @@ struct SolverConfig {
   // Super-steps estimated longer than this (us, at ~9 T cell-steps/s) are
   // launched eagerly instead of from a hipGraph: on the 8-GPU tile (0.24 ms
   // passes) a 20-step RCCL-loopback window took 0.276 ms eager vs 0.285 from
-  // the graph, 240 steps 3.23 vs 3.34 ms (profiles/r03_window5). 0 = always graphs.
+  // the graph, 240 steps 3.23 vs 3.34 ms (profiles/r03_window5). A fused
+  // periodic super-step (one launch) goes eager past a fifth of this: 8192^2
+  // (~130 us passes) 9.79 -> 10.0 T cells/s (profiles/r03_eager). 0 = always graphs.
   double graph_max_superstep_us = 150.0;
 };
 

@@ -283,9 +283,12 @@ bool StencilSolver<T>::capture(GraphSet& gs) {
 template <typename T>
 typename StencilSolver<T>::GraphSet* StencilSolver<T>::graphs_for(int S, int count) {
   if (!cfg_.use_graph) return nullptr;
-  // Long super-steps: eager launches beat the graph's replay (header).
+  // Long super-steps: eager launches beat the graph's replay (header). A fused
+  // periodic super-step is one launch, so the host stays ahead of the GPU
+  // from far shorter super-steps on (limit / 5).
   const double est_us = double(tile_.width) * double(tile_.height) * S / 9e6;
-  if (cfg_.graph_max_superstep_us > 0 && est_us > cfg_.graph_max_superstep_us) {
+  const double limit = fused_ ? cfg_.graph_max_superstep_us / 5.0 : cfg_.graph_max_superstep_us;
+  if (cfg_.graph_max_superstep_us > 0 && est_us > limit) {
     graph_status_ = "eager (super-steps of ~" + std::to_string(int(est_us)) + " us)";
     return nullptr;
   }

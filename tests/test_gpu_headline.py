@@ -153,7 +153,8 @@ def test_solver_blocked_run_bitwise_equals_single_steps(gpu, dtype, block):
     single = Stencil2D(StencilConfig(time_block=1, **kw))
     single.run(20)
     single.synchronize()
-    assert blocked.graph_status() == "captured"
+    # Fused periodic super-steps of this size launch eagerly (graph_max_superstep_us / 5).
+    assert blocked.graph_status().startswith("eager")
     assert torch.equal(blocked.core_view(), single.core_view())
 
 
