@@ -90,6 +90,8 @@ def task_gpu_solver(args):
     st = Stencil2D(cfg, ctx)
     if args.get("prepare"):
         st.prepare(args["prepare"])
+    if args.get("warm"):
+        assert st.warm(args["warm"], 0.01) >= 1  # untimed, state-preserving passes (collective)
     for n in args.get("runs", [args["iters"]]):
         if args.get("rank0_reads") and ctx.rank == 0:
             st.synchronize()

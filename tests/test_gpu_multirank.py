@@ -82,3 +82,18 @@ def test_one_rank_reading_its_field_keeps_ranks_in_step(gpu):
     got = torch.tensor(res[0]["grid"], dtype=torch.float64)
     ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), sum(runs)).double()
     assert (got - ref).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("direct", [True, False])
+def test_ipc_warm_and_prepare_leave_the_state_alone(gpu, direct):
+    """bench.py's prepare() + warm() on the IPC paths (device-initiated pushes and
+    the classic pack -> put -> unpack) launch real passes and exchanges but must
+    not advance the field: the result equals the plain run's reference."""
+    w, h, seed, runs = 272, 216, 19, [20, 20]
+    res = run_ranks("gpu_solver", 2, {"w": w, "h": h, "dims": "1x2", "iters": sum(runs), "runs": runs, "seed": seed,
+                                      "time_block": 20, "overlap": False, "direct": direct, "prepare": 20, "warm": 20},
+                    gpu=True)
+    assert all(r["backend"] == "ipc" and r["halo"].startswith("ipc direct") == direct for r in res), res
+    got = torch.tensor(res[0]["grid"], dtype=torch.float64)
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), sum(runs)).double()
+    assert (got - ref).abs().max().item() < 1e-5
