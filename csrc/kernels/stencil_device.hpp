@@ -571,6 +571,19 @@ struct StreamShape {
 // Same per-cell operations and order as jac(): bitwise identical.
 using f64x2 = double __attribute__((ext_vector_type(2)));
 using f64x4 = double __attribute__((ext_vector_type(4)));
+// The loaded row into fresh registers (4 v_mov_b64): as rot_in_copy for fp32,
+// this ends the prefetch registers' lifetime at entry, so the next load can
+// reuse them instead of the loop back edge copying rows around.
+__device__ __forceinline__ f64x4 copy_w4d(const f64x4& v) {
+  f64x4 r;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    double x;
+    asm("v_mov_b64 %0, %1" : "=v"(x) : "v"(v[i]));
+    r[i] = x;
+  }
+  return r;
+}
 __device__ __forceinline__ f64x4 jac_w4d(const f64x4& up, const f64x4& mid, const f64x4& dn, double c0, double c1) {
   const double left = lane_shift<double, kDppWaveShr1>(mid.w);   // lane - 1's last cell
   const double right = lane_shift<double, kDppWaveShl1>(mid.x);  // lane + 1's first cell
@@ -613,7 +626,7 @@ struct BodyWideF64 {  // 4 consecutive fp64 cells per lane (jac_w4d)
     const f64x2 a = *reinterpret_cast<const f64x2*>(p), b = *reinterpret_cast<const f64x2*>(p + 2);
     return __builtin_shufflevector(a, b, 0, 1, 2, 3);
   }
-  static __device__ __forceinline__ V enter(const V& v) { return v; }
+  static __device__ __forceinline__ V enter(const V& v) { return copy_w4d(v); }
   static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, double c0, double c1) {
     return jac_w4d(u, m, d, c0, c1);
   }
