@@ -128,8 +128,11 @@ int run(MpiEnv& env, const Cli& cli, index_t n_global) {
     os << env.processor_name() << " - rank: " << rank << " partial dot: " << partial << '\n';
     std::cout << os.str() << std::flush;
   }
+  env.barrier();  // the partial lines go out before the result (mpiexec still may interleave them)
   if (rank == 0) {
-    std::cout << "dot product result: " << result << '\n' << "time: " << best << 's' << std::endl;
+    std::ostringstream res;  // one write: the result line cannot be split by another rank's output
+    res << "dot product result: " << result << '\n' << "time: " << best << "s\n";
+    std::cout << res.str() << std::flush;
     std::ostringstream js;
     js << "{\"app\": \"dot\", \"n\": " << n_global << ", \"dtype\": \"" << (sizeof(T) == 4 ? "f32" : "f64")
        << "\", \"reduce\": \"" << cli.get("reduce", "single-pass") << "\", \"ranks\": " << size

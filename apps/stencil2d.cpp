@@ -242,6 +242,10 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
          << "\", \"dtype\": \"" << (sizeof(T) == 4 ? "f32" : "f64") << "\", \"backend\": \"" << backend
          << "\", \"graph\": \"" << (solver ? solver->graph_status() : std::string("n/a"))
          << "\", \"time_block\": " << time_block << ", \"iters\": " << iters;
+      if (solver) {
+        js << ", \"frame_first\": " << (solver->frame_overlap(solver->time_block()) ? "true" : "false");
+        if (!solver->frame_choice().empty()) js << ", \"schedule_choice\": \"" << solver->frame_choice() << "\"";
+      }
       if (want_sum) js << ", \"checksum\": " << app::fmt(checksum);
       js << app::meta_json(device_description(dev.device)) << "}";
       std::cout << "Gcells/s: " << app::fmt(gcells) << '\n';
@@ -261,7 +265,8 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
 int main(int argc, char** argv) {
   MpiEnv env(&argc, &argv);
   Cli cli(argc, argv, {"dump", "no-dump", "non-periodic", "strict-square", "no-overlap", "overlap", "no-graph",
-                       "loopback", "pageable", "checksum"});
+                       "loopback", "pageable", "checksum", "frame-overlap", "no-frame-overlap", "no-sum-form",
+                       "no-direct-halo"});
   comm_timeout() = cli.get_double("comm-timeout", 300.0);
   const DeviceBinding dev = bind_device(env, cli.get("bind", "bunch"));
   const int n = env.size();

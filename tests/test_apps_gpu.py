@@ -117,7 +117,9 @@ def test_pingpong_loopback_rccl(gpu):
 def test_dot_app_exact(gpu, reduce):
     r = mpirun(4, "dot", "--n", str(1 << 24), "--dtype", "f64", "--reduce", reduce, "--reps", "2")
     assert r.returncode == 0, r.stderr
+    # Ranks' lines are forwarded by mpiexec and may interleave: check the line and the JSON record.
     assert "dot product result: 1.67772e+07" in r.stdout
+    assert '"result": 1.67772e+07' in r.stdout
 
 
 def test_dot_atomics(gpu):
@@ -168,3 +170,28 @@ def test_pingpong_ipc_reference_output(gpu):
     r = mpirun(2, "pingpong", "--transport", "ipc", "131072")
     assert r.returncode == 0, r.stderr[-3000:]
     assert r.stdout.startswith("PASSED\nMessage size(MB): 1\nRound-trip time(ms): ")
+
+
+@pytest.mark.parametrize("mode", ["--frame-overlap", "--no-frame-overlap", None])
+def test_stencil_gpu_schedules_at_production_depth(gpu, tmp_path, mode):
+    """The app's multi-GPU schedules through RCCL loopback at S = 20 (per-step
+    form): frame-first, serial and the measured choice give the same checksum,
+    bit for bit, and agree with the CPU app."""
+    args = ["--global", "4096x2048", "--dims", "1x1", "--dtype", "f32", "--iters", "40", "--stencil", "3"]
+    extra = ["--loopback", "--time-block", "20", "--no-sum-form", "--no-overlap"] + ([mode] if mode else [])
+    g = mpirun(1, "stencil2d", *args, "--checksum", "--warmup", "0", *extra, cwd=tmp_path)
+    assert g.returncode == 0, g.stderr[-3000:]
+    js = g.stdout.strip().splitlines()[-1]
+    assert '"time_block": 20' in js
+    if mode == "--frame-overlap":
+        assert '"frame_first": true' in js
+    elif mode == "--no-frame-overlap":
+        assert '"frame_first": false' in js
+    else:
+        assert '"schedule_choice": "' in js
+    ref = mpirun(1, "stencil2d", *args, "--checksum", "--warmup", "0", "--time-block", "1", cwd=tmp_path)
+    assert ref.returncode == 0, ref.stderr[-3000:]
+    assert _checksum(g.stdout) == _checksum(ref.stdout)
+    c = mpirun(1, "stencil2d_cpu", *args, cwd=tmp_path, timeout=600)
+    assert c.returncode == 0, c.stderr[-3000:]
+    assert abs(_checksum(g.stdout) - _checksum(c.stdout)) <= 1e-6 * abs(_checksum(c.stdout))
