@@ -5,6 +5,8 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <chrono>
+
 #include <string>
 #include <utility>
 
@@ -87,6 +89,20 @@ class Stream {
   Stream& operator=(const Stream&) = delete;
   hipStream_t get() const { return s_; }
   void sync() const { MXS_HIP_CHECK(hipStreamSynchronize(s_)); }
+  // Poll for up to `spin_s` seconds, then block. A blocking wait sleeps the
+  // host thread: on one GPU it noticed the end of a 2 ms pass ~80 us late and
+  // the next launch from the cold core took 40-90 us instead of ~10
+  // (profiles/r03_window).
+  void spin_sync(double spin_s = 0.02) const {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      const hipError_t q = hipStreamQuery(s_);
+      if (q == hipSuccess) return;
+      if (q != hipErrorNotReady) MXS_HIP_CHECK(q);
+      if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > spin_s) break;
+    }
+    sync();
+  }
 
  private:
   hipStream_t s_ = nullptr;

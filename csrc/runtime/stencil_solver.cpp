@@ -584,8 +584,8 @@ void StencilSolver<T>::synchronize() {
   // Direct halo: also wait for the neighbours' pushes into our tiles, so the
   // field (ghost ring included) is final and no peer still writes into it.
   if (direct_) direct_->wait(main_.get());
-  main_.sync();
-  side_.sync();
+  main_.spin_sync();
+  side_.spin_sync();
   ex_->check();  // IPC backend: device-side waits carry their own deadline
   if (direct_) direct_->check();
   if (frame_status_.get()) {
