@@ -27,7 +27,11 @@
 // post-exchange, so a pass never waits for the host to enqueue the RCCL group
 // (the first pass of a run is preceded by one exchange when cur's ghost ring
 // is not fresh: construction, field_changed(), a thin-strip overlap step; with
-// peers, every call, so that all ranks issue the same collectives).
+// peers, every call, so that all ranks issue the same collectives). With
+// peers the LAST super-step of a call is a bare pass: its exchange would only
+// feed the next call, which primes anyway, so a call of n super-steps issues
+// exactly n exchanges (the reference's exchange-then-compute count) instead
+// of n + 1 — a 20-step window at N = 8 is one exchange + one pass.
 //
 // Per super-step (cur -> nxt), with `overlap` on and S > 1:
 //
@@ -207,6 +211,8 @@ class StencilSolver {
   const std::string& sum_form_note() const { return sum_note_; }
   // (S, count) of the super-steps the last run() enqueued.
   std::vector<std::pair<int, int>> last_run_blocks() const { return last_blocks_; }
+  // Halo exchanges the last run() enqueued (priming included).
+  int last_run_exchanges() const { return last_exchanges_; }
   // Frame schedule of depth S (building it if needed); nullptr: serial.
   const kernels::FrameSchedule* frame_schedule(int S);
   int time_block() const { return block_; }
@@ -235,7 +241,10 @@ class StencilSolver {
     int S, count;
   };
   void split(int iters, Group out[2]) const;
-  void run_group(int S, int count);
+  // `count` super-steps of size S; `last_bare`: the last one is a pass without
+  // its trailing exchange (with peers, the next call primes anyway).
+  void run_group(int S, int count, bool last_bare = false);
+  void enqueue_bare_pass(T* cur, T* nxt, int S);  // post-exchange pass, no exchange after it
 
   // Frame-first pass of depth S: shape + schedule + device table.
   struct FramePass {
@@ -266,7 +275,9 @@ class StencilSolver {
   PinnedBuffer<unsigned> frame_status_;
   std::uint64_t frame_timeout_ticks_ = 0;
   bool ghost_fresh_ = false;                 // cur_'s ghost ring holds the neighbours' current bands
+  int last_exchanges_ = 0;
   bool multi_rank_ = false;                  // peers: every run call primes (begin_run)
+  bool bare_tail_ = true;                    // with peers a call ends on a bare pass
   bool range_checked_ = false;
   bool user_sum_ = true;                     // the caller allows the sum form
   bool sum_coeffs_ok_ = false;               // 5|c| <= 1 and c^S normal

@@ -453,6 +453,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def("sum_form_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.sum_form_note(); }); })
       .def("last_run_blocks", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_blocks(); }); },
            "(S, count) super-steps the last run() enqueued")
+      .def("last_run_exchanges", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_exchanges(); }); },
+           "halo exchanges the last run() enqueued (priming included)")
       .def(
           "frame_schedule",
           [](SolverHandle& h, int S) -> py::object {

@@ -50,7 +50,14 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   HaloBootstrap boot;
   boot.rank = rank;
   boot.world_size = topo.size();
-  multi_rank_ = topo.size() > 1;
+  // MXS_PEER_SCHEDULE (measurement): 1 = a 1-rank RCCL-loopback solver follows
+  // the peers' schedule (prime every call, bare last pass), so one GPU can
+  // time the window shape an 8-GPU run executes; 2 = the same without the bare
+  // last pass (the round-3 schedule: n + 1 exchanges per call of n super-steps).
+  const char* peer_env = std::getenv("MXS_PEER_SCHEDULE");
+  const int peer_mode = cfg_.loopback_self && peer_env ? std::atoi(peer_env) : 0;
+  multi_rank_ = topo.size() > 1 || peer_mode == 1 || peer_mode == 2;
+  bare_tail_ = peer_mode != 2;
   boot.allgather = cfg_.bootstrap;
   boot.timeout_s = comm_timeout() > 0 ? comm_timeout() : 60.0;
   ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm, &boot);
@@ -323,35 +330,59 @@ void StencilSolver<T>::split(int iters, Group out[2]) const {
 }
 
 template <typename T>
-void StencilSolver<T>::run_group(int S, int count) {
+void StencilSolver<T>::run_group(int S, int count, bool last_bare) {
   if (count <= 0) return;
   last_blocks_.emplace_back(S, count);
   // Post-exchange super-steps (frame-first and serial): cur's ghost ring must
   // be fresh before the first one; each leaves the next one's fresh. The
   // thin-strip overlap schedule exchanges first and leaves it stale.
-  if (post_exchange() && !ghost_fresh_) ex_->exchange(cur_, main_.get());
+  if (post_exchange() && !ghost_fresh_) {
+    ex_->exchange(cur_, main_.get());
+    ++last_exchanges_;
+  }
+  last_bare = last_bare && post_exchange();
+  const int full = last_bare ? count - 1 : count;  // super-steps with their exchange
+  // Exchanges of the super-steps themselves (graph replays included): one each,
+  // the bare tail none; the fused periodic self-exchange is no exchange at all.
+  if (!fused_) last_exchanges_ += post_exchange() ? full : count;
+  auto bare_tail = [&] {
+    if (!last_bare) return;
+    enqueue_bare_pass(cur_, nxt_, S);
+    std::swap(cur_, nxt_);
+  };
   if (frame_pass(S, true)) {  // eager launches (header)
-    for (int i = 0; i < count; ++i) {
+    for (int i = 0; i < full; ++i) {
       enqueue_block(cur_, nxt_, S);
       std::swap(cur_, nxt_);
     }
     join_side();
-    ghost_fresh_ = true;
+    bare_tail();
+    ghost_fresh_ = !last_bare;
     return;
   }
-  ghost_fresh_ = post_exchange();
   int i = 0;
-  if (GraphSet* gs = graphs_for(S, count)) {
-    for (; i + gs->chain <= count; i += gs->chain) {
+  if (GraphSet* gs = full > 0 ? graphs_for(S, full) : nullptr) {
+    for (; i + gs->chain <= full; i += gs->chain) {
       MXS_TRACE_RANGE("stencil.graph_launch");
       gs->g[cur_ == buf_a_ ? 0 : 1].launch(main_.get());
       if (gs->chain % 2) std::swap(cur_, nxt_);  // an odd chain ends on the other buffer
     }
   }
-  for (; i < count; ++i) {  // no graph, or fewer than `chain` super-steps left
+  for (; i < full; ++i) {  // no graph, or fewer than `chain` super-steps left
     enqueue_block(cur_, nxt_, S);
     std::swap(cur_, nxt_);
   }
+  bare_tail();
+  ghost_fresh_ = post_exchange() && !last_bare;
+}
+
+// The last super-step of a call with peers: the pass alone, on the main stream
+// (after join_side() when the frame-first schedule ran before it). Its output's
+// ghost ring stays stale; the next call's priming exchange refreshes it.
+template <typename T>
+void StencilSolver<T>::enqueue_bare_pass(T* cur, T* nxt, int S) {
+  MXS_TRACE_RANGE("stencil.superstep_bare");
+  update(cur, nxt, S, 0, tile_.width, 0, tile_.height, main_.get());
 }
 
 // Direct halo: every pass pushes its output bands, so the current tile's ghost
@@ -404,11 +435,15 @@ template <typename T>
 void StencilSolver<T>::run(int iters) {
   MXS_TRACE_RANGE("stencil.run");
   last_blocks_.clear();
+  last_exchanges_ = 0;
   if (iters <= 0) return;
   begin_run();
   Group gr[2];
   split(iters, gr);
-  for (const Group& g : gr) run_group(g.S, g.count);
+  // With peers every call primes (begin_run), so the exchange after the call's
+  // last pass would be redundant: it ends on a bare pass (header).
+  const int last = gr[1].count > 0 ? 1 : 0;
+  for (int k = 0; k < 2; ++k) run_group(gr[k].S, gr[k].count, multi_rank_ && bare_tail_ && k == last);
 }
 
 template <typename T>
@@ -539,6 +574,12 @@ void StencilSolver<T>::prepare(int iters) {
     // without swapping (nxt is scratch; the exchange rewrites cur's ghost ring
     // with the same values a real super-step would).
     enqueue_block(cur_, nxt_, g.S);
+    // With peers a call ends on a bare pass (run_group): after a frame-first
+    // super-step that is the other kernel.
+    if (multi_rank_ && post_exchange() && frame_pass(g.S, false)) {
+      join_side();
+      enqueue_bare_pass(cur_, nxt_, g.S);
+    }
     warmed_.push_back(g.S);
   }
   join_side();

@@ -92,11 +92,14 @@ def task_gpu_solver(args):
         st.prepare(args["prepare"])
     if args.get("warm"):
         assert st.warm(args["warm"], 0.01) >= 1  # untimed, state-preserving passes (collective)
+    per_run = []
     for n in args.get("runs", [args["iters"]]):
         if args.get("rank0_reads") and ctx.rank == 0:
             st.synchronize()
             float(st.core_view()[0, 0])  # one rank alone touches its field between runs
         st.run(n)
+        if st.solver is not None:
+            per_run.append([int(st.solver.last_run_exchanges()), sum(c for _, c in st.solver.last_run_blocks())])
     st.synchronize()
     g = st.gather_global()
     out = {"rank": ctx.rank, "backend": st.backend, "halo": st.halo_mode(), "graph": st.graph_status(),
@@ -104,6 +107,7 @@ def task_gpu_solver(args):
     if st.solver is not None:
         out["choice"] = list(st.solver.frame_choice())
         out["frame"] = bool(st.solver.frame_overlap(st.time_block))
+        out["exchanges"] = per_run  # halo exchanges each run() enqueued, and its super-steps
     if ctx.rank == 0:
         out["grid"] = g.double().tolist()
     ctx.barrier()

@@ -84,6 +84,24 @@ def test_one_rank_reading_its_field_keeps_ranks_in_step(gpu):
     assert (got - ref).abs().max().item() < 1e-5
 
 
+@pytest.mark.parametrize("time_block", [20, 1])
+def test_peers_exchange_once_per_super_step(gpu, time_block):
+    """With peers a run of n super-steps issues exactly n exchanges: the priming
+    one, then one after every pass but the last (the next run primes anyway).
+    The 20-step window bench.py times at N = 8 is one exchange + one pass."""
+    w, h, seed = 264, 200, 13
+    runs = [45, 20, 7] if time_block > 1 else [3, 1, 2]
+    res = run_ranks("gpu_solver", 2, {"w": w, "h": h, "dims": "1x2", "iters": sum(runs), "runs": runs, "seed": seed,
+                                      "time_block": time_block, "overlap": False, "direct": False}, gpu=True)
+    for r in res:
+        assert r["native"] and r["backend"] == "ipc", r
+        assert all(ex == steps for ex, steps in r["exchanges"]), r["exchanges"]
+    assert [s for _, s in res[0]["exchanges"]] == [-(-n // time_block) for n in runs]
+    got = torch.tensor(res[0]["grid"], dtype=torch.float64)
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), sum(runs)).double()
+    assert (got - ref).abs().max().item() < 1e-5
+
+
 @pytest.mark.parametrize("direct", [True, False])
 def test_ipc_warm_and_prepare_leave_the_state_alone(gpu, direct):
     """bench.py's prepare() + warm() on the IPC paths (device-initiated pushes and
