@@ -196,19 +196,20 @@ Variant balanced(const float* in, float* out, const TileGeom& g, int per_cu, flo
 
 // Two-stage wave pipeline (S = S0 + S1 levels; 512-thread workgroups).
 template <int S0, int S1, int PF, bool WRAP = true, int PRIO = 0, bool SUM = false, int G = 4, bool XM = false,
-          bool JOINT = false, int LAG1 = 0>
+          bool JOINT = false, int LAG1 = 0, int XB = 0>
 Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullptr) {
   int per_cu = 0, cus = 0;
   constexpr int threads = 2 * G * kWaveSize;
   MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu, reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM, JOINT, LAG1>),
+      &per_cu, reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM, JOINT, LAG1, XB>),
       threads, 0));
   MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const int blocks = std::max(1, per_cu * cus);
   char buf[128];
-  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s%s%s%s%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
+  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s%s%s%s%s%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
                 PRIO == 1 ? "_prio0" : (PRIO == 2 ? "_prio1" : ""), SUM ? "_sum" : "",
-                G == 4 ? "" : (G == 2 ? "_g2" : "_g1"), XM ? "_xcd" : "", JOINT ? "_joint" : "", LAG1 == 3 ? "_lag1" : (LAG1 == 2 ? "_lag1s1" : (LAG1 == 1 ? "_lag1s0" : "")));
+                G == 4 ? "" : (G == 2 ? "_g2" : "_g1"), XM ? "_xcd" : "", JOINT ? "_joint" : "", LAG1 == 3 ? "_lag1" : (LAG1 == 2 ? "_lag1s1" : (LAG1 == 1 ? "_lag1s0" : "")),
+                XB == 1 ? "_perm" : "");
   const float c0 = SUM ? float(std::pow(0.2, S0 + S1)) : 0.2f;  // sum form: c0 carries c^S
   auto mk = [=](const float* I, float* O) {
     return [=](hipStream_t s) {
@@ -221,7 +222,7 @@ Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullpt
       PipeShares shares = PipeShares::equal(share);
       if (!XM && G == kWavesPerBlock && pipe_balanced() && blocks <= kMaxShareBlocks)
         pipe_starts(groups, g.height, blocks, pipe_fill_rows<S0, S1, PF, LAG1>(), &shares);
-      stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM, JOINT, LAG1><<<blocks, threads, 0, s>>>(
+      stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, PRIO, float, SUM, G, XM, JOINT, LAG1, XB><<<blocks, threads, 0, s>>>(
           I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, shares, c0, 0.2f);
     };
   };
@@ -463,6 +464,23 @@ int main(int argc, char** argv) {
     vs.push_back(n20);
     vs.push_back(joint_vs(pipe<8, 12, 6, false, 0, true, 4, false, true>(in, out, g), n20));
     vs.push_back(joint_vs(pipe<12, 12, 6, false, 0, true, 4, false, true>(in, out, g), n24));
+  } else if (focus && std::string(focus) == "perm") {  // lane-crossing sums via ds_bpermute (LDS pipe) vs DPP
+    // The production joint forms (32768^2: 12 + 8 top-down; 8192^2: 8 + 12
+    // bottom-up; S = 24), each bpermute variant checked BITWISE against its DPP twin.
+    auto twin = [&](Variant j, const Variant& plain) {
+      j.ref = plain.launch;
+      j.tol = 0.f;
+      return j;
+    };
+    const Variant a = pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g, tmp);
+    const Variant b = pipe<8, 12, 6, true, 0, true, 4, false, true, 3>(in, out, g, tmp);
+    const Variant c = pipe<12, 12, 6, true, 0, true, 4, false, true>(in, out, g, tmp);
+    vs.push_back(a);
+    vs.push_back(twin(pipe<12, 8, 6, true, 0, true, 4, false, true, 0, 1>(in, out, g), a));
+    vs.push_back(b);
+    vs.push_back(twin(pipe<8, 12, 6, true, 0, true, 4, false, true, 3, 1>(in, out, g), b));
+    vs.push_back(c);
+    vs.push_back(twin(pipe<12, 12, 6, true, 0, true, 4, false, true, 0, 1>(in, out, g), c));
   } else if (focus && std::string(focus) == "joint2") {  // joint windows: fetch depth, XCD-major order, priority
     vs.push_back(pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g));
     vs.push_back(pipe<12, 8, 3, true, 0, true, 4, false, true>(in, out, g));

@@ -58,10 +58,10 @@ std::function<void(const double*, double*, hipStream_t)> balanced_fn(const TileG
   };
 }
 
-template <int S0, int S1, int PF, bool WRAP, bool SUM = false, bool JOINT = false, int LAG1 = 0>
+template <int S0, int S1, int PF, bool WRAP, bool SUM = false, bool JOINT = false, int LAG1 = 0, int XB = 0>
 std::function<void(const double*, double*, hipStream_t)> pipe_fn(const TileGeom& g, int* per_cu = nullptr) {
   const int blocks = resident(
-      reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, 0, double, SUM, 4, false, JOINT, LAG1>),
+      reinterpret_cast<const void*>(stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, 0, double, SUM, 4, false, JOINT, LAG1, XB>),
       512);
   if (per_cu) *per_cu = blocks / 256;
   const double c0 = SUM ? std::pow(0.2, S0 + S1) : 0.2;  // sum form: c0 carries c^S
@@ -73,7 +73,7 @@ std::function<void(const double*, double*, hipStream_t)> pipe_fn(const TileGeom&
     PipeShares shares = PipeShares::equal(share);
     if (pipe_balanced() && blocks <= kMaxShareBlocks)
       pipe_starts(groups, g.height, blocks, pipe_fill_rows<S0, S1, PF, LAG1>(), &shares);
-    stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, 0, double, SUM, 4, false, JOINT, LAG1><<<blocks, 512, 0, s>>>(
+    stencil5_stream_pipe_kernel<S0, S1, PF, WRAP, 0, double, SUM, 4, false, JOINT, LAG1, XB><<<blocks, 512, 0, s>>>(
         I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, shares, c0, 0.2);
   };
 }
@@ -106,14 +106,15 @@ Variant balanced(const TileGeom& g, double* tmp) {
   return v;
 }
 
-template <int S0, int S1, int PF, bool WRAP, bool SUM = false, bool JOINT = false, int LAG1 = 0>
+template <int S0, int S1, int PF, bool WRAP, bool SUM = false, bool JOINT = false, int LAG1 = 0, int XB = 0>
 Variant pipe(const TileGeom& g, double* tmp) {
   int per_cu = 0;
   Variant v;
-  v.launch = pipe_fn<S0, S1, PF, WRAP, SUM, JOINT, LAG1>(g, &per_cu);
+  v.launch = pipe_fn<S0, S1, PF, WRAP, SUM, JOINT, LAG1, XB>(g, &per_cu);
   char buf[128];
-  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
-                SUM ? "_sum" : "", JOINT ? "_joint" : "", LAG1 == 3 ? "_lag1" : (LAG1 == 2 ? "_lag1s1" : (LAG1 == 1 ? "_lag1s0" : "")));
+  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s%s%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
+                SUM ? "_sum" : "", JOINT ? "_joint" : "", LAG1 == 3 ? "_lag1" : (LAG1 == 2 ? "_lag1s1" : (LAG1 == 1 ? "_lag1s0" : "")),
+                XB == 1 ? "_perm" : "");
   v.name = buf;
   v.steps = S0 + S1;
   v.ref = ref_fn<S0 + S1, WRAP>(g, tmp);
@@ -182,6 +183,20 @@ int main(int argc, char** argv) {
     b.tol = 0.0;
     Variant c = pipe<6, 6, 3, true, false, false>(g, tmp);
     Variant d = pipe<6, 6, 3, true, false, false, 3>(g, tmp);
+    d.ref = c.launch;
+    d.tol = 0.0;
+    vs.push_back(a);
+    vs.push_back(b);
+    vs.push_back(c);
+    vs.push_back(d);
+  }
+  if (f == "perm") {  // lane-crossing neighbours via ds_bpermute (LDS pipe) vs DPP moves, bitwise twins
+    Variant a = pipe<8, 8, 3, true, true, true, 3>(g, tmp);
+    Variant b = pipe<8, 8, 3, true, true, true, 3, 1>(g, tmp);
+    b.ref = a.launch;
+    b.tol = 0.0;
+    Variant c = pipe<8, 8, 3, true, true, true>(g, tmp);
+    Variant d = pipe<8, 8, 3, true, true, true, 0, 1>(g, tmp);
     d.ref = c.launch;
     d.tol = 0.0;
     vs.push_back(a);

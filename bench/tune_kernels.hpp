@@ -3,7 +3,7 @@
 // not compile them: the LDS ping-pong temporal-block tile (stencil5_tb_kernel;
 // production runs the single-buffer tile stencil5_tb1_kernel) and the
 // three-stage wave pipeline (stencil5_stream_pipe3_kernel: measured 3-5% behind
-// the two-stage pipeline, docs/PERF.md).
+// the two-stage pipeline, docs/PERF.md), and the LDS-crossbar bodies (XB = 1).
 #pragma once
 
 #include "../csrc/kernels/stencil_pipe.hpp"
@@ -373,6 +373,72 @@ __global__ __launch_bounds__(3 * kBlock) void stencil5_stream_pipe3_kernel(
     a += r1 - r0;
   }
 }
+
+// ------------------------------------------------ LDS-crossbar neighbours
+// Lane-crossing operands through the LDS crossbar (XB = 1; measured 35-40%
+// SLOWER than the DPP forms, profiles/r03_perm). The DPP
+// forms spend VALU issue slots on every lane-crossing value: fp32 sum form 2
+// scalar v_add_f32_dpp of its 8 slots per level-row (the packed add cannot take
+// a DPP source), fp64 4 v_mov_b32_dpp of 18. ds_bpermute_b32 moves the same
+// values on the LDS pipe, so the fp32 sum body becomes 7 packed adds (the two
+// neighbours land in one pair) and the fp64 sum body 14 adds. Lanes 0 / 63 read
+// the other end of the wave instead of DPP's zero fill: apron lanes, never
+// stored. Same operands per stored cell: bitwise identical.
+__device__ __forceinline__ int lane_addr(int d) { return ((int(__lane_id()) + d) & (kWaveSize - 1)) << 2; }
+__device__ __forceinline__ float perm_f(int addr, float v) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
+}
+__device__ __forceinline__ double perm_d(int addr, double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_bpermute(addr, int(b & 0xffffffff));
+  const int hi = __builtin_amdgcn_ds_bpermute(addr, int(b >> 32));
+  return __longlong_as_double((static_cast<long long>(hi) << 32) | static_cast<unsigned int>(lo));
+}
+__device__ __forceinline__ f32x4 sum_rot4f_perm(const f32x4& up, const f32x4& mid, const f32x4& dn) {
+  const f32x2 am = mid.xy, bm = mid.zw;  // (c1, c2), (c3, c0)
+  const f32x2 ns_a = up.xy + dn.xy, ns_b = up.zw + dn.zw;
+  const f32x2 p = pk_add_swap(am, bm);   // (c1 + c0, c2 + c3)
+  const f32x2 h_a = pk_add_swap(p, am);  // h3(c1), h3(c2)
+  f32x2 nb;
+  nb.x = perm_f(lane_addr(1), bm.y);      // c4 = lane + 1's c0
+  nb.y = perm_f(lane_addr(-1), bm.x);     // c[-1] = lane - 1's c3
+  const f32x2 h_b = pk_add_swap(nb, p);  // (c4 + p23, c[-1] + p01) = h3(c3), h3(c0)
+  f32x4 o;
+  o.xy = ns_a + h_a;
+  o.zw = ns_b + h_b;
+  return o;
+}
+__device__ __forceinline__ f64x4 sum_w4d_perm(const f64x4& up, const f64x4& mid, const f64x4& dn) {
+  const double left = perm_d(lane_addr(-1), mid.w);
+  const double right = perm_d(lane_addr(1), mid.x);
+  const double p01 = mid.x + mid.y, p23 = mid.z + mid.w;
+  f64x4 o;
+  o.x = (up.x + dn.x) + (p01 + left);
+  o.y = (up.y + dn.y) + (p01 + mid.z);
+  o.z = (up.z + dn.z) + (p23 + mid.y);
+  o.w = (up.w + dn.w) + (p23 + right);
+  return o;
+}
+struct BodySumF32Perm : BodySumF32 {
+  static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, float, float) {
+    return sum_rot4f_perm(u, m, d);
+  }
+};
+struct BodySumF64Perm : BodySumF64 {
+  static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, double, double) {
+    return sum_w4d_perm(u, m, d);
+  }
+};
+
+
+template <>
+struct FastBody<float, true, 1> {
+  using type = BodySumF32Perm;
+};
+template <>
+struct FastBody<double, true, 1> {
+  using type = BodySumF64Perm;
+};
 
 }  // namespace detail
 }  // namespace kernels

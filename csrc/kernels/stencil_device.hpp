@@ -695,22 +695,24 @@ struct BodySumF64 : BodyWideF64 {
   }
 };
 
-template <typename T, bool SUM = false>
+// XB: alternative bodies of the tuner (bench/tune_kernels.hpp specialises
+// FastBody<T, SUM, 1>); the library instantiates only XB = 0.
+template <typename T, bool SUM = false, int XB = 0>
 struct FastBody;
 template <>
-struct FastBody<float, false> {
+struct FastBody<float, false, 0> {
   using type = BodyRotF32;
 };
 template <>
-struct FastBody<double, false> {
+struct FastBody<double, false, 0> {
   using type = BodyWideF64;
 };
 template <>
-struct FastBody<float, true> {
+struct FastBody<float, true, 0> {
   using type = BodySumF32;
 };
 template <>
-struct FastBody<double, true> {
+struct FastBody<double, true, 0> {
   using type = BodySumF64;
 };
 
@@ -1399,12 +1401,12 @@ struct PipeShares {
 };
 
 template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float, bool SUM = false,
-          int G = kWavesPerBlock, bool XM = false, bool JOINT = false, int LAG1 = 0>
+          int G = kWavesPerBlock, bool XM = false, bool JOINT = false, int LAG1 = 0, int XB = 0>
 __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, const PipeShares shares, T c0, T c1) {
   using P = PipeShape<S0, S1, PF>;
-  using B = typename FastBody<T, SUM>::type;
+  using B = typename FastBody<T, SUM, XB>::type;
   constexpr int OW = StripShape<T, P::S, true>::OW;
   constexpr int OWG = JointShape<S0, S1, G>::OWG;
   __shared__ typename B::V ring[G * P::RING * kWaveSize];
