@@ -227,3 +227,26 @@ def test_auto_schedule_choice_is_recorded_and_exact(gpu):
     serial.run(60)
     serial.synchronize()
     assert torch.equal(auto.core_view(), serial.core_view())
+
+
+@pytest.mark.parametrize("frame", [True, False])
+@pytest.mark.parametrize("runs", [(20,), (60, 20), (40, 7)])
+def test_peer_schedule_bare_last_pass_bitwise(gpu, monkeypatch, frame, runs):
+    """The schedule every rank of an N > 1 run follows (MXS_PEER_SCHEDULE=1 makes
+    the loopback solver take it): each call primes, exchanges after every pass
+    but the last, and ends on a bare pass (after the frame-first passes, on the
+    main stream once the side stream has joined). Bitwise the 1-rank serial
+    schedule's field; exactly one exchange per super-step."""
+    monkeypatch.setenv("MXS_PEER_SCHEDULE", "1")
+    a = _loopback(16384, 8192, seed=77, frame_overlap=frame, time_block=20)
+    monkeypatch.delenv("MXS_PEER_SCHEDULE")
+    b = _loopback(16384, 8192, seed=77, frame_overlap=False, time_block=20)
+    for n in runs:
+        a.run(n)
+        blocks = a.last_run_blocks()
+        assert a.solver.last_run_exchanges() == sum(c for _, c in blocks), (n, blocks)
+        b.run(n)
+        assert b.solver.last_run_exchanges() <= sum(c for _, c in b.last_run_blocks()) + 1
+    a.synchronize()
+    b.synchronize()
+    assert torch.equal(a.core_view(), b.core_view())
