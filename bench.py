@@ -280,6 +280,9 @@ def main(argv=None) -> int:
         extras["pipe_level_order"] = "bottom-up" if hip().last_pipe_lag1() else "top-down"
         extras["pipe_balanced_shares"] = bool(hip().pipe_balanced())  # MXS_PIPE_BALANCED=0: equal row shares
         if st.solver is not None and not st.solver.fused_periodic():
+            # Halo exchanges inside the timed window: one per super-step (with
+            # peers the call primes and ends on a bare pass).
+            extras["timed_exchanges"] = int(st.solver.last_run_exchanges())
             extras["frame_overlap"] = bool(timed_blocks and st.solver.frame_overlap(timed_blocks[0][0]))
             choice, serial_ms, frame_ms = st.solver.frame_choice()
             if choice:  # measured by prepare(): ms per super-step of each schedule
