@@ -21,7 +21,8 @@
 // Positional arguments keep the reference contract: [local width (= height) [stencil width]].
 // More options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
 // --iters N, --warmup N, --time-block S (default: measured per tile size and dtype), --no-overlap, --no-graph,
-// --frame-overlap / --no-frame-overlap (default: prepare() times both schedules, keeps the faster),
+// --frame-overlap / --no-frame-overlap / --halo-last (default: prepare() times the serial, frame-first and
+// interior-first schedules and keeps the fastest),
 // --no-direct-halo (IPC backend: pack -> put -> unpack instead of the device-initiated push),
 // --c-center C --c-neighbor C (default 0.2 / 0.2), --no-sum-form (keep the per-step evaluation in the
 // time-blocked kernels: bitwise equal to the CPU app; default: sum form when the coefficients are equal),
@@ -124,6 +125,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   cfg.use_graph = !cli.flag("no-graph");
   cfg.frame_overlap = cli.flag("frame-overlap");
   cfg.frame_auto = !cli.flag("no-frame-overlap");
+  cfg.halo_last = cli.flag("halo-last");
   cfg.loopback_self = loopback;
   cfg.coeffs = {c_center, c_neighbor, sum_form};
   cfg.time_block = time_block;
@@ -265,7 +267,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
 int main(int argc, char** argv) {
   MpiEnv env(&argc, &argv);
   Cli cli(argc, argv, {"dump", "no-dump", "non-periodic", "strict-square", "no-overlap", "overlap", "no-graph",
-                       "loopback", "pageable", "checksum", "frame-overlap", "no-frame-overlap", "no-sum-form",
+                       "loopback", "pageable", "checksum", "frame-overlap", "no-frame-overlap", "halo-last", "no-sum-form",
                        "no-direct-halo"});
   comm_timeout() = cli.get_double("comm-timeout", 300.0);
   const DeviceBinding dev = bind_device(env, cli.get("bind", "bunch"));

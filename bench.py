@@ -207,6 +207,9 @@ def main(argv=None) -> int:
                    help="multi-GPU: always exchange the next halo under the pass (frame-first overlap); default: "
                         "prepare() times it against the serial schedule and keeps the faster (docs/PERF.md)")
     p.add_argument("--no-frame-overlap", action="store_true", help="multi-GPU: always the serial schedule")
+    p.add_argument("--halo-last", action="store_true",
+                   help="multi-GPU: always the interior-first schedule (each super-step's halo exchange under the "
+                        "chunks that read only core cells); default: one of prepare()'s timed candidates")
     p.add_argument("--overlap", action="store_true", help="force the interior/exchange overlap schedule")
     p.add_argument("--loopback", action="store_true",
                    help="1 GPU: route the self-neighbour halos through RCCL (exercises the multi-GPU schedule)")
@@ -249,6 +252,7 @@ def main(argv=None) -> int:
                         graph=not args.no_graph,
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback,
                         sum_form=not args.no_sum_form, frame_overlap=(True if args.frame_overlap else (False if args.no_frame_overlap else None)),
+                        halo_last=args.halo_last,
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3)
@@ -284,10 +288,10 @@ def main(argv=None) -> int:
             # peers the call primes and ends on a bare pass).
             extras["timed_exchanges"] = int(st.solver.last_run_exchanges())
             extras["frame_overlap"] = bool(timed_blocks and st.solver.frame_overlap(timed_blocks[0][0]))
-            choice, serial_ms, frame_ms = st.solver.frame_choice()
-            if choice:  # measured by prepare(): ms per super-step of each schedule
-                extras["schedule_choice"] = {"chosen": choice, "serial_ms": round(serial_ms, 4),
-                                             "frame_first_ms": round(frame_ms, 4)}
+            extras["halo_last"] = bool(timed_blocks and st.solver.halo_last(timed_blocks[0][0]))
+            times = st.solver.schedule_times()
+            if times["chosen"]:  # measured by prepare(): ms per super-step of each candidate (0 = not one)
+                extras["schedule_choice"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in times.items()}
     del st
     if gpu:
         torch.cuda.empty_cache()

@@ -217,6 +217,151 @@ inline FrameSchedule make_frame_schedule(std::int64_t groups, std::int64_t rows,
   return s;
 }
 
+// ---------------------------------------------------------------- halo last
+// Interior-first schedule of a PRE-exchange super-step (the reference's
+// "exchange, then compute", stencil2d/mpi-2d-stencil-subarray-cuda.cu:169-172,
+// with the compute split so the exchange hides under it). The pass is cut into
+// two sets of chunks that two launches of the chunk-list kernel run on
+// disjoint CUs:
+//   * inner: chunks whose input footprint lies in the core (not an edge group,
+//     rows [hf, rows - hf) with hf >= S): launched first, on `blocks - outer`
+//     workgroups, while pack -> RCCL -> unpack of this super-step's halo runs on
+//     the CUs it leaves free (a pipeline workgroup fills its CU; RCCL's kernels
+//     need whole CUs);
+//   * outer: the chunks that read the ghost ring (the edge groups whose joint
+//     windows reach into the ghost columns, the top / bottom hf rows of the other
+//     groups): launched after the unpack, on `outer` workgroups.
+// `outer` is sized so that the outer set, started `lead` row iterations late
+// (the exchange), ends with the inner set, in steps of `granule` workgroups:
+// workgroups are dealt round-robin over the 8 XCDs, so with both launches a
+// multiple of 8 every XCD holds the same split and each outer workgroup finds a
+// free CU (36 outer next to 220 inner left some XCDs one CU short: that outer
+// workgroup waited for an inner one and the pass took 1.7x as long).
+struct HaloLastSchedule {
+  FrameSchedule inner;
+  FrameSchedule outer;
+  std::int64_t hf = 0;
+  double inner_cost = 0, outer_cost = 0;  // slowest workgroup (rows + fills) of each set
+  double serial_cost = 0;                 // the same pass as one balanced launch
+};
+
+namespace detail {
+// Fill-aware partition of `runs` over `blocks` workgroups (equal budgets).
+inline FrameSchedule partition_runs(const std::vector<Run>& runs, int blocks, std::int64_t fill, double* cost) {
+  FrameSchedule s;
+  s.blocks = blocks;
+  std::vector<std::vector<FrameChunk>> lists(static_cast<size_t>(blocks));
+  std::vector<std::int64_t> load(static_cast<size_t>(blocks), 0);
+  if (!runs.empty()) {
+    const std::int64_t T = min_budget(runs, blocks, fill, [](int, std::int64_t t) { return t; });
+    greedy_walk(runs, blocks, fill, [&](int) { return T; },
+                [&](int w, std::int32_t g, std::int64_t r0, std::int64_t r1) {
+                  lists[size_t(w)].push_back(FrameChunk{g, std::int32_t(r0), std::int32_t(r1), 0});
+                  load[size_t(w)] += r1 - r0 + fill;
+                });
+  }
+  double c = 0;
+  size_t entries = 1;
+  for (int w = 0; w < blocks; ++w) {
+    c = std::max(c, double(load[size_t(w)]));
+    entries = std::max(entries, lists[size_t(w)].size());
+  }
+  if (cost) *cost = c;
+  s.entries = int(entries);
+  s.bulk_cost = c;
+  s.table.assign(size_t(blocks) * entries, FrameChunk{0, 0, 0, 0});
+  for (int w = 0; w < blocks; ++w)
+    for (size_t e = 0; e < lists[size_t(w)].size(); ++e) s.table[size_t(w) * entries + e] = lists[size_t(w)][e];
+  return s;
+}
+inline std::int64_t runs_cost(const std::vector<Run>& runs, int blocks, std::int64_t fill) {
+  if (runs.empty()) return 0;
+  if (blocks <= 0) return std::int64_t(1) << 40;
+  return min_budget(runs, blocks, fill, [](int, std::int64_t t) { return t; });
+}
+}  // namespace detail
+
+// ghost_group[g]: group g's joint windows read ghost columns (its chunks are all
+// outer). depth: the time block S (hf >= depth). outer_wgs: 0 = auto from
+// lead_frac (the exchange's share of a serial pass). frame_rows: hf (0 = depth).
+inline HaloLastSchedule make_halo_last_schedule(std::int64_t groups, std::int64_t rows, int blocks, std::int64_t fill,
+                                                std::int64_t depth, const std::vector<std::uint8_t>& ghost_group,
+                                                int outer_wgs = 0, double lead_frac = 0.12,
+                                                std::int64_t frame_rows = 0, int granule = 1, int min_outer = 1) {
+  if (groups <= 0 || rows <= 0 || blocks < 2 || fill < 0 || depth <= 0 || std::int64_t(ghost_group.size()) != groups)
+    throw std::invalid_argument("make_halo_last_schedule: bad shape");
+  HaloLastSchedule h;
+  h.hf = std::max(depth, frame_rows);
+  std::vector<detail::Run> inner, outer, all;
+  for (std::int64_t g = 0; g < groups; ++g) {
+    const auto gi = std::int32_t(g);
+    all.push_back(detail::Run{gi, 0, rows});
+    if (ghost_group[size_t(g)] || rows <= 2 * h.hf) {
+      outer.push_back(detail::Run{gi, 0, rows});
+    } else {
+      outer.push_back(detail::Run{gi, 0, h.hf});
+      outer.push_back(detail::Run{gi, rows - h.hf, rows});
+      inner.push_back(detail::Run{gi, h.hf, rows - h.hf});
+    }
+  }
+  if (inner.empty()) throw std::invalid_argument("make_halo_last_schedule: no interior");
+  h.serial_cost = double(detail::runs_cost(all, blocks, fill));
+  granule = std::max(1, granule);
+  int m = outer_wgs;
+  if (m <= 0) {
+    // The smallest outer set whose (delayed) finish does not trail the inner set,
+    // and no fewer than min_outer: the exchange's kernels run on the CUs the
+    // inner launch leaves free (RCCL's p2p kernel starved on 8-16 free CUs and
+    // finished only with the inner launch, profiles/r03_halolast).
+    const double lead = lead_frac * h.serial_cost;
+    double best = 1e300;
+    const int k0 = std::max(granule, (std::max(1, min_outer) + granule - 1) / granule * granule);
+    for (int k = k0; k < blocks; k += granule) {
+      const double ci = double(detail::runs_cost(inner, blocks - k, fill));
+      const double co = lead + double(detail::runs_cost(outer, k, fill));
+      const double t = std::max(ci, co);
+      if (t < best) {
+        best = t;
+        m = k;
+      }
+      if (co <= ci) break;  // more outer workgroups only slow the inner set
+    }
+  }
+  if (m <= 0) m = std::max(granule, min_outer);
+  m = std::min(std::max(m, 1), blocks - 1);
+  h.inner = detail::partition_runs(inner, blocks - m, fill, &h.inner_cost);
+  h.outer = detail::partition_runs(outer, m, fill, &h.outer_cost);
+  return h;
+}
+
+// Both sets together cover every (group, row) exactly once; every inner chunk's
+// input footprint (rows [r0 - depth, r1 + depth), a non-ghost group) is in the
+// core. Returns "" or the first violation (tests).
+inline std::string check_halo_last_schedule(const HaloLastSchedule& h, std::int64_t groups, std::int64_t rows,
+                                            std::int64_t depth, const std::vector<std::uint8_t>& ghost_group) {
+  std::vector<std::uint8_t> seen(size_t(groups * rows), 0);
+  for (int set = 0; set < 2; ++set) {
+    const FrameSchedule& s = set == 0 ? h.inner : h.outer;
+    for (int w = 0; w < s.blocks; ++w)
+      for (int e = 0; e < s.entries; ++e) {
+        const FrameChunk& c = s.at(w, e);
+        if (c.r1 <= c.r0) continue;
+        if (c.group < 0 || c.group >= groups || c.r0 < 0 || c.r1 > rows) return "chunk out of range";
+        if (c.flags != 0) return "halo-last chunks carry no signal";
+        if (set == 0 && (ghost_group[size_t(c.group)] || c.r0 < depth || c.r1 > rows - depth))
+          return "inner chunk reads the ghost ring";
+        for (std::int64_t r = c.r0; r < c.r1; ++r) {
+          auto& v = seen[size_t(c.group * rows + r)];
+          if (v) return "row covered twice";
+          v = 1;
+        }
+      }
+  }
+  for (auto v : seen)
+    if (!v) return "row not covered";
+  return "";
+}
+
 // Every (group, row) covered exactly once, frame chunks first and signalled,
 // every output frame row / edge group inside a signalled chunk. Returns "" or
 // the first violation (tests).

@@ -152,6 +152,10 @@ struct FramePassShape {
   index_t groups = 0;  // column groups of OWG output columns over the core width
   index_t owg = 0;
   index_t fill = 0;    // pipeline-fill row iterations per chunk
+  // Input columns a group's joint windows read: [x - read_lead, x - read_lead +
+  // read_span) for a group whose first output column is x (its chunks read the
+  // ghost columns when that range leaves [0, width)).
+  index_t read_lead = 0, read_span = 0;
 };
 // False when `steps` has no frame-first form here (fp32 S = 20 / 24, fp64
 // S = 16 on whole lane vectors; other depths keep the serial schedule). The

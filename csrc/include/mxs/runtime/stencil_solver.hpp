@@ -51,6 +51,16 @@
 // grid fuses the self-exchange into the kernel's wrap-around addressing
 // (`fuse_periodic_self`).
 //
+// Interior-first opening (`halo_last`; or picked by `frame_auto`'s measurement):
+// the call's first super-step, when it starts with a priming exchange, is two
+// launches of the chunk-list kernel on disjoint CUs:
+//
+//   side stream : inner chunks (input in the core), blocks - outer workgroups
+//   main stream : pack(cur) -> RCCL -> unpack(cur) -> outer chunks (ghost ring)
+//
+// (the fork is skipped when main has drained, e.g. after synchronize(): a
+// cross-stream wait costs ~15 us). A 20-step window at N > 1 is exactly this.
+//
 // Frame-first overlap (`frame_overlap` forces it; `frame_auto`, the default, picks it
 // when prepare() measures it faster than the serial schedule): with remote
 // peers over RCCL and a depth that has a frame form (fp32 S = 20 / 24, fp64
@@ -140,6 +150,15 @@ struct SolverConfig {
   // of each schedule (state-preserving, collective like prepare itself) and
   // keeps the faster one; until then, and when no prepare() runs, serial.
   bool frame_auto = true;
+  // Interior-first (halo-last) opening: the first super-step of a call, which
+  // starts with a priming exchange (with peers: every call), runs the chunks
+  // whose input lies in the core on most CUs while that exchange runs on the
+  // CUs they leave free, then the chunks that read the ghost ring
+  // (kernels::make_halo_last_schedule). Forced by `halo_last`; with frame_auto
+  // prepare() times it against the serial opening (prime, then the pass).
+  // Only the opening: back-to-back interior-first super-steps pay two
+  // cross-stream waits each (measured 35% slower over 12 super-steps).
+  bool halo_last = false;
   // Frame-only workgroups that exit early and leave their CUs to the exchange
   // (-1: MXS_FRAME_COMM_WGS or 16), and the frame chunk height (0: MXS_FRAME_ROWS
   // or auto, kernels::make_frame_schedule).
@@ -199,6 +218,12 @@ class StencilSolver {
   bool overlapped() const { return cfg_.overlap; }
   // Whether super-steps of depth S run the frame-first overlapped schedule.
   bool frame_overlap(int S) const;
+  // Whether the opening super-step of a call at depth S runs interior-first
+  // (halo-last: its priming exchange under the core chunks).
+  bool halo_last(int S) const;
+  const std::string& opening_choice() const { return opening_choice_; }
+  double opening_serial_ms() const { return opening_ms_[0]; }
+  double opening_halo_last_ms() const { return opening_ms_[1]; }
   // The auto choice: "" before prepare() decided, else "frame" or "serial" and
   // the median times (ms per super-step) of both.
   const std::string& frame_choice() const { return frame_choice_; }
@@ -243,7 +268,9 @@ class StencilSolver {
   void split(int iters, Group out[2]) const;
   // `count` super-steps of size S; `last_bare`: the last one is a pass without
   // its trailing exchange (with peers, the next call primes anyway).
-  void run_group(int S, int count, bool last_bare = false);
+  // `first`: the call's first group (an interior-first opening may take its
+  // first super-step).
+  void run_group(int S, int count, bool last_bare = false, bool first = false);
   void enqueue_bare_pass(T* cur, T* nxt, int S);  // post-exchange pass, no exchange after it
 
   // Frame-first pass of depth S: shape + schedule + device table.
@@ -254,6 +281,19 @@ class StencilSolver {
     DeviceBuffer<kernels::FrameChunk> table;
   };
   FramePass* frame_pass(int S, bool build);  // nullptr: serial schedule for S
+  // Interior-first pass of depth S: two launches of the chunk-list kernel
+  // (inner on blocks - outer workgroups, outer after the exchange).
+  struct HaloLastPass {
+    int S = 0;
+    kernels::FramePassShape inner_shape, outer_shape;  // blocks = workgroups of each launch
+    kernels::HaloLastSchedule sched;
+    DeviceBuffer<kernels::FrameChunk> inner_table, outer_table;
+  };
+  HaloLastPass* halo_last_pass(int S, bool build);  // nullptr: not in use / no form for S
+  void enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl);
+  bool halo_last_on_ = false;                // a call's opening super-step runs interior-first
+  std::vector<std::unique_ptr<HaloLastPass>> halo_lasts_;
+  std::vector<int> no_halo_last_;
   // Super-steps exchange AFTER their pass (the ghost ring of the next pass's
   // input): every schedule but the fused periodic, the direct IPC halo and the
   // thin-strip overlap, which exchange first.
@@ -263,7 +303,9 @@ class StencilSolver {
   bool frame_allowed_ = false;               // config / backend / peers allow the overlap
   bool frame_on_ = false;                    // the frame-first schedule is in use (forced, or chosen)
   std::string frame_choice_;
-  double choice_ms_[2] = {0, 0};
+  double choice_ms_[2] = {0, 0};     // steady super-steps: serial, frame-first (ms each)
+  double opening_ms_[2] = {0, 0};    // a call's opening super-step: prime + pass, interior-first (ms)
+  std::string opening_choice_;       // "" before prepare() decided, "serial" or "halo-last"
   void choose_schedule(int S);               // frame_auto: time both, keep the faster
   bool side_pending_ = false;                // frame passes on the side stream not yet joined to main
   void join_side();                          // main stream waits for the side stream's work

@@ -38,6 +38,9 @@ void fill_shape(const TileGeom& g, FramePassShape* out) {
   out->owg = OWG;
   out->groups = (g.width + OWG - 1) / OWG;
   out->fill = pipe_fill_rows<JS0, S - JS0, pipe_pf<T, S>(), LAG1>();
+  using J = JointShape<JS0, S - JS0, kWavesPerBlock>;
+  out->read_lead = J::LEAD;
+  out->read_span = (kWavesPerBlock - 1) * J::OW0 + 256;
 }
 
 template <typename T, int S, bool SUM>

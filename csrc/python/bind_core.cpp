@@ -189,4 +189,37 @@ PYBIND11_MODULE(_mxs_core, m) {
       py::arg("groups"), py::arg("rows"), py::arg("blocks"), py::arg("fill"), py::arg("frame_rows") = 0,
       py::arg("comm_wgs") = 8, py::arg("edge_left") = 1, py::arg("edge_right") = 1,
       "per-workgroup chunk lists (group, r0, r1, flags) + the coverage check ('' = ok)");
+  // Interior-first (halo-last) schedule of the pre-exchange overlapped pass.
+  m.def(
+      "halo_last_schedule",
+      [](std::int64_t groups, std::int64_t rows, int blocks, std::int64_t fill, std::int64_t depth,
+         std::vector<std::uint8_t> ghost, int outer_wgs, double lead_frac, std::int64_t frame_rows, int granule, int min_outer) {
+        const auto h = kernels::make_halo_last_schedule(groups, rows, blocks, fill, depth, ghost, outer_wgs, lead_frac,
+                                                        frame_rows, granule, min_outer);
+        auto lists = [](const kernels::FrameSchedule& s) {
+          py::list table;
+          for (int w = 0; w < s.blocks; ++w) {
+            py::list l;
+            for (int e = 0; e < s.entries; ++e) {
+              const auto& c = s.at(w, e);
+              if (c.r1 > c.r0) l.append(py::make_tuple(c.group, c.r0, c.r1));
+            }
+            table.append(l);
+          }
+          return table;
+        };
+        py::dict d;
+        d["inner"] = lists(h.inner);
+        d["outer"] = lists(h.outer);
+        d["hf"] = h.hf;
+        d["inner_cost"] = h.inner_cost;
+        d["outer_cost"] = h.outer_cost;
+        d["serial_cost"] = h.serial_cost;
+        d["check"] = kernels::check_halo_last_schedule(h, groups, rows, depth, ghost);
+        return d;
+      },
+      py::arg("groups"), py::arg("rows"), py::arg("blocks"), py::arg("fill"), py::arg("depth"), py::arg("ghost"),
+      py::arg("outer_wgs") = 0, py::arg("lead_frac") = 0.12, py::arg("frame_rows") = 0, py::arg("granule") = 1,
+      py::arg("min_outer") = 1,
+      "inner / outer chunk lists (group, r0, r1) of the interior-first pass + the check ('' = ok)");
 }

@@ -398,9 +398,11 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        bool use_graph, bool loopback_self, StencilKind kind, double c0, double c1, int box_radius,
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
                        py::object bootstrap, int graph_supersteps, bool sum_form, bool direct_halo, bool frame_overlap,
-                       int frame_comm_wgs, int frame_rows, double graph_max_superstep_us, bool frame_auto) {
+                       int frame_comm_wgs, int frame_rows, double graph_max_superstep_us, bool frame_auto,
+                       bool halo_last) {
              SolverConfig cfg;
              cfg.frame_auto = frame_auto;
+             cfg.halo_last = halo_last;
              cfg.graph_max_superstep_us = graph_max_superstep_us;
              cfg.frame_overlap = frame_overlap;
              cfg.frame_comm_wgs = frame_comm_wgs;
@@ -435,20 +437,39 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
            py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = false,
            py::arg("frame_overlap") = false, py::arg("frame_comm_wgs") = -1, py::arg("frame_rows") = 0,
-           py::arg("graph_max_superstep_us") = 150.0, py::arg("frame_auto") = true,
+           py::arg("graph_max_superstep_us") = 150.0, py::arg("frame_auto") = true, py::arg("halo_last") = false,
            py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")
       .def(
           "frame_overlap", [](SolverHandle& h, int S) { return h.visit([S](auto& s) { return s.frame_overlap(S); }); },
           py::arg("S"), "whether super-steps of depth S run the frame-first overlapped schedule")
+      .def(
+          "halo_last", [](SolverHandle& h, int S) { return h.visit([S](auto& s) { return s.halo_last(S); }); },
+          py::arg("S"), "whether a call's opening super-step of depth S runs interior-first (halo-last)")
+      .def("schedule_times",
+           [](SolverHandle& h) {
+             return h.visit([](auto& s) {
+               py::dict d;
+               d["chosen"] = s.frame_choice();
+               d["serial_ms"] = s.frame_choice_serial_ms();
+               d["frame_first_ms"] = s.frame_choice_frame_ms();
+               d["opening"] = s.opening_choice();
+               d["opening_serial_ms"] = s.opening_serial_ms();
+               d["opening_halo_last_ms"] = s.opening_halo_last_ms();
+               return d;
+             });
+           },
+           "prepare()'s measurements: steady super-steps (serial / frame-first, ms each) and a call's opening "
+           "super-step (prime + pass / interior-first, ms); 0 = not a candidate")
       .def("frame_choice",
            [](SolverHandle& h) {
              return h.visit([](auto& s) {
                return py::make_tuple(s.frame_choice(), s.frame_choice_serial_ms(), s.frame_choice_frame_ms());
              });
            },
-           "auto schedule choice made by prepare(): (\"\" | \"serial\" | \"frame\", serial ms, frame ms per super-step)")
+           "auto schedule choice made by prepare(): (\"\" | \"serial\" | \"frame\" | \"halo-last\", serial ms, frame ms "
+           "per super-step)")
       .def("sum_form_active", [](SolverHandle& h) { return h.visit([](auto& s) { return s.sum_form_active(); }); })
       .def("sum_form_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.sum_form_note(); }); })
       .def("last_run_blocks", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_blocks(); }); },

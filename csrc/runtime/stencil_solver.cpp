@@ -76,11 +76,12 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
            kernels::stencil5_periodic_supported<T>(tile_);
   // Frame-first overlap: RCCL with a wire transfer, the tuned kernel forms,
   // every edge a neighbour's (time blocking), the thin-strip overlap off.
-  frame_allowed_ = (cfg_.frame_overlap || cfg_.frame_auto) && cfg_.backend == HaloBackend::Rccl &&
+  frame_allowed_ = (cfg_.frame_overlap || cfg_.frame_auto || cfg_.halo_last) && cfg_.backend == HaloBackend::Rccl &&
                    !plan.sends.empty() && !fused_ &&
                    cfg_.kind == StencilKind::Jacobi5 && cfg_.variant == kernels::StencilVariant::Auto &&
                    block_ > 1 && !cfg_.overlap;
   frame_on_ = frame_allowed_ && cfg_.frame_overlap;
+  halo_last_on_ = frame_allowed_ && cfg_.halo_last;
   if (frame_allowed_) {
     frame_ctl_.reset(1);
     MXS_HIP_CHECK(hipMemsetAsync(frame_ctl_.get(), 0, sizeof(unsigned), main_.get()));
@@ -330,9 +331,21 @@ void StencilSolver<T>::split(int iters, Group out[2]) const {
 }
 
 template <typename T>
-void StencilSolver<T>::run_group(int S, int count, bool last_bare) {
+void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
   if (count <= 0) return;
   last_blocks_.emplace_back(S, count);
+  // Interior-first opening: the call's first super-step would start with a
+  // priming exchange (with peers: every call); run it under the core chunks.
+  if (first && halo_last_on_ && post_exchange() && !ghost_fresh_) {
+    if (HaloLastPass* hl = halo_last_pass(S, true)) {
+      enqueue_halo_last(cur_, nxt_, hl);
+      std::swap(cur_, nxt_);
+      ++last_exchanges_;
+      ghost_fresh_ = false;  // its output's ring: primed by the next super-step / call
+      if (--count == 0) return;
+    }
+  }
+  join_side();  // an interior-first opening (or frame passes) may leave side work pending
   // Post-exchange super-steps (frame-first and serial): cur's ghost ring must
   // be fresh before the first one; each leaves the next one's fresh. The
   // thin-strip overlap schedule exchanges first and leaves it stale.
@@ -417,6 +430,8 @@ void StencilSolver<T>::ensure_range() {
   graphs_.clear();
   frames_.clear();
   no_frame_.clear();
+  halo_lasts_.clear();
+  no_halo_last_.clear();
   warmed_.clear();
 }
 
@@ -442,8 +457,9 @@ void StencilSolver<T>::run(int iters) {
   split(iters, gr);
   // With peers every call primes (begin_run), so the exchange after the call's
   // last pass would be redundant: it ends on a bare pass (header).
-  const int last = gr[1].count > 0 ? 1 : 0;
-  for (int k = 0; k < 2; ++k) run_group(gr[k].S, gr[k].count, multi_rank_ && bare_tail_ && k == last);
+  const int last = gr[1].count > 0 ? 1 : 0, first = gr[0].count > 0 ? 0 : 1;
+  for (int k = 0; k < 2; ++k)
+    run_group(gr[k].S, gr[k].count, multi_rank_ && bare_tail_ && k == last, k == first);
 }
 
 template <typename T>
@@ -504,38 +520,176 @@ bool StencilSolver<T>::frame_overlap(int S) const {
 // differently still match each other's sends and receives.
 template <typename T>
 void StencilSolver<T>::choose_schedule(int S) {
-  if (!frame_allowed_ || !cfg_.frame_auto || cfg_.frame_overlap || !frame_choice_.empty()) return;
+  if (!frame_allowed_ || !cfg_.frame_auto || cfg_.frame_overlap || cfg_.halo_last || !frame_choice_.empty()) return;
   frame_on_ = true;
   const bool has_frame = frame_pass(S, true) != nullptr;
-  if (!has_frame) {
-    frame_on_ = false;
-    return;  // no frame form at this depth: nothing to choose (decided at the next prepare)
-  }
+  frame_on_ = false;
+  halo_last_on_ = true;
+  HaloLastPass* hl = halo_last_pass(S, true);
+  halo_last_on_ = false;
+  if (!has_frame && !hl) return;  // nothing to choose at this depth (decided at the next prepare)
   if (!ghost_fresh_) {
     ex_->exchange(cur_, main_.get());
     ghost_fresh_ = true;
   }
-  std::vector<double> t[2];
+  // Steady super-steps: serial vs frame-first, 2 back-to-back super-steps each.
+  // Opening super-step of a call (a priming exchange, then the pass): serial
+  // vs interior-first, one super-step from drained streams, as a short timed
+  // window sees it. Alternating rounds, medians; every launch is state-preserving
+  // (cur -> nxt, cur's ring re-exchanged with the same values).
+  std::vector<double> t[4];
   Event e0(true), e1(true);
-  for (int rep = 0; rep < 4; ++rep)
+  auto timed = [&](auto&& enqueue) {
+    join_side();
+    main_.sync();
+    side_.sync();
+    side_pending_ = false;
+    e0.record(main_.get());
+    enqueue();
+    join_side();
+    e1.record(main_.get());
+    e1.sync();
+    return double(e1.since(e0));
+  };
+  // A candidate without a form here is replaced by the serial one, so every
+  // rank issues the same exchanges whatever it can run.
+  for (int rep = 0; rep < 4; ++rep) {
     for (int mode = 0; mode < 2; ++mode) {
-      frame_on_ = mode == 1;
-      join_side();
-      main_.sync();
-      side_.sync();
-      e0.record(main_.get());
-      for (int i = 0; i < 2; ++i) enqueue_block(cur_, nxt_, S);
-      join_side();
-      e1.record(main_.get());
-      e1.sync();
-      if (rep > 0) t[mode].push_back(double(e1.since(e0)) / 2.0);  // the first round warms both
+      frame_on_ = mode == 1 && has_frame;
+      const double ms = timed([&] {
+        for (int i = 0; i < 2; ++i) enqueue_block(cur_, nxt_, S);
+      });
+      if (rep > 0 && (mode == 0 || has_frame)) t[mode].push_back(ms / 2.0);  // round 0 warms every shape
     }
-  for (int mode = 0; mode < 2; ++mode) {
-    std::sort(t[mode].begin(), t[mode].end());
-    choice_ms_[mode] = t[mode][t[mode].size() / 2];
+    frame_on_ = false;
+    const double serial_open = timed([&] {
+      ex_->exchange(cur_, main_.get());
+      enqueue_bare_pass(cur_, nxt_, S);
+    });
+    const double hl_open = timed([&] {
+      if (hl) {
+        enqueue_halo_last(cur_, nxt_, hl);
+      } else {
+        ex_->exchange(cur_, main_.get());
+        enqueue_bare_pass(cur_, nxt_, S);
+      }
+    });
+    if (rep > 0) {
+      t[2].push_back(serial_open);
+      if (hl) t[3].push_back(hl_open);
+    }
   }
-  frame_on_ = choice_ms_[1] < choice_ms_[0];
+  auto median = [](std::vector<double>& v) {
+    if (v.empty()) return 0.0;
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+  };
+  choice_ms_[0] = median(t[0]);
+  choice_ms_[1] = median(t[1]);
+  opening_ms_[0] = median(t[2]);
+  opening_ms_[1] = median(t[3]);
+  frame_on_ = has_frame && choice_ms_[1] < choice_ms_[0];
+  halo_last_on_ = hl && opening_ms_[1] < opening_ms_[0];
   frame_choice_ = frame_on_ ? "frame" : "serial";
+  opening_choice_ = halo_last_on_ ? "halo-last" : "serial";
+}
+
+// Interior-first pass of depth S (built on first use while the schedule is on).
+// Workgroups are dealt round-robin over the XCDs: both launches of the pass are
+// sized in multiples of this (kernels::make_halo_last_schedule).
+constexpr int kXcds = 8;
+template <typename T>
+typename StencilSolver<T>::HaloLastPass* StencilSolver<T>::halo_last_pass(int S, bool build) {
+  if (!halo_last_on_) return nullptr;
+  for (auto& h : halo_lasts_)
+    if (h->S == S) return h.get();
+  if (!build || std::find(no_halo_last_.begin(), no_halo_last_.end(), S) != no_halo_last_.end()) return nullptr;
+  kernels::FramePassShape shape;
+  if (!kernels::frame_pass_shape<T>(tile_, S, cfg_.coeffs, &shape) || shape.blocks < 2) {
+    no_halo_last_.push_back(S);
+    return nullptr;
+  }
+  // Groups whose joint windows read ghost columns (all their chunks are outer).
+  std::vector<std::uint8_t> ghost(size_t(shape.groups), 0);
+  for (index_t g = 0; g < shape.groups; ++g) {
+    const index_t x0 = g * shape.owg - shape.read_lead;
+    ghost[size_t(g)] = (x0 < 0 || x0 + shape.read_span > tile_.width) ? 1 : 0;
+  }
+  auto env_num = [](const char* k, double dflt) {
+    const char* e = std::getenv(k);
+    return e && *e ? std::atof(e) : dflt;
+  };
+  auto hl = std::make_unique<HaloLastPass>();
+  hl->S = S;
+  try {
+    hl->sched = kernels::make_halo_last_schedule(shape.groups, tile_.height, shape.blocks, shape.fill, S, ghost,
+                                                 int(env_num("MXS_HALO_LAST_WGS", 0)),
+                                                 env_num("MXS_HALO_LAST_LEAD", 0.12),
+                                                 std::int64_t(env_num("MXS_HALO_LAST_ROWS", 0)),
+                                                 shape.blocks % kXcds == 0 ? kXcds : 1,
+                                                 int(env_num("MXS_HALO_LAST_MIN_WGS", 32)));
+  } catch (const std::invalid_argument&) {
+    no_halo_last_.push_back(S);
+    return nullptr;
+  }
+  index_t longest = 0;
+  for (const auto* sc : {&hl->sched.inner, &hl->sched.outer})
+    for (const auto& c : sc->table) longest = std::max<index_t>(longest, c.r1 - c.r0);
+  if (longest * tile_.pitch * index_t(sizeof(T)) > kernels::kMaxChunkBytes) {
+    no_halo_last_.push_back(S);  // a chunk past the buffer-descriptor range
+    return nullptr;
+  }
+  hl->inner_shape = shape;
+  hl->inner_shape.blocks = hl->sched.inner.blocks;
+  hl->outer_shape = shape;
+  hl->outer_shape.blocks = hl->sched.outer.blocks;
+  hl->inner_table.reset(index_t(hl->sched.inner.table.size()));
+  hl->outer_table.reset(index_t(hl->sched.outer.table.size()));
+  MXS_HIP_CHECK(hipMemcpy(hl->inner_table.get(), hl->sched.inner.table.data(), hl->inner_table.bytes(),
+                          hipMemcpyHostToDevice));
+  MXS_HIP_CHECK(hipMemcpy(hl->outer_table.get(), hl->sched.outer.table.data(), hl->outer_table.bytes(),
+                          hipMemcpyHostToDevice));
+  halo_lasts_.push_back(std::move(hl));
+  return halo_lasts_.back().get();
+}
+
+template <typename T>
+bool StencilSolver<T>::halo_last(int S) const {
+  if (!halo_last_on_) return false;
+  for (const auto& h : halo_lasts_)
+    if (h->S == S) return true;
+  return std::find(no_halo_last_.begin(), no_halo_last_.end(), S) == no_halo_last_.end() &&
+         kernels::frame_pass_shape<T>(tile_, S, cfg_.coeffs, nullptr);
+}
+
+// One interior-first super-step, cur -> nxt. cur must be complete (the side
+// stream's previous inner launch joined to main, then main forks the side
+// stream), so the inner launch reads a finished core while the main stream
+// exchanges cur's ghost ring (disjoint cells) and then runs the outer chunks;
+// the two launches write disjoint cells of nxt. The inner launch is submitted
+// first, so it holds its CUs before RCCL's kernels look for free ones; with
+// streams that share a hardware queue everything simply runs in order.
+template <typename T>
+void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl) {
+  MXS_TRACE_RANGE("stencil.superstep_halo_last");
+  hipStream_t m = main_.get(), side = side_.get();
+  join_side();
+  // The inner launch reads cur: it must follow everything enqueued on main.
+  // When main has drained (a call after synchronize()) the fork is skipped: a
+  // cross-stream wait costs ~15 us of queue-to-queue latency, and the timed
+  // window of an N > 1 bench run is one such super-step.
+  if (hipStreamQuery(m) != hipSuccess) {
+    (void)hipGetLastError();  // hipErrorNotReady is not an error here
+    fork_.record(m);
+    fork_.wait_on(side);
+  }
+  kernels::stencil5_frame_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->inner_shape, hl->inner_table.get(),
+                                  hl->sched.inner.entries, frame_ctl_.get(), side);
+  side_pending_ = true;
+  ex_->set_copy_block(64);  // one-wave copy workgroups fit beside a pipeline workgroup
+  ex_->exchange(cur, m);
+  kernels::stencil5_frame_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->outer_shape, hl->outer_table.get(),
+                                  hl->sched.outer.entries, frame_ctl_.get(), m);
 }
 
 template <typename T>
@@ -564,6 +718,10 @@ void StencilSolver<T>::prepare(int iters) {
   for (const Group& g : gr) {
     if (g.count <= 0) continue;
     (void)frame_pass(g.S, true);
+    if (HaloLastPass* hl = halo_last_pass(g.S, true); hl && std::find(warmed_.begin(), warmed_.end(), g.S) == warmed_.end()) {
+      enqueue_halo_last(cur_, nxt_, hl);  // cur -> nxt (scratch), cur's ring re-exchanged: state unchanged
+      join_side();
+    }
     if (post_exchange() && !ghost_fresh_) {
       ex_->exchange(cur_, main_.get());
       ghost_fresh_ = true;
@@ -613,6 +771,7 @@ void StencilSolver<T>::step() {
 
 template <typename T>
 void StencilSolver<T>::exchange_only() {
+  join_side();
   ex_->exchange(cur_, main_.get());
   ghost_fresh_ = true;
 }
@@ -627,6 +786,7 @@ void StencilSolver<T>::synchronize() {
   if (direct_) direct_->wait(main_.get());
   main_.spin_sync();
   side_.spin_sync();
+  side_pending_ = false;  // both streams drained: nothing for main to wait for
   ex_->check();  // IPC backend: device-side waits carry their own deadline
   if (direct_) direct_->check();
   if (frame_status_.get()) {

@@ -86,6 +86,11 @@ class StencilConfig:
     frame_overlap: bool | None = None
     frame_comm_wgs: int = -1         # frame-only workgroups leaving CUs to the exchange (-1 = default)
     frame_rows: int = 0              # frame chunk height (0 = auto)
+    # Interior-first opening: a call's first super-step, which starts with a
+    # priming exchange (with peers: every call), runs its core chunks while that
+    # exchange runs on the CUs they leave free. True forces it; with
+    # frame_overlap=None prepare() times it against the serial opening.
+    halo_last: bool = False
     # Super-steps estimated longer than this run from eager launches, not a
     # hipGraph (long passes: eager measured faster). 0 = always graphs.
     graph_max_superstep_us: float = 150.0
@@ -176,7 +181,8 @@ class Stencil2D:
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
                                           backend == "ipc" and cfg.direct_halo is not False,
                                           bool(cfg.frame_overlap), cfg.frame_comm_wgs, cfg.frame_rows,
-                                          cfg.graph_max_superstep_us, cfg.frame_overlap is None)
+                                          cfg.graph_max_superstep_us, cfg.frame_overlap is None and not cfg.halo_last,
+                                          cfg.halo_last)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
@@ -344,12 +350,18 @@ class Stencil2D:
         if self.solver.direct_halo():
             return "ipc direct (device-initiated push of each pass's edge bands into the neighbours' tiles)" + blk
         choice = self.solver.frame_choice()[0]
+        opening = ""
+        if tb > 1 and self.solver.halo_last(tb):
+            opening = (" + interior-first opening (a call's priming exchange runs under the chunks that read only "
+                       "core cells; the ghost-ring chunks follow on the CUs left free)")
         if tb > 1 and self.solver.frame_overlap(tb):
             return (f"{self.backend} + frame-first overlap (each pass stores its {tb}-deep output frame first; "
-                    f"the next halo's pack -> RCCL send/recv -> unpack runs under the rest of the pass)" + blk)
+                    f"the next halo's pack -> RCCL send/recv -> unpack runs under the rest of the pass)" + opening + blk)
+        if opening:
+            return f"{self.backend}" + opening + blk
         mode = " + overlap" if self.solver.overlapped() else ""
         if not mode and tb > 1 and self.backend == "rccl" and choice == "serial":
-            mode = " (pass, then halo exchange; prepare() measured the frame-first overlap slower)"
+            mode = " (pass, then halo exchange; prepare() measured the overlapped schedules slower)"
         return f"{self.backend}" + mode + blk
 
     # ----------------------------------------------------------------- dump

@@ -22,10 +22,12 @@ p = argparse.ArgumentParser()
 p.add_argument("--tile", default="16384x8192")
 p.add_argument("--k", type=int, default=20)
 p.add_argument("--reps", type=int, default=12)
+p.add_argument("--halo-last", action="store_true", help="the interior-first schedule instead of the serial one")
 a = p.parse_args()
 w, h = (int(x) for x in a.tile.split("x"))
 ctx = init(backend="gloo", device="cuda")
-st = Stencil2D(StencilConfig(global_width=w, global_height=h, dims="1x1", dtype="f32", loopback=True), ctx)
+st = Stencil2D(StencilConfig(global_width=w, global_height=h, dims="1x1", dtype="f32", loopback=True,
+                             frame_overlap=False, halo_last=a.halo_last), ctx)
 st.run(5)
 st.prepare(a.k)
 st.warm(a.k, 0.1)

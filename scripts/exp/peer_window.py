@@ -1,7 +1,8 @@
 """The window an N > 1 run times, rehearsed on one GPU through RCCL loopback:
 with peers every run() primes the ghost ring (a collective decision), so a
 call of n super-steps used to issue n + 1 exchanges (prime + one after every
-pass); it now ends on a bare pass (n exchanges). MXS_PEER_SCHEDULE makes a
+pass); it now ends on a bare pass (n exchanges); peer_halo_last: the interior-first schedule (each
+super-step's own halo exchanged under its core chunks). MXS_PEER_SCHEDULE makes a
 1-rank loopback solver follow the peers' schedule (1 = bare last pass, 2 = the
 old n + 1 form). Interleaved window by window, timed as bench.py does.
 
@@ -28,8 +29,10 @@ p.add_argument("--out", default=None)
 a = p.parse_args()
 w, h = (int(x) for x in a.tile.split("x"))
 ctx = init(backend="gloo", device="cuda")
-confs = {"fused": ({}, None), "loopback_1rank": (dict(loopback=True), None),
-         "peer_n_plus_1": (dict(loopback=True), "2"), "peer_bare_tail": (dict(loopback=True), "1")}
+confs = {"fused": ({}, None), "loopback_1rank": (dict(loopback=True, frame_overlap=False), None),
+         "peer_n_plus_1": (dict(loopback=True, frame_overlap=False), "2"),
+         "peer_bare_tail": (dict(loopback=True, frame_overlap=False), "1"),
+         "peer_halo_last": (dict(loopback=True, frame_overlap=False, halo_last=True), "1")}
 sts = {}
 for name, (kw, env) in confs.items():
     if env is None:
@@ -63,7 +66,8 @@ for K in a.k:
              "median_gcells_per_s": round(w * h * K / (v[len(v) // 2] * 1e-3) / 1e9, 1),
              "exchanges_per_call": int(st.solver.last_run_exchanges()),
              "super_steps": [list(b) for b in st.solver.last_run_blocks()],
-             "frame_choice": list(st.solver.frame_choice())}
+             "runs_schedule": ("halo-last" if st.solver.halo_last(20) else
+                               ("frame" if st.solver.frame_overlap(20) else "serial"))}
         recs.append(r)
         print(json.dumps(r), flush=True)
 if a.out:

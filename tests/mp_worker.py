@@ -86,7 +86,8 @@ def task_gpu_solver(args):
                         dtype=args.get("dtype", "f32"), seed=args.get("seed", 5), backend=args.get("backend", "auto"),
                         overlap=args.get("overlap", True), graph=args.get("graph", True),
                         time_block=args.get("time_block", 12), direct_halo=args.get("direct", None),
-                        sum_form=args.get("sum_form", True), frame_overlap=args.get("frame_overlap", None))
+                        sum_form=args.get("sum_form", True), frame_overlap=args.get("frame_overlap", None),
+                        halo_last=args.get("halo_last", False))
     st = Stencil2D(cfg, ctx)
     if args.get("prepare"):
         st.prepare(args["prepare"])

@@ -97,3 +97,42 @@ def test_frame_schedule_raises_frame_rows_to_fit():
     assert d["check"] == "" and d["signals"] <= 64 and d["frame_rows"] > 64
     with pytest.raises(ValueError, match="frame chunks"):
         C.frame_schedule(200, 1000, 64, 47, 0, 8)
+
+
+def _ghost(groups):
+    return [1] + [0] * (groups - 2) + [1] if groups > 1 else [1]
+
+
+@pytest.mark.parametrize("groups,rows,fill", [(18, 8192, 40), (18, 16384, 52), (36, 16384, 66), (9, 8192, 40),
+                                             (5, 2048, 47), (3, 300, 40)])
+@pytest.mark.parametrize("outer", [0, 16])
+def test_halo_last_schedule_covers_and_keeps_inner_in_the_core(groups, rows, fill, outer):
+    """Interior-first (halo-last) pass: inner and outer chunk lists together
+    cover every (group, row) once; no inner chunk reads the ghost ring (edge
+    groups and rows within S of the top / bottom are outer)."""
+    d = C.halo_last_schedule(groups, rows, 256, fill, 20, _ghost(groups), outer)
+    assert d["check"] == ""
+    assert len(d["inner"]) + len(d["outer"]) == 256
+    if outer:
+        assert len(d["outer"]) == outer
+
+
+def test_halo_last_schedule_8gpu_tile_balance():
+    """The 8-GPU tile (18 groups x 8192 rows, S = 20): the automatic outer set is
+    small, the inner set costs at most ~4% more than the one-launch pass, and
+    the outer set, started after the exchange (lead 12%), ends with it."""
+    d = C.halo_last_schedule(18, 8192, 256, 40, 20, _ghost(18))
+    assert 8 <= len(d["outer"]) <= 64
+    assert d["inner_cost"] <= 1.04 * d["serial_cost"]
+    assert d["outer_cost"] + 0.12 * d["serial_cost"] <= 1.04 * d["inner_cost"]
+
+
+def test_halo_last_schedule_xcd_granule():
+    """Both launches in multiples of the 8 XCDs (the solver's setting)."""
+    d = C.halo_last_schedule(18, 8192, 256, 40, 20, _ghost(18), granule=8)
+    assert d["check"] == "" and len(d["outer"]) % 8 == 0 and len(d["inner"]) % 8 == 0
+
+
+def test_halo_last_schedule_refuses_without_interior():
+    with pytest.raises(ValueError, match="no interior"):
+        C.halo_last_schedule(2, 1000, 256, 40, 20, [1, 1])

@@ -2,7 +2,8 @@
 the 8-GPU tile (16384 x 8192) through RCCL loopback, in the peers' schedule
 (MXS_PEER_SCHEDULE=1: every call primes, the last pass of a call is bare). The
 driver's 20-step window must be exactly one exchange + one 20-level pipeline
-pass, and the record must say so."""
+pass (serial, or the interior-first opening when prepare() measured it
+faster), and the record must say so."""
 import json
 import os
 import subprocess
@@ -29,6 +30,9 @@ def test_bench_8gpu_tile_window_through_loopback(gpu):
     assert ex["timed_super_steps"] == [[20, 1]]
     assert ex["timed_exchanges"] == 1  # the priming exchange; the pass is bare
     assert ex["stencil_kernel"] == "stream_pipe_sum" and ex["sum_form_used"] is True
-    assert ex["schedule_choice"]["chosen"] in ("serial", "frame")
+    sc = ex["schedule_choice"]
+    assert sc["chosen"] in ("serial", "frame") and sc["opening"] in ("serial", "halo-last")
+    # The window is the call's opening super-step: interior-first when measured faster.
+    assert ex["halo_last"] == (sc["opening"] == "halo-last")
     # 16384 x 8192 x 20 cell-updates: one pass (~0.25 ms) + one loopback exchange.
     assert d["value"] > 5000, d

@@ -218,9 +218,13 @@ def test_auto_schedule_choice_is_recorded_and_exact(gpu):
     assert auto.solver.frame_choice()[0] == ""
     auto.run(20)
     auto.prepare(20)
-    choice, serial_ms, frame_ms = auto.solver.frame_choice()
-    assert choice in ("serial", "frame") and serial_ms > 0 and frame_ms > 0
-    assert (choice == "frame") == (frame_ms < serial_ms) == auto.solver.frame_overlap(20)
+    t = auto.solver.schedule_times()
+    choice, opening = t["chosen"], t["opening"]
+    assert choice in ("serial", "frame") and t["serial_ms"] > 0 and t["frame_first_ms"] > 0
+    assert opening in ("serial", "halo-last") and t["opening_serial_ms"] > 0 and t["opening_halo_last_ms"] > 0
+    assert (choice == "frame") == (t["frame_first_ms"] < t["serial_ms"]) == auto.solver.frame_overlap(20)
+    assert (opening == "halo-last") == (t["opening_halo_last_ms"] < t["opening_serial_ms"]) == auto.solver.halo_last(20)
+    assert choice == auto.solver.frame_choice()[0]
     auto.run(40)
     auto.synchronize()
     serial = Stencil2D(StencilConfig(frame_overlap=False, **kw))
@@ -247,6 +251,77 @@ def test_peer_schedule_bare_last_pass_bitwise(gpu, monkeypatch, frame, runs):
         assert a.solver.last_run_exchanges() == sum(c for _, c in blocks), (n, blocks)
         b.run(n)
         assert b.solver.last_run_exchanges() <= sum(c for _, c in b.last_run_blocks()) + 1
+    a.synchronize()
+    b.synchronize()
+    assert torch.equal(a.core_view(), b.core_view())
+
+
+@pytest.mark.parametrize("w,h,dtype,S,runs", [
+    (16384, 8192, "f32", 20, (20,)),        # the 8-GPU tile, the driver's 20-step window: one pass
+    (16384, 8192, "f32", 20, (40, 20)),     # three passes over two calls
+    (32768, 16384, "f32", 20, (20,)),       # the 2-GPU tile
+    (4096, 2048, "f32", 24, (48,)),         # S = 24 (12 + 12)
+    (4000, 1536, "f32", 24, (24, 24)),      # ragged last group
+    (4096, 2048, "f64", 16, (32,)),         # fp64 wide lanes, 8 + 8
+])
+@pytest.mark.parametrize("sum_form", [True, False])
+def test_halo_last_bitwise_vs_serial(gpu, monkeypatch, w, h, dtype, S, runs, sum_form):
+    """Interior-first opening (the call's priming exchange runs under the chunks
+    that read only core cells, the ghost-ring chunks after it on the CUs left
+    free; the call's later super-steps serial), in the peers' schedule, where
+    every call opens with a priming exchange: only the order of the work
+    changes, so the field is bitwise the serial schedule's; one exchange per
+    super-step."""
+    monkeypatch.setenv("MXS_PEER_SCHEDULE", "1")
+    a = _loopback(w, h, dtype, seed=w + h + 1, sum_form=sum_form, frame_overlap=False, halo_last=True,
+                  time_block=S)
+    monkeypatch.delenv("MXS_PEER_SCHEDULE")
+    b = _loopback(w, h, dtype, seed=w + h + 1, sum_form=sum_form, frame_overlap=False, time_block=S)
+    assert a.solver.halo_last(S) and not a.solver.frame_overlap(S) and not b.solver.halo_last(S)
+    assert "interior-first" in a.halo_mode()
+    for n in runs:
+        a.run(n)
+        # One super-step: the interior-first pair of launches; more: the last is the serial bare pass.
+        want = _frame_kernel(sum_form) if n == S else ("stream_pipe_sum" if sum_form else "stream_pipe")
+        assert hip().last_stencil_dispatch() == want
+        assert a.last_run_blocks() == [(S, n // S)]
+        assert a.solver.last_run_exchanges() == n // S
+        b.run(n)
+    a.synchronize()
+    b.synchronize()
+    assert torch.equal(a.core_view(), b.core_view())
+
+
+@pytest.mark.parametrize("runs", [(20,), (60, 20), (40, 7)])
+def test_halo_last_peer_schedule_and_mixed_groups(gpu, monkeypatch, runs):
+    """The interior-first schedule under the peers' rules (MXS_PEER_SCHEDULE=1),
+    including calls whose second super-step group has no interior-first form
+    (40 + 7: S = 7 runs serially after it): bitwise the serial field, one
+    exchange per super-step."""
+    monkeypatch.setenv("MXS_PEER_SCHEDULE", "1")
+    a = _loopback(16384, 8192, seed=78, frame_overlap=False, halo_last=True, time_block=20)
+    monkeypatch.delenv("MXS_PEER_SCHEDULE")
+    b = _loopback(16384, 8192, seed=78, frame_overlap=False, time_block=20)
+    for n in runs:
+        a.run(n)
+        assert a.solver.last_run_exchanges() == sum(c for _, c in a.last_run_blocks())
+        b.run(n)
+    a.synchronize()
+    b.synchronize()
+    assert torch.equal(a.core_view(), b.core_view())
+
+
+def test_halo_last_warm_prepare_keep_the_state(gpu):
+    """prepare() launches the interior-first opening into the scratch buffer
+    (cur -> nxt, cur's ring re-exchanged with the same values), warm() the
+    steady passes: the field is unchanged."""
+    a = _loopback(16384, 8192, seed=79, frame_overlap=False, halo_last=True, time_block=20)
+    b = _loopback(16384, 8192, seed=79, frame_overlap=False, time_block=20)
+    a.run(20)
+    a.prepare(20)
+    assert a.warm(20, 0.01) >= 1
+    a.run(20)
+    b.run(40)
     a.synchronize()
     b.synchronize()
     assert torch.equal(a.core_view(), b.core_view())

@@ -44,21 +44,23 @@ def test_pingpong_two_gpus(gpu, transport, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("n,dims", [g for g in GRIDS if g[0] <= NGPU and g[0] >= 2])
-@pytest.mark.parametrize("frame", [False, True, None])
+@pytest.mark.parametrize("frame", [False, True, None, "halo-last"])
 def test_production_depth_schedules_one_rank_per_gpu(gpu, n, dims, frame):
     """The bench's multi-GPU path at its depth (S = 20 pipeline, 2048 x 1024
     tiles per rank): serial post-exchange, frame-first overlap and the measured
-    auto choice (prepare) all give the per-step result of the one-step loop."""
+    interior-first (halo-last) overlap and the measured auto choice (prepare)
+    all give the per-step result of the one-step loop."""
     r, c = (int(x) for x in dims.split("x"))
     w, h, iters, seed = 2048 * c, 1024 * r, 60, 13
     res = run_ranks("gpu_solver", n, {"w": w, "h": h, "dims": dims, "iters": iters, "seed": seed, "backend": "rccl",
-                                      "time_block": 20, "overlap": False, "sum_form": False, "frame_overlap": frame,
-                                      "prepare": 20}, gpu=True, timeout=900)
+                                      "time_block": 20, "overlap": False, "sum_form": False,
+                                      "frame_overlap": False if frame == "halo-last" else frame,
+                                      "halo_last": frame == "halo-last", "prepare": 20}, gpu=True, timeout=900)
     assert all(x["native"] and x["time_block"] == 20 for x in res)
     if frame is True:
         assert all(x["frame"] for x in res)
     if frame is None:
-        assert all(x["choice"][0] in ("serial", "frame") for x in res)
+        assert all(x["choice"][0] in ("serial", "frame", "halo-last") for x in res)
     got = torch.tensor(res[0]["grid"], dtype=torch.float64)
     ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), iters).double()
     assert (got - ref).abs().max().item() < 1e-5
