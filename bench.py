@@ -6,7 +6,9 @@ GB/s + µs latency". Config: the BASELINE 8-GPU problem — a 32768 x 32768 fp32
 periodic grid, 5-point Jacobi, decomposed over a Cartesian process grid
 (MPI_Dims_create order: 1, 2 rows x 1 col, 2 x 2, 4 rows x 2 cols), halo
 exchange by native RCCL point-to-point over xGMI (pack -> per-peer send/recv ->
-unpack, captured in a hipGraph with the update). The global grid is fixed as N
+unpack). With peers a call of n super-steps issues n exchanges: its opening
+one (run interior-first, under the core chunks, when prepare() measured that
+faster), one after every pass but the last. The global grid is fixed as N
 grows (strong scaling). Random-init synthetic data (deterministic per global
 cell). At N = 1 the only neighbour is the rank itself: the self-exchange is
 fused into the kernel's periodic addressing (no copy at all), and the record
