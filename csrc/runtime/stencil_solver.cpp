@@ -718,7 +718,8 @@ void StencilSolver<T>::prepare(int iters) {
   for (const Group& g : gr) {
     if (g.count <= 0) continue;
     (void)frame_pass(g.S, true);
-    if (HaloLastPass* hl = halo_last_pass(g.S, true); hl && std::find(warmed_.begin(), warmed_.end(), g.S) == warmed_.end()) {
+    const bool cold = std::find(warmed_.begin(), warmed_.end(), g.S) == warmed_.end();
+    if (HaloLastPass* hl = halo_last_pass(g.S, true); hl && cold) {
       enqueue_halo_last(cur_, nxt_, hl);  // cur -> nxt (scratch), cur's ring re-exchanged: state unchanged
       join_side();
     }
