@@ -224,6 +224,13 @@ class StencilSolver {
   const std::string& opening_choice() const { return opening_choice_; }
   double opening_serial_ms() const { return opening_ms_[0]; }
   double opening_halo_last_ms() const { return opening_ms_[1]; }
+  // Workgroups of the outer (ghost-ring) launch of the interior-first opening
+  // at depth S (0: none built).
+  int halo_last_outer_wgs(int S) const {
+    for (const auto& h : halo_lasts_)
+      if (h->S == S) return h->sched.outer.blocks;
+    return 0;
+  }
   // The auto choice: "" before prepare() decided, else "frame" or "serial" and
   // the median times (ms per super-step) of both.
   const std::string& frame_choice() const { return frame_choice_; }
@@ -290,6 +297,7 @@ class StencilSolver {
     DeviceBuffer<kernels::FrameChunk> inner_table, outer_table;
   };
   HaloLastPass* halo_last_pass(int S, bool build);  // nullptr: not in use / no form for S
+  std::unique_ptr<HaloLastPass> build_halo_last(int S, int outer_wgs);  // nullptr: no form for S
   void enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl);
   bool halo_last_on_ = false;                // a call's opening super-step runs interior-first
   std::vector<std::unique_ptr<HaloLastPass>> halo_lasts_;

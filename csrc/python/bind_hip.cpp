@@ -457,6 +457,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
                d["opening"] = s.opening_choice();
                d["opening_serial_ms"] = s.opening_serial_ms();
                d["opening_halo_last_ms"] = s.opening_halo_last_ms();
+               d["opening_outer_wgs"] = s.halo_last_outer_wgs(s.time_block());
                return d;
              });
            },

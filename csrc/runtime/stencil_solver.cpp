@@ -1,6 +1,7 @@
 #include "mxs/runtime/stencil_solver.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdlib>
 #include <limits>
@@ -12,6 +13,12 @@
 #include "mxs/core/trace.hpp"
 
 namespace mxs {
+
+namespace {
+// Workgroups are dealt round-robin over the XCDs: both launches of an
+// interior-first pass are sized in multiples of this (kernels::make_halo_last_schedule).
+constexpr int kXcds = 8;
+}  // namespace
 
 template <typename T>
 StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGeom& tile, T* buf_a, T* buf_b,
@@ -528,6 +535,24 @@ void StencilSolver<T>::choose_schedule(int S) {
   HaloLastPass* hl = halo_last_pass(S, true);
   halo_last_on_ = false;
   if (!has_frame && !hl) return;  // nothing to choose at this depth (decided at the next prepare)
+  // Interior-first candidates: the modelled outer set and one XCD step either
+  // side. Where the outer workgroups land decides the opening (36 of them left
+  // some XCD a CU short; on one box 32 / 40 / 48 measured 0.296 / 0.259 /
+  // 0.431 ms against 0.269 serial, profiles/r03_halolast), so it is measured.
+  std::vector<std::unique_ptr<HaloLastPass>> alt;
+  const bool env_wgs = std::getenv("MXS_HALO_LAST_WGS") != nullptr;
+  if (hl && !env_wgs) {
+    const int m = hl->sched.outer.blocks;
+    for (int d : {-kXcds, kXcds}) {
+      const int k = m + d;
+      if (k >= 32 && k < hl->inner_shape.blocks + m) {
+        if (auto h = build_halo_last(S, k)) alt.push_back(std::move(h));
+      }
+    }
+  }
+  std::vector<HaloLastPass*> cands;
+  if (hl) cands.push_back(hl);
+  for (auto& h : alt) cands.push_back(h.get());
   if (!ghost_fresh_) {
     ex_->exchange(cur_, main_.get());
     ghost_fresh_ = true;
@@ -537,8 +562,24 @@ void StencilSolver<T>::choose_schedule(int S) {
   // vs interior-first, one super-step from drained streams, as a short timed
   // window sees it. Alternating rounds, medians; every launch is state-preserving
   // (cur -> nxt, cur's ring re-exchanged with the same values).
-  std::vector<double> t[4];
+  std::vector<double> t[2], t_open_serial;
+  std::vector<std::vector<double>> t_open(3);
   Event e0(true), e1(true);
+  // Opening candidates are timed the way a caller's window sees them: host
+  // clock from drained streams to both drained again (an event recorded on main
+  // before the opening would itself force the fork the opening skips).
+  auto timed_host = [&](auto&& enqueue) {
+    join_side();
+    main_.sync();
+    side_.sync();
+    side_pending_ = false;
+    const auto t0 = std::chrono::steady_clock::now();
+    enqueue();
+    main_.spin_sync();
+    side_.spin_sync();
+    side_pending_ = false;
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  };
   auto timed = [&](auto&& enqueue) {
     join_side();
     main_.sync();
@@ -562,21 +603,21 @@ void StencilSolver<T>::choose_schedule(int S) {
       if (rep > 0 && (mode == 0 || has_frame)) t[mode].push_back(ms / 2.0);  // round 0 warms every shape
     }
     frame_on_ = false;
-    const double serial_open = timed([&] {
+    const double serial_open = timed_host([&] {
       ex_->exchange(cur_, main_.get());
       enqueue_bare_pass(cur_, nxt_, S);
     });
-    const double hl_open = timed([&] {
-      if (hl) {
-        enqueue_halo_last(cur_, nxt_, hl);
-      } else {
-        ex_->exchange(cur_, main_.get());
-        enqueue_bare_pass(cur_, nxt_, S);
-      }
-    });
-    if (rep > 0) {
-      t[2].push_back(serial_open);
-      if (hl) t[3].push_back(hl_open);
+    if (rep > 0) t_open_serial.push_back(serial_open);
+    for (size_t c = 0; c < 3; ++c) {  // always 3 openings: the same exchanges on every rank
+      const double ms = timed_host([&] {
+        if (c < cands.size()) {
+          enqueue_halo_last(cur_, nxt_, cands[c]);
+        } else {
+          ex_->exchange(cur_, main_.get());
+          enqueue_bare_pass(cur_, nxt_, S);
+        }
+      });
+      if (rep > 0 && c < cands.size()) t_open[c].push_back(ms);
     }
   }
   auto median = [](std::vector<double>& v) {
@@ -586,29 +627,42 @@ void StencilSolver<T>::choose_schedule(int S) {
   };
   choice_ms_[0] = median(t[0]);
   choice_ms_[1] = median(t[1]);
-  opening_ms_[0] = median(t[2]);
-  opening_ms_[1] = median(t[3]);
+  opening_ms_[0] = median(t_open_serial);
+  size_t best = 0;
+  for (size_t c = 0; c < cands.size(); ++c)
+    if (median(t_open[c]) < median(t_open[best])) best = c;
+  opening_ms_[1] = cands.empty() ? 0.0 : median(t_open[best]);
+  if (best > 0) {  // keep the measured best outer set for S
+    for (auto& h : halo_lasts_)
+      if (h->S == S) h = std::move(alt[best - 1]);
+  }
   frame_on_ = has_frame && choice_ms_[1] < choice_ms_[0];
-  halo_last_on_ = hl && opening_ms_[1] < opening_ms_[0];
+  halo_last_on_ = !cands.empty() && opening_ms_[1] < opening_ms_[0];
   frame_choice_ = frame_on_ ? "frame" : "serial";
   opening_choice_ = halo_last_on_ ? "halo-last" : "serial";
 }
 
 // Interior-first pass of depth S (built on first use while the schedule is on).
-// Workgroups are dealt round-robin over the XCDs: both launches of the pass are
-// sized in multiples of this (kernels::make_halo_last_schedule).
-constexpr int kXcds = 8;
 template <typename T>
 typename StencilSolver<T>::HaloLastPass* StencilSolver<T>::halo_last_pass(int S, bool build) {
   if (!halo_last_on_) return nullptr;
   for (auto& h : halo_lasts_)
     if (h->S == S) return h.get();
   if (!build || std::find(no_halo_last_.begin(), no_halo_last_.end(), S) != no_halo_last_.end()) return nullptr;
-  kernels::FramePassShape shape;
-  if (!kernels::frame_pass_shape<T>(tile_, S, cfg_.coeffs, &shape) || shape.blocks < 2) {
+  auto hl = build_halo_last(S, 0);
+  if (!hl) {
     no_halo_last_.push_back(S);
     return nullptr;
   }
+  halo_lasts_.push_back(std::move(hl));
+  return halo_lasts_.back().get();
+}
+
+// outer_wgs: 0 = MXS_HALO_LAST_WGS or the schedule's model.
+template <typename T>
+std::unique_ptr<typename StencilSolver<T>::HaloLastPass> StencilSolver<T>::build_halo_last(int S, int outer_wgs) {
+  kernels::FramePassShape shape;
+  if (!kernels::frame_pass_shape<T>(tile_, S, cfg_.coeffs, &shape) || shape.blocks < 2) return nullptr;
   // Groups whose joint windows read ghost columns (all their chunks are outer).
   std::vector<std::uint8_t> ghost(size_t(shape.groups), 0);
   for (index_t g = 0; g < shape.groups; ++g) {
@@ -623,22 +677,18 @@ typename StencilSolver<T>::HaloLastPass* StencilSolver<T>::halo_last_pass(int S,
   hl->S = S;
   try {
     hl->sched = kernels::make_halo_last_schedule(shape.groups, tile_.height, shape.blocks, shape.fill, S, ghost,
-                                                 int(env_num("MXS_HALO_LAST_WGS", 0)),
+                                                 outer_wgs > 0 ? outer_wgs : int(env_num("MXS_HALO_LAST_WGS", 0)),
                                                  env_num("MXS_HALO_LAST_LEAD", 0.12),
                                                  std::int64_t(env_num("MXS_HALO_LAST_ROWS", 0)),
                                                  shape.blocks % kXcds == 0 ? kXcds : 1,
                                                  int(env_num("MXS_HALO_LAST_MIN_WGS", 32)));
   } catch (const std::invalid_argument&) {
-    no_halo_last_.push_back(S);
     return nullptr;
   }
   index_t longest = 0;
   for (const auto* sc : {&hl->sched.inner, &hl->sched.outer})
     for (const auto& c : sc->table) longest = std::max<index_t>(longest, c.r1 - c.r0);
-  if (longest * tile_.pitch * index_t(sizeof(T)) > kernels::kMaxChunkBytes) {
-    no_halo_last_.push_back(S);  // a chunk past the buffer-descriptor range
-    return nullptr;
-  }
+  if (longest * tile_.pitch * index_t(sizeof(T)) > kernels::kMaxChunkBytes) return nullptr;  // past the descriptor range
   hl->inner_shape = shape;
   hl->inner_shape.blocks = hl->sched.inner.blocks;
   hl->outer_shape = shape;
@@ -649,8 +699,7 @@ typename StencilSolver<T>::HaloLastPass* StencilSolver<T>::halo_last_pass(int S,
                           hipMemcpyHostToDevice));
   MXS_HIP_CHECK(hipMemcpy(hl->outer_table.get(), hl->sched.outer.table.data(), hl->outer_table.bytes(),
                           hipMemcpyHostToDevice));
-  halo_lasts_.push_back(std::move(hl));
-  return halo_lasts_.back().get();
+  return hl;
 }
 
 template <typename T>
