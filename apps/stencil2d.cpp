@@ -247,6 +247,8 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
       if (solver) {
         js << ", \"frame_first\": " << (solver->frame_overlap(solver->time_block()) ? "true" : "false");
         if (!solver->frame_choice().empty()) js << ", \"schedule_choice\": \"" << solver->frame_choice() << "\"";
+        js << ", \"interior_first_opening\": " << (solver->halo_last(solver->time_block()) ? "true" : "false");
+        if (!solver->opening_choice().empty()) js << ", \"opening_choice\": \"" << solver->opening_choice() << "\"";
       }
       if (want_sum) js << ", \"checksum\": " << app::fmt(checksum);
       js << app::meta_json(device_description(dev.device)) << "}";

@@ -172,11 +172,11 @@ def test_pingpong_ipc_reference_output(gpu):
     assert r.stdout.startswith("PASSED\nMessage size(MB): 1\nRound-trip time(ms): ")
 
 
-@pytest.mark.parametrize("mode", ["--frame-overlap", "--no-frame-overlap", None])
+@pytest.mark.parametrize("mode", ["--frame-overlap", "--no-frame-overlap", "--halo-last", None])
 def test_stencil_gpu_schedules_at_production_depth(gpu, tmp_path, mode):
     """The app's multi-GPU schedules through RCCL loopback at S = 20 (per-step
-    form): frame-first, serial and the measured choice give the same checksum,
-    bit for bit, and agree with the CPU app."""
+    form): frame-first, serial, the interior-first opening and the measured
+    choice give the same checksum, bit for bit, and agree with the CPU app."""
     args = ["--global", "4096x2048", "--dims", "1x1", "--dtype", "f32", "--iters", "40", "--stencil", "3"]
     extra = ["--loopback", "--time-block", "20", "--no-sum-form", "--no-overlap"] + ([mode] if mode else [])
     g = mpirun(1, "stencil2d", *args, "--checksum", "--warmup", "0", *extra, cwd=tmp_path)
@@ -187,8 +187,10 @@ def test_stencil_gpu_schedules_at_production_depth(gpu, tmp_path, mode):
         assert '"frame_first": true' in js
     elif mode == "--no-frame-overlap":
         assert '"frame_first": false' in js
+    elif mode == "--halo-last":
+        assert '"interior_first_opening": true' in js
     else:
-        assert '"schedule_choice": "' in js
+        assert '"schedule_choice": "' in js and '"opening_choice": "' in js
     ref = mpirun(1, "stencil2d", *args, "--checksum", "--warmup", "0", "--time-block", "1", cwd=tmp_path)
     assert ref.returncode == 0, ref.stderr[-3000:]
     assert _checksum(g.stdout) == _checksum(ref.stdout)
