@@ -83,6 +83,8 @@ class HaloExchanger {
   // Threads per workgroup of the pack / unpack launches (0 = default 256;
   // 64 = one-wave workgroups that run beside a pipeline pass).
   void set_copy_block(int threads) { copy_block_ = threads; }
+  // Workgroups per copy segment (0 = sized from the segments, or MXS_HALO_GRID).
+  void set_copy_grid(int wgs) { copy_grid_ = wgs; }
 
  private:
   HaloPlan plan_;
@@ -92,6 +94,7 @@ class HaloExchanger {
   DeviceBuffer<T> send_, recv_;
   std::unique_ptr<IpcHaloTransport<T>> ipc_;
   int copy_block_ = 0;
+  int copy_grid_ = 0;
 };
 
 }  // namespace mxs

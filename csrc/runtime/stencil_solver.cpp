@@ -735,8 +735,18 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl) {
   kernels::stencil5_frame_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->inner_shape, hl->inner_table.get(),
                                   hl->sched.inner.entries, frame_ctl_.get(), side);
   side_pending_ = true;
-  ex_->set_copy_block(64);  // one-wave copy workgroups fit beside a pipeline workgroup
+  // One-wave copy workgroups sized from the segments (they fit beside the inner
+  // launch's workgroups). MXS_HALO_LAST_COPY_WGS (experiments): 4-wave
+  // workgroups, that many per segment; 4 per segment made the exchange so slow
+  // that the 8-GPU-tile opening took 0.415 ms instead of 0.264.
+  static const int copy_wgs = [] {
+    const char* e = std::getenv("MXS_HALO_LAST_COPY_WGS");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
+  ex_->set_copy_grid(copy_wgs);
   ex_->exchange(cur, m);
+  ex_->set_copy_grid(0);
   kernels::stencil5_frame_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->outer_shape, hl->outer_table.get(),
                                   hl->sched.outer.entries, frame_ctl_.get(), m);
 }
