@@ -15,9 +15,24 @@ def free_port() -> int:
         return s.getsockname()[1]
 
 
+class _PortTaken(RuntimeError):
+    """The rendezvous port was taken between free_port() and the store's bind."""
+
+
 def run_ranks(task: str, nprocs: int, args: dict, timeout: int = 240, gpu: bool = False) -> list[dict]:
     """`gpu=True`: every rank sees the (single) GPU — ranks share it, as in the
-    IPC-backend tests; otherwise GPUs are hidden (CPU / gloo)."""
+    IPC-backend tests; otherwise GPUs are hidden (CPU / gloo). A rendezvous port
+    grabbed by another process before rank 0 binds it (EADDRINUSE: nothing ran
+    yet) is retried with a fresh port."""
+    for _ in range(3):
+        try:
+            return _run_once(task, nprocs, args, timeout, gpu)
+        except _PortTaken:
+            continue
+    return _run_once(task, nprocs, args, timeout, gpu)
+
+
+def _run_once(task, nprocs, args, timeout, gpu):
     port = free_port()
     procs = []
     for r in range(nprocs):
@@ -34,6 +49,8 @@ def run_ranks(task: str, nprocs: int, args: dict, timeout: int = 240, gpu: bool 
         for p in procs:
             out, err = p.communicate(timeout=timeout)
             if p.returncode != 0:
+                if "EADDRINUSE" in err or "address already in use" in err:
+                    raise _PortTaken(err[-500:])
                 raise RuntimeError(f"rank failed rc={p.returncode}\n{err[-3000:]}")
             line = [ln for ln in out.splitlines() if ln.startswith("RESULT ")]
             assert line, f"no result\nstdout={out[-2000:]}\nstderr={err[-2000:]}"
@@ -42,4 +59,9 @@ def run_ranks(task: str, nprocs: int, args: dict, timeout: int = 240, gpu: bool 
         for p in procs:
             if p.poll() is None:
                 p.kill()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                pass
     return sorted(results, key=lambda r: r["rank"])
