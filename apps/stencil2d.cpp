@@ -5,8 +5,9 @@
 // device data moves by one of:
 //   --backend rccl        per-peer ncclSend/ncclRecv over xGMI (default when every
 //                         rank has its own GPU): each pass, then the exchange of its
-//                         output (post-exchange); --frame-overlap runs the exchange
-//                         under a frame-first pass instead (opt-in, docs/PERF.md);
+//                         output (post-exchange); a call's opening super-step runs
+//                         its priming exchange under the core chunks when prepare()
+//                         measured that faster on every rank (--opening);
 //   --backend ipc         HIP IPC: direct writes into the peers' receive buffers,
 //                         device-side ready/free counters, overlap + hipGraph
 //                         (default when ranks share a GPU, where RCCL refuses);
@@ -21,8 +22,8 @@
 // Positional arguments keep the reference contract: [local width (= height) [stencil width]].
 // More options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
 // --iters N, --warmup N, --time-block S (default: measured per tile size and dtype), --no-overlap, --no-graph,
-// --frame-overlap / --no-frame-overlap / --halo-last (default: prepare() times the serial, frame-first and
-// interior-first schedules and keeps the fastest),
+// --opening auto|serial|interior-first (--halo-last = interior-first; default auto: prepare() times the
+// serial and interior-first openings, agrees the worst-rank medians over all ranks and keeps the faster),
 // --no-direct-halo (IPC backend: pack -> put -> unpack instead of the device-initiated push),
 // --c-center C --c-neighbor C (default 0.2 / 0.2), --no-sum-form (keep the per-step evaluation in the
 // time-blocked kernels: bitwise equal to the CPU app; default: sum form when the coefficients are equal),
@@ -91,12 +92,15 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   const double c_center = cli.get_double("c-center", 0.2), c_neighbor = cli.get_double("c-neighbor", 0.2);
   // --no-sum-form: per-step evaluation everywhere (bitwise equal to the CPU app).
   const bool sum_form = !cli.flag("no-sum-form") && c_center == c_neighbor;
-  const int time_block =
+  int time_block =
       (backend == "mpi-staged" || !all_periodic)
           ? 1
           : int(cli.get_int("time-block", iters > 0 && lw >= 64 && lh >= 64
                                               ? kernels::auto_time_block(lw, lh, int(sizeof(T)), sum_form)
                                               : 1));
+  // The time block sets the ghost depth and the exchanges per call: the same on
+  // every rank (an uneven decomposition gives ranks different tile sizes).
+  time_block = -int(env.max_over_ranks(-double(time_block)));
   const TileGeom g = TileGeom::aligned(lw, lh, std::max(sw / 2, time_block), std::max(sh / 2, time_block),
                                        int(sizeof(T)));
   std::unique_ptr<RcclComm> comm;
@@ -108,7 +112,9 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
 
   SolverConfig cfg;
   cfg.backend = backend == "rccl" ? HaloBackend::Rccl : backend == "ipc" ? HaloBackend::Ipc : HaloBackend::Local;
-  if (backend == "ipc") cfg.bootstrap = [](const std::string& b) { return mpi_allgather_bytes(MPI_COMM_WORLD, b); };
+  // Host allgather: the IPC backend's set-up and the solver's collective
+  // agreements (time block, opening, sum-form range) without RCCL.
+  cfg.bootstrap = [](const std::string& b) { return mpi_allgather_bytes(MPI_COMM_WORLD, b); };
   // IPC: device-initiated halo (each pass pushes its edge bands into the
   // neighbours' tiles) unless --no-direct-halo asks for pack -> put -> unpack.
   cfg.direct_halo = backend == "ipc" && !cli.flag("no-direct-halo");
@@ -123,9 +129,10 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   kernels::set_gpu_share(shared_gpu ? std::max(1, env.local_size() / std::max(1, dev.devices_used)) : 1);
   cfg.overlap = cli.flag("overlap") || (!cli.flag("no-overlap") && !shared_gpu && time_block == 1);
   cfg.use_graph = !cli.flag("no-graph");
-  cfg.frame_overlap = cli.flag("frame-overlap");
-  cfg.frame_auto = !cli.flag("no-frame-overlap");
-  cfg.halo_last = cli.flag("halo-last");
+  const std::string opening = cli.flag("halo-last") ? "interior-first" : cli.get("opening", "auto");
+  MXS_CHECK(opening == "auto" || opening == "serial" || opening == "interior-first",
+            "--opening must be auto, serial or interior-first, got " << opening);
+  cfg.opening = opening == "serial" ? Opening::Serial : opening == "interior-first" ? Opening::InteriorFirst : Opening::Auto;
   cfg.loopback_self = loopback;
   cfg.coeffs = {c_center, c_neighbor, sum_form};
   cfg.time_block = time_block;
@@ -245,10 +252,9 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
          << "\", \"graph\": \"" << (solver ? solver->graph_status() : std::string("n/a"))
          << "\", \"time_block\": " << time_block << ", \"iters\": " << iters;
       if (solver) {
-        js << ", \"frame_first\": " << (solver->frame_overlap(solver->time_block()) ? "true" : "false");
-        if (!solver->frame_choice().empty()) js << ", \"schedule_choice\": \"" << solver->frame_choice() << "\"";
         js << ", \"interior_first_opening\": " << (solver->halo_last(solver->time_block()) ? "true" : "false");
         if (!solver->opening_choice().empty()) js << ", \"opening_choice\": \"" << solver->opening_choice() << "\"";
+        js << ", \"last_opening\": \"" << solver->last_run_opening() << "\"";
       }
       if (want_sum) js << ", \"checksum\": " << app::fmt(checksum);
       js << app::meta_json(device_description(dev.device)) << "}";
@@ -269,7 +275,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
 int main(int argc, char** argv) {
   MpiEnv env(&argc, &argv);
   Cli cli(argc, argv, {"dump", "no-dump", "non-periodic", "strict-square", "no-overlap", "overlap", "no-graph",
-                       "loopback", "pageable", "checksum", "frame-overlap", "no-frame-overlap", "halo-last", "no-sum-form",
+                       "loopback", "pageable", "checksum", "halo-last", "no-sum-form",
                        "no-direct-halo"});
   comm_timeout() = cli.get_double("comm-timeout", 300.0);
   const DeviceBinding dev = bind_device(env, cli.get("bind", "bunch"));

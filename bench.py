@@ -42,12 +42,24 @@ one of the K steps runs in full inside the window.
     python bench.py                       # N=1
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
 
+Self-description (extras): the executed super-steps and exchanges (``halo``,
+``timed_super_steps``, ``timed_exchanges``), the opening prepare() chose and
+the worst-rank timings it agreed on (``schedule_choice``), the RCCL
+communicator's own rank count and every rank's device (``rccl_ranks``,
+``rank_devices``), an event-timed phase breakdown of one untimed replica of the
+window (``window_phases``: pack / RCCL / unpack / passes / host overhead), and
+every MXS_* / NCCL_* / RCCL_* / HIP_* / HSA_* variable that was set (``env``).
+An experiments build (-DMXS_EXPERIMENTS=ON, where MXS_* tuning knobs take effect)
+with such a knob set refuses to report a headline.
+
 Extras (not the headline number, BASELINE configs 2/3/5):
   * every N: the parallel dot product, 2^30 fp64 split over the N ranks,
     single-pass device reduction + RCCL all-reduce of the partial (GB/s read);
   * N = 1: 8192^2 fp32 and fp64 single-GPU stencil rates;
   * N >= 2: GPU-GPU ping-pong between ranks 0 and 1, 8 B - 256 MiB, RCCL
-    blocking / async / overlap (device-initiated HIP IPC with --pingpong-ipc). Summary
+    blocking / async / overlap / bidir; the device-initiated HIP IPC transport
+    only with --pingpong-ipc (opt-in: its cross-GPU coherence is verified only by
+    the multi-GPU tests, and a fault there would take the record with it). Summary
     (latency at 8 B, GB/s at 1 MiB / 16 MiB / 256 MiB) in extras, the full
     sweep in gpurun_out/bench_pingpong_n<N>.json.
 """
@@ -65,8 +77,28 @@ PINGPONG_SIZES = [8 << i for i in range(26)]  # 8 B .. 256 MiB
 SUMMARY_SIZES = {"1MiB": 1 << 20, "16MiB": 16 << 20, "256MiB": 256 << 20}
 
 
+ENV_PREFIXES = ("MXS_", "NCCL_", "RCCL_", "HIP_", "HSA_", "GPU_", "ROCR_", "TORCH_NCCL_")
+# MXS_* variables a release build reads (not tuning knobs): recorded, allowed.
+MXS_RUNTIME_ENV = {"MXS_IPC_CROSS_DEVICE", "MXS_BUILD_DIR"}
+
+
 def _ms(x):
     return round(x * 1e3, 4)
+
+
+def env_record() -> dict:
+    """Every runtime-relevant variable that is set (MXS_*, NCCL_*, RCCL_*, HIP_*, HSA_*, ...)."""
+    return {k: v for k, v in sorted(os.environ.items()) if k.startswith(ENV_PREFIXES)}
+
+
+def refuse_reason(experiments_build: bool, env: dict) -> str | None:
+    """Why the headline must not be reported, or None. An experiments build
+    honours the MXS_* tuning knobs (pass layouts, copy grids, schedule probes):
+    with one set the run is an experiment, not the framework's result."""
+    knobs = sorted(k for k in env if k.startswith("MXS_") and k not in MXS_RUNTIME_ENV)
+    if experiments_build and knobs:
+        return f"experiments build with tuning knobs set: {', '.join(knobs)}"
+    return None
 
 
 def _sync():
@@ -115,8 +147,18 @@ def dot_extras(ctx, extras: dict, n_global: int) -> None:
     gpu = torch.cuda.is_available()
     dp = DotProduct(ctx, n_global, "f64", "single-pass", "rccl" if gpu else "torch")
     value, dt = dp.timed(reps=20, warmup=3)
+    br = dp.breakdown(reps=10)
     tag = "dot_2p30_f64" if n_global == 2**30 else f"dot_{n_global}_f64"
     if ctx.is_root:
+        if br:
+            # Event-timed on the stream, median per rep: the local reduction
+            # (counter reset + single-pass kernel) and, at N > 1, the RCCL
+            # all-reduce of the partial. The wall figure above also carries the
+            # host's per-rep launches between them.
+            extras[f"{tag}_kernel_us"] = round(br["kernel_us"], 2)
+            if n > 1:
+                extras[f"{tag}_allreduce_us"] = round(br["allreduce_us"], 2)
+            extras[f"{tag}_kernel_tbytes_per_s_per_gpu"] = round(dp.bytes_read / n / (br["kernel_us"] * 1e-6) / 1e12, 3)
         extras[f"{tag}_us"] = round(dt * 1e6, 2)
         extras[f"{tag}_gbytes_per_s"] = round(dp.bytes_read / dt / 1e9, 1)
         extras[f"{tag}_per_gpu_tbytes_per_s"] = round(dp.bytes_read / dt / 1e12 / n, 3)
@@ -175,6 +217,11 @@ def pingpong_extras(ctx, extras: dict, max_bytes: int, with_ipc: bool = False) -
             alone = rec.get("compute_alone_us", 0.0) + rec.get("comm_alone_us", 0.0)
             if rec.get("overlapped_us"):
                 extras[f"{key}_256MiB_overlap_speedup"] = round(alone / rec["overlapped_us"], 3)
+    if not with_ipc:
+        extras["pingpong_ipc"] = ("not run: the device-initiated HIP IPC transport across GPUs is opt-in "
+                                  "(--pingpong-ipc); RCCL figures only")
+    lat = {t: extras.get(f"pingpong_{t}_8B_latency_us") for t in ("rccl_async", "ipc_device")}
+    extras["pingpong_8B_latency_us"] = {k: v for k, v in lat.items() if v is not None}
     extras["pingpong_verified"] = all(r.get("passed", False) for r in sweep)
     path = os.path.join("gpurun_out", f"bench_pingpong_n{ctx.world_size}.json")
     try:
@@ -205,16 +252,16 @@ def main(argv=None) -> int:
     p.add_argument("--no-fuse-periodic", action="store_true",
                    help="N = 1: explicit self-exchange (copies into the ghost ring) + the ghost-ring pass instead "
                         "of the wrap-around addressing")
-    p.add_argument("--frame-overlap", action="store_true",
-                   help="multi-GPU: always exchange the next halo under the pass (frame-first overlap); default: "
-                        "prepare() times it against the serial schedule and keeps the faster (docs/PERF.md)")
-    p.add_argument("--no-frame-overlap", action="store_true", help="multi-GPU: always the serial schedule")
-    p.add_argument("--halo-last", action="store_true",
-                   help="multi-GPU: always the interior-first schedule (each super-step's halo exchange under the "
-                        "chunks that read only core cells); default: one of prepare()'s timed candidates")
-    p.add_argument("--overlap", action="store_true", help="force the interior/exchange overlap schedule")
+    p.add_argument("--opening", default="auto", choices=["auto", "serial", "interior-first"],
+                   help="multi-GPU: a call's opening super-step (its priming exchange) serial, or interior-first "
+                        "(under the chunks that read only core cells); auto: prepare() times both on every rank "
+                        "and all ranks adopt the same choice")
+    p.add_argument("--overlap", action="store_true", help="force the thin-strip interior/exchange overlap schedule")
     p.add_argument("--loopback", action="store_true",
                    help="1 GPU: route the self-neighbour halos through RCCL (exercises the multi-GPU schedule)")
+    p.add_argument("--rehearse-peers", action="store_true",
+                   help="with --loopback: follow the peers' schedule (every call primes, its last pass is bare, "
+                        "the opening is chosen as with peers): one GPU rehearses an N-GPU window")
     p.add_argument("--backend", default="auto", choices=["auto", "rccl", "ipc", "local", "torch"])
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-extras", action="store_true")
@@ -233,6 +280,16 @@ def main(argv=None) -> int:
     from cuda_mpi_scratch_amd.parallel import choose_dims, init as dist_init
 
     gpu = torch.cuda.is_available()
+    env = env_record()
+    if gpu:
+        from cuda_mpi_scratch_amd import hip
+
+        why = refuse_reason(bool(hip().experiments_build()), env)
+        if why:
+            print(f"bench.py: refusing to report a headline: {why}", file=sys.stderr)
+            return 3
+    if args.rehearse_peers and not args.loopback:
+        p.error("--rehearse-peers needs --loopback")
     ctx = dist_init(backend="nccl" if gpu else "gloo", timeout_s=max(60, int(args.comm_timeout) + 60))
     n = ctx.world_size
     if n != args.gpus and ctx.is_root:
@@ -253,14 +310,13 @@ def main(argv=None) -> int:
                         overlap=False if args.no_overlap else (True if args.overlap else None),
                         graph=not args.no_graph,
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback,
-                        sum_form=not args.no_sum_form, frame_overlap=(True if args.frame_overlap else (False if args.no_frame_overlap else None)),
-                        halo_last=args.halo_last,
+                        sum_form=not args.no_sum_form, opening=args.opening, rehearse_peers=args.rehearse_peers,
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3)
     timed_blocks = st.last_run_blocks()  # the super-steps the timed window executed
     value = st.cells_per_step * args.steps / dt / 1e9
-    halo = st.halo_mode()
+    halo = st.halo_mode()  # what the timed run() executed
     exchange = ("none: 1x1 periodic self-exchange fused into the kernel addressing"
                 if st.solver is not None and st.solver.fused_periodic()
                 else f"{st.backend} point-to-point per neighbour")
@@ -276,24 +332,39 @@ def main(argv=None) -> int:
                                    if sum_used else "per step: fma(c_n, (n+s)+(w+e), c_c*c)"),
                     "clock_warmup_ms": args.clock_warmup_ms,
                     "tile": f"{st.decomp.width}x{st.decomp.height}",
-                    "process_grid": f"{rows} rows x {cols} cols of ranks"}
+                    "process_grid": f"{rows} rows x {cols} cols of ranks",
+                    "env": env}
     if gpu:
         from cuda_mpi_scratch_amd import hip
 
-        extras["stencil_kernel"] = hip().last_stencil_dispatch()
-        extras["pipe_joint_windows"] = bool(hip().pipe_joint())  # MXS_PIPE_JOINT=0 runs the per-strip layout
-        # Level order of the last pipeline pass (bottom-up on short chunks, MXS_PIPE_LAG1=0 disables it).
-        extras["pipe_level_order"] = "bottom-up" if hip().last_pipe_lag1() else "top-down"
-        extras["pipe_balanced_shares"] = bool(hip().pipe_balanced())  # MXS_PIPE_BALANCED=0: equal row shares
-        if st.solver is not None and not st.solver.fused_periodic():
-            # Halo exchanges inside the timed window: one per super-step (with
-            # peers the call primes and ends on a bare pass).
-            extras["timed_exchanges"] = int(st.solver.last_run_exchanges())
-            extras["frame_overlap"] = bool(timed_blocks and st.solver.frame_overlap(timed_blocks[0][0]))
-            extras["halo_last"] = bool(timed_blocks and st.solver.halo_last(timed_blocks[0][0]))
-            times = st.solver.schedule_times()
-            if times["chosen"]:  # measured by prepare(): ms per super-step of each candidate (0 = not one)
-                extras["schedule_choice"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in times.items()}
+        H = hip()
+        extras["experiments_build"] = bool(H.experiments_build())
+        extras["stencil_kernel"] = H.last_stencil_dispatch()
+        extras["pipe_joint_windows"] = bool(H.pipe_joint())
+        # Level order of the last pipeline pass (bottom-up on short chunks).
+        extras["pipe_level_order"] = "bottom-up" if H.last_pipe_lag1() else "top-down"
+        extras["pipe_balanced_shares"] = bool(H.pipe_balanced())
+        if st.solver is not None:
+            extras["opening"] = st.solver.last_run_opening()
+            if not st.solver.fused_periodic():
+                # Halo exchanges inside the timed window: one per super-step (with
+                # peers the call primes and ends on a bare pass).
+                extras["timed_exchanges"] = int(st.solver.last_run_exchanges())
+                extras["schedule_choice"] = {k: (round(v, 4) if isinstance(v, float) else v)
+                                             for k, v in st.solver.schedule_times().items()}
+        # Who ran: the RCCL communicator's own view (not the launcher's) and every rank's device.
+        if st.comm is not None:
+            extras["rccl_ranks"] = int(st.comm.count())
+        dev = st.comm.device() if st.comm is not None else torch.cuda.current_device()
+        props = torch.cuda.get_device_properties(dev)
+        me = f"{dev}:{getattr(props, 'pci_bus_id', '?')}:{getattr(props, 'gcnArchName', props.name)}"
+        extras["rank_devices"] = [b.decode() for b in ctx.allgather_bytes(me.encode(), key="mxs/bench/devices")]
+        # One untimed, state-preserving replica of the window's opening super-step,
+        # event-timed phase by phase (collective).
+        try:
+            extras["window_phases"] = st.profile_window(args.steps)
+        except Exception as e:  # noqa: BLE001 - diagnostic only
+            extras["window_phases_error"] = str(e)[:200]
     del st
     if gpu:
         torch.cuda.empty_cache()

@@ -35,6 +35,8 @@ constexpr ncclDataType_t rccl_type() {
   else if constexpr (std::is_same_v<T, int>) return ncclInt32;
   else if constexpr (std::is_same_v<T, unsigned char> || std::is_same_v<T, char>) return ncclUint8;
   else if constexpr (std::is_same_v<T, long long> || std::is_same_v<T, long>) return ncclInt64;
+  else if constexpr (std::is_same_v<T, unsigned>) return ncclUint32;
+  else if constexpr (std::is_same_v<T, unsigned long long> || std::is_same_v<T, unsigned long>) return ncclUint64;
   else static_assert(sizeof(T) == 0, "unsupported RCCL element type");
 }
 
@@ -66,10 +68,21 @@ class RcclComm {
   // communicator is aborted first so the error path cannot block on it).
   void wait(hipStream_t stream, const char* what) const;
 
+  // Ranks the communicator really spans (ncclCommCount) and the HIP device
+  // this rank's end of it runs on (ncclCommCuDevice): the run records quote
+  // these, not the launcher's view.
+  int count() const;
+  int device() const;
+
   // Sum-allreduce `count` elements in place or out of place on `stream`.
   template <typename T>
   void allreduce_sum(const T* send, T* recv, size_t count, hipStream_t stream) const {
     MXS_RCCL_CHECK(ncclAllReduce(send, recv, count, rccl_type<T>(), ncclSum, live(), stream));
+  }
+  // Element-wise max over ranks (the solver's collective schedule decisions).
+  template <typename T>
+  void allreduce_max(const T* send, T* recv, size_t count, hipStream_t stream) const {
+    MXS_RCCL_CHECK(ncclAllReduce(send, recv, count, rccl_type<T>(), ncclMax, live(), stream));
   }
   template <typename T>
   void send(const T* buf, size_t count, int peer, hipStream_t stream) const {

@@ -4,6 +4,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstdlib>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -25,5 +26,22 @@ constexpr int kWaveSize = 64;
 // sized from the device attribute (runtime/hip_utils.hpp: device_cu_count()).
 constexpr int kNumCUs = 256;
 constexpr int kNumXCDs = 8;
+
+// Tuning / measurement knobs read from the environment (MXS_HALO_GRID,
+// MXS_HALO_LAST_*, MXS_PIPE_*, ...) exist only in an experiments build
+// (-DMXS_EXPERIMENTS=ON): a release build ignores them, so a stray variable
+// cannot change what a production run executes. bench.py records every MXS_*
+// variable and refuses to report a headline from an experiments build that
+// has one set.
+#if defined(MXS_EXPERIMENTS)
+constexpr bool kExperimentsBuild = true;
+inline const char* experiment_env(const char* name) {
+  const char* e = std::getenv(name);
+  return e && *e ? e : nullptr;
+}
+#else
+constexpr bool kExperimentsBuild = false;
+inline const char* experiment_env(const char*) { return nullptr; }
+#endif
 
 }  // namespace mxs

@@ -16,7 +16,7 @@
 #include <cstdint>
 
 #include "mxs/grid/layout.hpp"
-#include "mxs/kernels/frame_schedule.hpp"
+#include "mxs/kernels/chunk_schedule.hpp"
 
 namespace mxs {
 namespace kernels {
@@ -134,16 +134,13 @@ template <typename T>
 void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0, index_t y1,
                  Stencil5Coeffs c, bool wrap, hipStream_t s, StencilVariant v = StencilVariant::Auto);
 
-// --------------------------------------- overlapped multi-GPU pass (frame first)
-// The S-step pass over the whole core of a ghost-ring tile (no wrap) on the
-// two-stage pipeline, with the workgroups' chunks ordered by a FrameSchedule
-// (kernels/frame_schedule.hpp): the chunks that produce the S-deep output
-// frame run first, each workgroup adds 1 to *counter once its frame chunks are
-// stored (agent-scope release), and `comm_wgs` frame-only workgroups exit
-// early so the halo exchange's kernels get CUs while the pass continues.
-// Bitwise identical to stencil5_tb over the same core (same per-cell
-// arithmetic, same kernel body; only the chunk order differs).
-struct FramePassShape {
+// ------------------------------------- chunk-list pass (interior-first super-step)
+// The S-step pass over chunks of the core of a ghost-ring tile (no wrap) on the
+// two-stage pipeline: workgroup w runs the chunk list table[w * entries ..]
+// (kernels/chunk_schedule.hpp). Bitwise identical, per cell, to stencil5_tb
+// over the same core (same per-cell arithmetic and kernel body; only the
+// workgroup-to-chunk assignment differs).
+struct ChunkPassShape {
   int steps = 0;
   bool sum = false;   // sum form (c_center == c_neighbor and allowed)
   int js0 = 0;        // stage-0 levels of the joint windows
@@ -157,23 +154,16 @@ struct FramePassShape {
   // ghost columns when that range leaves [0, width)).
   index_t read_lead = 0, read_span = 0;
 };
-// False when `steps` has no frame-first form here (fp32 S = 20 / 24, fp64
-// S = 16 on whole lane vectors; other depths keep the serial schedule). The
-// caller still has to keep every chunk of its schedule within kMaxChunkBytes (rows x
-// pitch: the kernel's buffer-descriptor stores).
+// False when `steps` has no chunk-list form here (fp32 S = 20 / 24, fp64
+// S = 16 on whole lane vectors; other depths keep the one-launch pass). The
+// caller still has to keep every chunk of its schedule within kMaxChunkBytes
+// (rows x pitch: the kernel's buffer-descriptor stores).
 template <typename T>
-bool frame_pass_shape(const TileGeom& g, int steps, const Stencil5Coeffs& c, FramePassShape* out);
-// table: shape.blocks x entries chunks in device memory (FrameSchedule::table).
+bool chunk_pass_shape(const TileGeom& g, int steps, const Stencil5Coeffs& c, ChunkPassShape* out);
+// table: shape.blocks x entries chunks in device memory (ChunkSchedule::table).
 template <typename T>
-void stencil5_frame_pass(const T* in, T* out, const TileGeom& g, const Stencil5Coeffs& c, const FramePassShape& shape,
-                         const FrameChunk* table, int entries, unsigned* counter, hipStream_t s);
-// One lane spins (device deadline of `timeout_ticks` wall-clock ticks, then
-// *status = 1, a system-scope store: `status` may be pinned host memory) until
-// *counter >= target, then resets *counter to 0: the comm stream's wait for a
-// frame_pass running on another stream.
-void wait_counter(unsigned* counter, unsigned target, std::uint64_t timeout_ticks, unsigned* status, hipStream_t s);
-// Device wall-clock ticks per second (the deadline unit above).
-double wall_clock_hz();
+void stencil5_chunk_pass(const T* in, T* out, const TileGeom& g, const Stencil5Coeffs& c, const ChunkPassShape& shape,
+                         const PassChunk* table, int entries, hipStream_t s);
 
 // max |x[i]| over n elements into *out (device pointer, overwritten; NaN if
 // any element is NaN): the range check of the sum form.
@@ -207,7 +197,7 @@ void set_pipe_lag1(bool on);
 bool pipe_lag1();
 // Whether the most recent stencil launch was a pipeline pass in that order.
 bool last_pipe_lag1();
-// Fill-aware workgroup shares of the pipeline passes (frame_schedule.hpp:
+// Fill-aware workgroup shares of the pipeline passes (chunk_schedule.hpp:
 // balanced_starts; default on): a share that crosses a column-group boundary
 // pays a second pipeline fill, and with equal row shares those workgroups set
 // the pass time. MXS_PIPE_BALANCED=0 restores equal shares. Bitwise equal output.
@@ -250,9 +240,9 @@ struct Copy2DBatch {
   Copy2D op[kMaxCopies];
 };
 // grid_x: workgroups per copy (0 = sized from the largest copy; tuning only).
-// block: threads per workgroup (0 = 256, or MXS_HALO_BLOCK). One-wave (64)
-// workgroups are the ones the hardware places beside a running pipeline
-// workgroup (the frame-first schedule's copies); 256 is faster alone.
+// block: threads per workgroup (0 = 256). One-wave (64) workgroups are the
+// ones the hardware places beside a running pipeline workgroup (the
+// interior-first super-step's copies); 256 is faster alone.
 template <typename T>
 void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x = 0, int block = 0);
 

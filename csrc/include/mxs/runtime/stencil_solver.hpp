@@ -51,39 +51,36 @@
 // grid fuses the self-exchange into the kernel's wrap-around addressing
 // (`fuse_periodic_self`).
 //
-// Interior-first opening (`halo_last`; or picked by `frame_auto`'s measurement):
-// the call's first super-step, when it starts with a priming exchange, is two
-// launches of the chunk-list kernel on disjoint CUs:
+// Interior-first opening (`opening` = InteriorFirst forces it; Auto, the
+// default, lets prepare() measure it against the serial opening): the call's
+// first super-step, when it starts with a priming exchange (with peers: every
+// call), is two launches of the chunk-list kernel on disjoint CUs:
 //
 //   side stream : inner chunks (input in the core), blocks - outer workgroups
 //   main stream : pack(cur) -> RCCL -> unpack(cur) -> outer chunks (ghost ring)
 //
 // (the fork is skipped when main has drained, e.g. after synchronize(): a
 // cross-stream wait costs ~15 us). A 20-step window at N > 1 is exactly this.
+// Later super-steps of a call stay serial: back-to-back interior-first
+// super-steps pay two cross-stream waits each (35% slower over 12 super-steps),
+// and a steady-state frame-first overlap measured 3-6% slower than serial on
+// its own (docs/PERF.md), so it was removed.
 //
-// Frame-first overlap (`frame_overlap` forces it; `frame_auto`, the default, picks it
-// when prepare() measures it faster than the serial schedule): with remote
-// peers over RCCL and a depth that has a frame form (fp32 S = 20 / 24, fp64
-// S = 16: kernels::frame_pass_shape), a super-step is one pass on the side
-// stream whose chunk order (kernels/frame_schedule.hpp) stores the S-deep output
-// frame first and signals a device counter; the main stream waits for that
-// counter and exchanges the NEXT super-step's halo (pack -> RCCL -> unpack of
-// nxt) while the pass finishes the interior:
-//
-//   side stream : wait(fork) -> frame-first pass cur -> nxt
-//   main stream : record(fork) -> wait_counter -> pack(nxt) -> RCCL -> unpack(nxt)
-//
-// (the next super-step's fork is recorded after that unpack; the main stream
-// joins the side stream once, after the last super-step of a run)
-//
-// so cur's ghost ring is fresh whenever a pass starts (the first pass of a run
-// is preceded by one exchange when it is not: construction, field_changed(), a
-// thin-strip overlap step; with peers, the first pass of every call, so that
-// all ranks issue the same collectives). The pass is submitted before the counter wait, so even
-// streams that share a hardware queue cannot deadlock (the wait then just runs
-// after the pass). These super-steps are launched eagerly, not from a graph,
-// for the same reason: a graph's branches are dispatched in an order the host
-// does not choose.
+// Collective invariants (every rank must issue the same RCCL groups in the same
+// order, whatever it decides locally):
+//   * every call with peers primes exactly once and issues one exchange per
+//     super-step but the bare last one; the interior-first opening IS the
+//     priming exchange, so a rank without a chunk-list form for its tile
+//     (uneven decomposition) runs prime + pass instead and stays in step;
+//   * prepare()'s schedule decision is taken from timings agreed over ranks
+//     (element-wise max through an RCCL all-reduce, or the host allgather):
+//     every rank adopts the same opening; interior-first only when its
+//     worst-rank median beats the serial one by min_gain and by more than the
+//     worst-rank spread (interquartile range) of either;
+//   * the sum form's range guard takes max|u| over all ranks (at the first
+//     check and in every collective call: prepare, warm, profile_window).
+// Every host wait with collectives in flight goes through wait_idle(), which
+// polls under the communication watchdog and names the phase on failure.
 //
 // Sum-form guard: the sum form sums S levels unscaled (magnitudes up to
 // 5^S max|u|) and scales by c^S once. It runs only when 5 |c| <= 1 (the
@@ -101,6 +98,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <tuple>
 #include <utility>
 #include <vector>
 
@@ -112,6 +110,19 @@
 namespace mxs {
 
 enum class StencilKind : int { Jacobi5 = 0, Box = 1 };
+enum class Opening : int { Auto = 0, Serial = 1, InteriorFirst = 2 };
+
+// Event-timed phases of one untimed replica of a run's opening super-step
+// (StencilSolver::profile_window): what a short timed window spends where.
+struct WindowPhases {
+  std::string opening;        // "interior-first", "serial", "fused" or "direct"
+  int exchanges = 0;          // halo exchanges the replica issued
+  double host_enqueue_us = 0;  // host time to enqueue the super-step
+  double gpu_span_us = 0;      // first to last GPU marker
+  double wall_us = 0;          // host: start of enqueue to both streams drained
+  // (phase, start us, end us) relative to the first GPU marker.
+  std::vector<std::tuple<std::string, double, double>> phases;
+};
 
 struct SolverConfig {
   HaloBackend backend = HaloBackend::Local;
@@ -131,7 +142,8 @@ struct SolverConfig {
   kernels::Stencil5Coeffs coeffs;
   kernels::BoxWeights box;
   kernels::StencilVariant variant = kernels::StencilVariant::Auto;
-  // HaloBackend::Ipc: host allgather used once at construction (collective).
+  // Host allgather (collective): the Ipc backend's set-up, and the schedule /
+  // range agreement of backends without an RCCL communicator.
   HostAllgather bootstrap;
   // Super-steps captured per hipGraph (0 = auto: ~1 ms of work per launch).
   int graph_supersteps = 0;
@@ -140,30 +152,17 @@ struct SolverConfig {
   // neighbours' ghost rings and publishes a ready counter; the next pass waits
   // for the neighbours' counters. Replaces pack -> put -> wait -> unpack.
   bool direct_halo = false;
-  // Frame-first overlap of the RCCL halo with the pass (see above). Off by
-  // default: on one GPU (RCCL loopback, 16384 x 8192 tile) it measured 3-8%
-  // slower than the serial schedule with eager launches (docs/PERF.md,
-  // "Frame-first overlap"); it is exact and tested, and stays opt-in until a
-  // multi-GPU run shows the wire time it hides is worth the copies' interference.
-  bool frame_overlap = false;
-  // Auto: when frame_overlap is allowed here, prepare() times a few super-steps
-  // of each schedule (state-preserving, collective like prepare itself) and
-  // keeps the faster one; until then, and when no prepare() runs, serial.
-  bool frame_auto = true;
-  // Interior-first (halo-last) opening: the first super-step of a call, which
-  // starts with a priming exchange (with peers: every call), runs the chunks
-  // whose input lies in the core on most CUs while that exchange runs on the
-  // CUs they leave free, then the chunks that read the ghost ring
-  // (kernels::make_halo_last_schedule). Forced by `halo_last`; with frame_auto
-  // prepare() times it against the serial opening (prime, then the pass).
-  // Only the opening: back-to-back interior-first super-steps pay two
-  // cross-stream waits each (measured 35% slower over 12 super-steps).
-  bool halo_last = false;
-  // Frame-only workgroups that exit early and leave their CUs to the exchange
-  // (-1: MXS_FRAME_COMM_WGS or 16), and the frame chunk height (0: MXS_FRAME_ROWS
-  // or auto, kernels::make_frame_schedule).
-  int frame_comm_wgs = -1;
-  int frame_rows = 0;
+  // Opening super-step of a call with peers (see above): measured (Auto),
+  // always prime + pass (Serial), always interior-first where the tile has the
+  // form (InteriorFirst).
+  Opening opening = Opening::Auto;
+  // Auto: interior-first must beat serial by at least this fraction (and by
+  // more than the measured spread) to be chosen.
+  double min_gain = 0.03;
+  // A 1-rank RCCL-loopback solver follows the peers' schedule (every call
+  // primes, its last pass is bare, the opening is chosen as with peers), so
+  // one GPU rehearses the window shape an N-GPU run executes.
+  bool rehearse_peers = false;
   // Super-steps estimated longer than this (us, at ~9 T cell-steps/s) are
   // launched eagerly instead of from a hipGraph: on the 8-GPU tile (0.24 ms
   // passes) a 20-step RCCL-loopback window took 0.276 ms eager vs 0.285 from
@@ -184,11 +183,12 @@ class StencilSolver {
 
   void step();            // enqueue one iteration
   void run(int iters);    // enqueue `iters` iterations (super-steps of time_block, graph replay)
-  // Make a later run(iters) free of one-off costs: capture (and pre-upload) the
-  // graphs of every super-step size run(iters) uses and launch every kernel
-  // shape once. The warm-up launches write only the scratch buffer and refresh
-  // the ghost ring, so the iteration state is unchanged. Collective (all ranks
-  // call it with the same iters: it runs halo exchanges). Idempotent per size.
+  // Make a later run(iters) free of one-off costs: decide the opening (Auto,
+  // with peers), capture (and pre-upload) the graphs of every super-step size
+  // run(iters) uses and launch every kernel shape once. The warm-up launches
+  // write only the scratch buffer and refresh the ghost ring, so the iteration
+  // state is unchanged. Collective (all ranks call it with the same iters: it
+  // runs halo exchanges). Idempotent per size.
   void prepare(int iters);
   // `passes` more untimed launches of run(iters)'s super-step shapes, with the
   // same state-preserving rule as prepare() (scratch output, ghost refresh):
@@ -196,14 +196,27 @@ class StencilSolver {
   // (a cold 20-step window at 32768^2 runs ~20% slower than a warm one,
   // profiles/r02_deep/clock_ramp.txt). Collective: same passes on all ranks.
   void warm(int iters, int passes);
+  // Collective, state-preserving: one untimed replica of run(iters)'s opening
+  // super-step (priming exchange + pass, or the interior-first opening) with a
+  // GPU event between its phases, from drained streams after a device barrier
+  // (the bench's window shape). For run records: where a short window's time goes.
+  WindowPhases profile_window(int iters);
   void exchange_only();   // enqueue a halo exchange of the current tile (no update)
-  void synchronize();     // wait for everything enqueued so far
+  void synchronize();     // wait for everything enqueued so far (watchdog)
   // The caller wrote the field (checkpoint load, initial data, any direct
-  // write): the next run re-exchanges the ghost ring before its first
-  // frame-first pass and re-checks the sum form's range.
+  // write): the next run re-exchanges the ghost ring before its first pass and
+  // re-checks the sum form's range.
   void field_changed() {
     ghost_fresh_ = false;
     range_checked_ = false;
+  }
+  // Fault injection (like the apps' --fault-inject): the host
+  // sleeps `seconds` on entering `phase` ("prepare", "warm", "run",
+  // "profile_window"), so tests can stall one rank inside a collective phase
+  // and check that the others fail within the watchdog timeout naming it.
+  void inject_stall(const std::string& phase, double seconds) {
+    stall_phase_ = phase;
+    stall_s_ = seconds;
   }
 
   T* current() const { return cur_; }
@@ -216,14 +229,21 @@ class StencilSolver {
   bool fused_periodic() const { return fused_; }
   bool direct_halo() const { return direct_ != nullptr; }
   bool overlapped() const { return cfg_.overlap; }
-  // Whether super-steps of depth S run the frame-first overlapped schedule.
-  bool frame_overlap(int S) const;
-  // Whether the opening super-step of a call at depth S runs interior-first
-  // (halo-last: its priming exchange under the core chunks).
+  // Whether the solver follows the peers' schedule (remote peers, or a
+  // loopback rehearsal of them).
+  bool multi_rank() const { return multi_rank_; }
+  // Whether the opening super-step of a call at depth S runs interior-first on
+  // this rank (the opening is on and the tile has the chunk-list form).
   bool halo_last(int S) const;
+  // prepare()'s decision ("" before it decided, "serial" or "interior-first")
+  // and the agreed (worst-rank) medians / spreads it was taken from.
   const std::string& opening_choice() const { return opening_choice_; }
+  const std::string& opening_reason() const { return opening_reason_; }
   double opening_serial_ms() const { return opening_ms_[0]; }
   double opening_halo_last_ms() const { return opening_ms_[1]; }
+  double opening_serial_spread_ms() const { return opening_spread_[0]; }
+  double opening_halo_last_spread_ms() const { return opening_spread_[1]; }
+  int opening_samples() const { return opening_samples_; }
   // Workgroups of the outer (ghost-ring) launch of the interior-first opening
   // at depth S (0: none built).
   int halo_last_outer_wgs(int S) const {
@@ -231,11 +251,6 @@ class StencilSolver {
       if (h->S == S) return h->sched.outer.blocks;
     return 0;
   }
-  // The auto choice: "" before prepare() decided, else "frame" or "serial" and
-  // the median times (ms per super-step) of both.
-  const std::string& frame_choice() const { return frame_choice_; }
-  double frame_choice_serial_ms() const { return choice_ms_[0]; }
-  double frame_choice_frame_ms() const { return choice_ms_[1]; }
   // Whether the passes currently take the sum form (coefficients, user choice
   // and the measured range all allow it).
   bool sum_form_active() const { return cfg_.coeffs.sum_form && kernels::uses_sum_form(cfg_.coeffs); }
@@ -245,8 +260,9 @@ class StencilSolver {
   std::vector<std::pair<int, int>> last_run_blocks() const { return last_blocks_; }
   // Halo exchanges the last run() enqueued (priming included).
   int last_run_exchanges() const { return last_exchanges_; }
-  // Frame schedule of depth S (building it if needed); nullptr: serial.
-  const kernels::FrameSchedule* frame_schedule(int S);
+  // Opening of the last run(): "interior-first", "serial" (prime + pass),
+  // "fresh" (no priming exchange needed), "fused", "direct" or "" (no run).
+  const std::string& last_run_opening() const { return last_opening_; }
   int time_block() const { return block_; }
   int graph_supersteps() const { return chain_; }
   index_t cells_per_iteration() const { return tile_.width * tile_.height; }
@@ -280,25 +296,32 @@ class StencilSolver {
   void run_group(int S, int count, bool last_bare = false, bool first = false);
   void enqueue_bare_pass(T* cur, T* nxt, int S);  // post-exchange pass, no exchange after it
 
-  // Frame-first pass of depth S: shape + schedule + device table.
-  struct FramePass {
-    int S = 0;
-    kernels::FramePassShape shape;
-    kernels::FrameSchedule sched;
-    DeviceBuffer<kernels::FrameChunk> table;
+  // GPU markers of profile_window (nullptr in every other call).
+  struct Marks {
+    std::vector<std::unique_ptr<Event>> ev;
+    std::vector<std::string> name;
+    void mark(const std::string& n, hipStream_t s) {
+      ev.push_back(std::make_unique<Event>(true));
+      ev.back()->record(s);
+      name.push_back(n);
+    }
   };
-  FramePass* frame_pass(int S, bool build);  // nullptr: serial schedule for S
   // Interior-first pass of depth S: two launches of the chunk-list kernel
   // (inner on blocks - outer workgroups, outer after the exchange).
   struct HaloLastPass {
     int S = 0;
-    kernels::FramePassShape inner_shape, outer_shape;  // blocks = workgroups of each launch
+    kernels::ChunkPassShape inner_shape, outer_shape;  // blocks = workgroups of each launch
     kernels::HaloLastSchedule sched;
-    DeviceBuffer<kernels::FrameChunk> inner_table, outer_table;
+    DeviceBuffer<kernels::PassChunk> inner_table, outer_table;
   };
   HaloLastPass* halo_last_pass(int S, bool build);  // nullptr: not in use / no form for S
   std::unique_ptr<HaloLastPass> build_halo_last(int S, int outer_wgs);  // nullptr: no form for S
-  void enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl);
+  void enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks* marks = nullptr);
+  // The priming exchange of a call's first super-step, interior-first where
+  // this rank has the form, else exchange + pass: exactly one exchange either
+  // way. Advances cur -> nxt when `advance`.
+  void enqueue_opening(int S, bool advance);
+  bool halo_last_allowed_ = false;           // RCCL with remote peers, tuned pipeline forms, no thin strips
   bool halo_last_on_ = false;                // a call's opening super-step runs interior-first
   std::vector<std::unique_ptr<HaloLastPass>> halo_lasts_;
   std::vector<int> no_halo_last_;
@@ -306,34 +329,44 @@ class StencilSolver {
   // input): every schedule but the fused periodic, the direct IPC halo and the
   // thin-strip overlap, which exchange first.
   bool post_exchange() const { return !fused_ && !direct_ && !cfg_.overlap; }
-  void ensure_range();                       // sum-form range check (host sync)
-  void begin_run();                          // range check + prime
-  bool frame_allowed_ = false;               // config / backend / peers allow the overlap
-  bool frame_on_ = false;                    // the frame-first schedule is in use (forced, or chosen)
-  std::string frame_choice_;
-  double choice_ms_[2] = {0, 0};     // steady super-steps: serial, frame-first (ms each)
-  double opening_ms_[2] = {0, 0};    // a call's opening super-step: prime + pass, interior-first (ms)
-  std::string opening_choice_;       // "" before prepare() decided, "serial" or "halo-last"
-  void choose_schedule(int S);               // frame_auto: time both, keep the faster
-  bool side_pending_ = false;                // frame passes on the side stream not yet joined to main
+  // Sum-form range check: local measurement after a field change, agreed
+  // over ranks at the first check and whenever `collective`.
+  void ensure_range(bool collective);
+  void begin_run(bool collective);           // range check + prime
+  double opening_ms_[2] = {0, 0};            // agreed medians: prime + pass, interior-first (ms)
+  double opening_spread_[2] = {0, 0};        // agreed interquartile ranges (ms)
+  int opening_samples_ = 0;
+  std::string opening_choice_;               // "" before prepare() decided, "serial" or "interior-first"
+  std::string opening_reason_;
+  void choose_opening(int S);                // Opening::Auto: time both, agree, keep the faster
+  bool side_pending_ = false;                // side-stream work not yet joined to main
   void join_side();                          // main stream waits for the side stream's work
-  std::vector<std::unique_ptr<FramePass>> frames_;
-  std::vector<int> no_frame_;                // depths without a frame form
-  DeviceBuffer<unsigned> frame_ctl_;         // frame counter (device memory)
-  // Wait-deadline status in coherent pinned host memory: synchronize() reads it
-  // without a device-to-host copy inside the caller's timed window.
-  PinnedBuffer<unsigned> frame_status_;
-  std::uint64_t frame_timeout_ticks_ = 0;
+  // Collective agreement: element-wise max over ranks (RCCL all-reduce, or
+  // the host allgather). No-op on one rank.
+  void agree_max(std::vector<double>& v, const char* phase);
+  // RCCL ranks only: every rank reaches this point before any returns (a
+  // one-element all-reduce, waited under the watchdog).
+  void device_barrier(const char* phase);
+  // Both streams drained, polled under the communication watchdog when
+  // collectives may be in flight; failures name `phase`.
+  void wait_idle(const char* phase);
+  void maybe_stall(const char* phase) const;
+  int world_ = 1;                            // ranks of the topology
   bool ghost_fresh_ = false;                 // cur_'s ghost ring holds the neighbours' current bands
   int last_exchanges_ = 0;
+  std::string last_opening_;
   bool multi_rank_ = false;                  // peers: every run call primes (begin_run)
-  bool bare_tail_ = true;                    // with peers a call ends on a bare pass
-  bool range_checked_ = false;
+  bool range_checked_ = false;              // local_absmax_ is this field's
+  bool range_agreed_ = false;               // the ranks agreed on a range at least once
+  double local_absmax_ = 0;
   bool user_sum_ = true;                     // the caller allows the sum form
   bool sum_coeffs_ok_ = false;               // 5|c| <= 1 and c^S normal
   std::string sum_note_;
   DeviceBuffer<T> absmax_;
+  DeviceBuffer<double> agree_buf_;
   std::vector<std::pair<int, int>> last_blocks_;
+  std::string stall_phase_;
+  double stall_s_ = 0;
 
   TileGeom tile_;
   SolverConfig cfg_;
@@ -343,7 +376,7 @@ class StencilSolver {
   T* buf_b_;
   T* cur_;
   T* nxt_;
-  const RcclComm* comm_ = nullptr;  // watchdog waits (synchronize) when set
+  const RcclComm* comm_ = nullptr;  // watchdog waits and collective agreement when set
   std::unique_ptr<HaloExchanger<T>> ex_;
   std::unique_ptr<IpcDirectHalo<T>> direct_;  // SolverConfig::direct_halo
   // Direct halo: refresh the current tile's ghost ring from the neighbours

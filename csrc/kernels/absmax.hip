@@ -1,5 +1,4 @@
-// Small device helpers of the overlapped multi-GPU schedule and of the sum-form
-// range guard (kernels.hpp: wait_counter, absmax).
+// The sum-form range guard's reduction (kernels.hpp: absmax).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -12,25 +11,6 @@
 namespace mxs {
 namespace kernels {
 namespace {
-
-// One lane polls (L1-bypassing relaxed agent loads, s_sleep between polls)
-// until the frame pass's workgroups have all signalled, then rearms the
-// counter for the next pass. The launch that follows on this stream (the halo
-// pack) starts with the dispatch's cache acquire, after the producers'
-// agent-scope release: it reads the stored frame, not stale lines.
-__global__ void wait_counter_kernel(unsigned* counter, unsigned target, std::uint64_t timeout_ticks,
-                                    unsigned* status) {
-  if (threadIdx.x != 0) return;
-  const std::uint64_t t0 = wall_clock64();
-  while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-    if (wall_clock64() - t0 > timeout_ticks) {
-      __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // pinned host word
-      break;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-  __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // |x| as an unsigned bit pattern: for non-negative IEEE values the integer
 // order is the value order, and any NaN sorts above +inf.
@@ -78,18 +58,6 @@ __global__ __launch_bounds__(kAbsBlock) void absmax_kernel(const T* __restrict__
 }
 
 }  // namespace
-
-void wait_counter(unsigned* counter, unsigned target, std::uint64_t timeout_ticks, unsigned* status, hipStream_t s) {
-  wait_counter_kernel<<<1, kWaveSize, 0, s>>>(counter, target, timeout_ticks, status);
-  MXS_HIP_CHECK_LAUNCH();
-}
-
-double wall_clock_hz() {
-  int dev = 0, khz = 0;
-  MXS_HIP_CHECK(hipGetDevice(&dev));
-  MXS_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
-  return double(khz) * 1e3;
-}
 
 template <typename T>
 void absmax(const T* x, index_t n, T* out, hipStream_t s) {

@@ -119,9 +119,9 @@ void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_
   // a 16384-wide tile = 1.3 MB per segment), and the earlier cap of 64
   // workgroups per segment moved them at ~0.4 TB/s (7 us per pack of the 8-GPU tile).
   constexpr index_t kVec = 16 / sizeof(T) > 0 ? 16 / sizeof(T) : 1;
-  // MXS_HALO_BLOCK (tuning): threads per workgroup (64, 128 or 256).
+  // MXS_HALO_BLOCK (experiments build only): threads per workgroup (64, 128 or 256).
   static const int env_block = [] {
-    const char* e = std::getenv("MXS_HALO_BLOCK");
+    const char* e = experiment_env("MXS_HALO_BLOCK");
     const int v = e && *e ? std::atoi(e) : kBlock;
     return v == 64 || v == 128 ? v : kBlock;
   }();

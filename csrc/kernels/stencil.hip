@@ -347,15 +347,15 @@ const char* last_stencil_dispatch() { return g_last_dispatch.load(std::memory_or
 namespace {
 std::atomic<int> g_gpu_share{1};
 std::atomic<bool> g_pipe_joint{[] {
-  const char* e = std::getenv("MXS_PIPE_JOINT");
+  const char* e = experiment_env("MXS_PIPE_JOINT");  // experiments build only
   return !(e && std::string(e) == "0");
 }()};
 std::atomic<bool> g_pipe_lag1{[] {
-  const char* e = std::getenv("MXS_PIPE_LAG1");
+  const char* e = experiment_env("MXS_PIPE_LAG1");  // experiments build only
   return !(e && std::string(e) == "0");
 }()};
 std::atomic<bool> g_pipe_balanced{[] {
-  const char* e = std::getenv("MXS_PIPE_BALANCED");
+  const char* e = experiment_env("MXS_PIPE_BALANCED");  // experiments build only
   return !(e && std::string(e) == "0");
 }()};
 }  // namespace

@@ -1384,7 +1384,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 // read the same 2S apron rows, share that XCD's L2.
 // JOINT: joint stage-1 windows (JointShape), OWG output columns per group.
 // Workgroup ranges of the linear (group x rows) space: equal shares of `share`
-// rows (n == 0), or explicit fill-aware starts (kernels/frame_schedule.hpp:
+// rows (n == 0), or explicit fill-aware starts (kernels/chunk_schedule.hpp:
 // balanced_starts), start[w] .. start[w + 1] for workgroup w — passed by value
 // in the kernel arguments (2 KB), so a launch needs no device table and stays
 // graph-capturable.
@@ -1449,23 +1449,19 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
   }
 }
 
-// Frame-first pass of the overlapped multi-GPU schedule (kernels/frame_schedule.hpp):
-// the joint-window pipeline of stencil5_stream_pipe_kernel (ghost-ring tile, no
-// wrap) over an explicit chunk list per workgroup instead of an equal share.
-// After a chunk flagged kFrameSignal the workgroup publishes what it stored —
-// every storing wave drains its stores, the workgroup meets, one lane releases
-// at agent scope and adds 1 to `counter` (MI355X_MICROARCH.md, producer form)
-// — so the halo exchange of those cells can start while the pass goes on.
-// The halo copy kernel (copy2d_batch_kernel, 32 VGPRs) runs beside this pass:
-// two pass waves per SIMD must leave it 32 of the 512 VGPRs, which the sum
-// forms do (fp32 12 + 8 / 12 + 12: 238, 8 + 12: 225, 8-VGPR granules). The
-// per-step 8 + 12 and fp64 8 + 8 forms (244) leave 16: their copies wait for
-// CUs the frame-only workgroups free (still exact, less overlap).
+// Chunk-list pass (kernels/chunk_schedule.hpp): the joint-window pipeline of
+// stencil5_stream_pipe_kernel (ghost-ring tile, no wrap) over an explicit chunk
+// list per workgroup instead of one contiguous share. The interior-first
+// multi-GPU super-step runs two launches of it on disjoint CUs (core chunks
+// beside the halo exchange, then the ghost-ring chunks). The halo copy kernel
+// (copy2d_batch_kernel, 32 VGPRs) runs beside it: two pass waves per SIMD leave
+// it 32 of the 512 VGPRs in the sum forms (fp32 12 + 8 / 12 + 12: 238, 8 + 12:
+// 225, 8-VGPR granules); the per-step 8 + 12 and fp64 8 + 8 forms (244) leave
+// 16, and their copies take the CUs the inner launch leaves free.
 template <int S0, int S1, int PF, typename T, bool SUM, int LAG1>
-__global__ __launch_bounds__(2 * kWavesPerBlock * kWaveSize) void stencil5_pipe_frame_kernel(
+__global__ __launch_bounds__(2 * kWavesPerBlock * kWaveSize) void stencil5_pipe_chunks_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
-    index_t x_begin, index_t x_end, index_t y_begin, const FrameChunk* __restrict__ table, int entries,
-    unsigned* __restrict__ counter, T c0, T c1) {
+    index_t x_begin, index_t x_end, index_t y_begin, const PassChunk* __restrict__ table, int entries, T c0, T c1) {
   constexpr int G = kWavesPerBlock;
   using P = PipeShape<S0, S1, PF>;
   using B = typename FastBody<T, SUM>::type;
@@ -1473,22 +1469,13 @@ __global__ __launch_bounds__(2 * kWavesPerBlock * kWaveSize) void stencil5_pipe_
   __shared__ typename B::V ring[G * P::RING * kWaveSize];
   const int wave = threadIdx.x / kWaveSize;
   const int strip = wave % G, stage = wave / G;
-  const FrameChunk* __restrict__ mine = table + index_t(blockIdx.x) * entries;
+  const PassChunk* __restrict__ mine = table + index_t(blockIdx.x) * entries;
 #pragma unroll 1
   for (int e = 0; e < entries; ++e) {  // workgroup-uniform
-    const FrameChunk c = mine[e];
+    const PassChunk c = mine[e];
     if (c.r1 <= c.r0) break;  // lists are packed from slot 0
     pipe_chunk<B, S0, S1, PF, false, true, G, LAG1>(in, out, pitch, core_off, W, H, x_begin + index_t(c.group) * OWG,
                                                    x_end, y_begin + c.r0, y_begin + c.r1, c0, c1, ring, stage, strip);
-    if (c.flags & kFrameSignal) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
   }
 }
 

@@ -9,7 +9,7 @@
 #include "mxs/grid/layout.hpp"
 #include "mxs/grid/regions.hpp"
 #include "mxs/halo/plan.hpp"
-#include "mxs/kernels/frame_schedule.hpp"
+#include "mxs/kernels/chunk_schedule.hpp"
 #include "mxs/topo/cart.hpp"
 
 namespace py = pybind11;
@@ -157,46 +157,14 @@ PYBIND11_MODULE(_mxs_core, m) {
 
   m.def("balanced_starts", &kernels::balanced_starts, py::arg("groups"), py::arg("rows"), py::arg("blocks"),
         py::arg("fill"), "fill-aware linear starts of the pipeline workgroups' shares (blocks + 1 entries)");
-  // Frame-first schedule of the overlapped multi-GPU pass (kernels/frame_schedule.hpp).
-  m.def(
-      "frame_schedule",
-      [](std::int64_t groups, std::int64_t rows, int blocks, std::int64_t fill, std::int64_t frame_rows, int comm_wgs,
-         int edge_left, int edge_right) {
-        const auto s =
-            kernels::make_frame_schedule(groups, rows, blocks, fill, frame_rows, comm_wgs, edge_left, edge_right);
-        py::list table;
-        for (int w = 0; w < s.blocks; ++w) {
-          py::list l;
-          for (int e = 0; e < s.entries; ++e) {
-            const auto& c = s.at(w, e);
-            if (c.r1 > c.r0) l.append(py::make_tuple(c.group, c.r0, c.r1, c.flags));
-          }
-          table.append(l);
-        }
-        py::dict d;
-        d["blocks"] = s.blocks;
-        d["entries"] = s.entries;
-        d["signals"] = s.signals;
-        d["comm_wgs"] = s.comm_wgs;
-        d["frame_rows"] = s.frame_rows;
-        d["frame_cost"] = s.frame_cost;
-        d["bulk_cost"] = s.bulk_cost;
-        d["table"] = table;
-        d["check"] = kernels::check_frame_schedule(s, groups, rows, std::min<std::int64_t>(rows, 32), edge_left,
-                                                   edge_right);
-        return d;
-      },
-      py::arg("groups"), py::arg("rows"), py::arg("blocks"), py::arg("fill"), py::arg("frame_rows") = 0,
-      py::arg("comm_wgs") = 8, py::arg("edge_left") = 1, py::arg("edge_right") = 1,
-      "per-workgroup chunk lists (group, r0, r1, flags) + the coverage check ('' = ok)");
   // Interior-first (halo-last) schedule of the pre-exchange overlapped pass.
   m.def(
       "halo_last_schedule",
       [](std::int64_t groups, std::int64_t rows, int blocks, std::int64_t fill, std::int64_t depth,
-         std::vector<std::uint8_t> ghost, int outer_wgs, double lead_frac, std::int64_t frame_rows, int granule, int min_outer) {
+         std::vector<std::uint8_t> ghost, int outer_wgs, double lead_frac, std::int64_t band_rows, int granule, int min_outer) {
         const auto h = kernels::make_halo_last_schedule(groups, rows, blocks, fill, depth, ghost, outer_wgs, lead_frac,
-                                                        frame_rows, granule, min_outer);
-        auto lists = [](const kernels::FrameSchedule& s) {
+                                                        band_rows, granule, min_outer);
+        auto lists = [](const kernels::ChunkSchedule& s) {
           py::list table;
           for (int w = 0; w < s.blocks; ++w) {
             py::list l;
@@ -219,7 +187,7 @@ PYBIND11_MODULE(_mxs_core, m) {
         return d;
       },
       py::arg("groups"), py::arg("rows"), py::arg("blocks"), py::arg("fill"), py::arg("depth"), py::arg("ghost"),
-      py::arg("outer_wgs") = 0, py::arg("lead_frac") = 0.12, py::arg("frame_rows") = 0, py::arg("granule") = 1,
+      py::arg("outer_wgs") = 0, py::arg("lead_frac") = 0.12, py::arg("band_rows") = 0, py::arg("granule") = 1,
       py::arg("min_outer") = 1,
       "inner / outer chunk lists (group, r0, r1) of the interior-first pass + the check ('' = ok)");
 }

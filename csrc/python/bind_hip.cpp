@@ -202,36 +202,42 @@ PYBIND11_MODULE(_mxs_hip, m) {
       },
       py::arg("x"), py::arg("n"), py::arg("dtype") = "f32", "max |x[i]| (device reduction; NaN if any is NaN)");
   m.def(
-      "stencil5_frame_pass",
+      "stencil5_chunk_pass",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, double c0, double c1,
-         const std::string& dt, int comm_wgs, int frame_rows, std::uintptr_t s, bool sum_form) -> py::object {
-        // One frame-first pass with its own schedule (tuning / tests): the
-        // table lives for the call, so the launch is synchronised before return.
+         const std::string& dt, int outer_wgs, std::uintptr_t s, bool sum_form) -> py::object {
+        // One interior-first pass (tests / tuning): the inner and the outer
+        // chunk lists of kernels::make_halo_last_schedule as two launches of the
+        // chunk-list kernel on one stream. The tables live for the call, so the
+        // launches are synchronised before return.
         kernels::Stencil5Coeffs c{c0, c1, sum_form};
         auto run = [&](auto tag) -> py::object {
           using T = decltype(tag);
-          kernels::FramePassShape sh;
-          if (!kernels::frame_pass_shape<T>(g, steps, c, &sh)) return py::none();
-          const auto sched = kernels::make_frame_schedule(sh.groups, g.height, sh.blocks, sh.fill, frame_rows,
-                                                          comm_wgs < 0 ? 8 : comm_wgs);
-          DeviceBuffer<kernels::FrameChunk> tab(index_t(sched.table.size()));
-          DeviceBuffer<unsigned> ctr(1);
-          MXS_HIP_CHECK(hipMemcpy(tab.get(), sched.table.data(), tab.bytes(), hipMemcpyHostToDevice));
-          MXS_HIP_CHECK(hipMemsetAsync(ctr.get(), 0, sizeof(unsigned), strm(s)));
+          kernels::ChunkPassShape sh;
+          if (!kernels::chunk_pass_shape<T>(g, steps, c, &sh) || sh.blocks < 2) return py::none();
+          std::vector<std::uint8_t> ghost(size_t(sh.groups), 0);
+          for (index_t k = 0; k < sh.groups; ++k) {
+            const index_t x0 = k * sh.owg - sh.read_lead;
+            ghost[size_t(k)] = (x0 < 0 || x0 + sh.read_span > g.width) ? 1 : 0;
+          }
+          const auto hl = kernels::make_halo_last_schedule(sh.groups, g.height, sh.blocks, sh.fill, steps, ghost,
+                                                           outer_wgs, 0.12, 0, sh.blocks % kNumXCDs == 0 ? kNumXCDs : 1,
+                                                           32);
+          DeviceBuffer<kernels::PassChunk> ti(index_t(hl.inner.table.size())), to(index_t(hl.outer.table.size()));
+          MXS_HIP_CHECK(hipMemcpy(ti.get(), hl.inner.table.data(), ti.bytes(), hipMemcpyHostToDevice));
+          MXS_HIP_CHECK(hipMemcpy(to.get(), hl.outer.table.data(), to.bytes(), hipMemcpyHostToDevice));
+          kernels::ChunkPassShape si = sh, so = sh;
+          si.blocks = hl.inner.blocks;
+          so.blocks = hl.outer.blocks;
           Event e0(true), e1(true);
           e0.record(strm(s));
-          kernels::stencil5_frame_pass<T>(ptr<T>(in), ptr<T>(out), g, c, sh, tab.get(), sched.entries, ctr.get(),
-                                          strm(s));
+          kernels::stencil5_chunk_pass<T>(ptr<T>(in), ptr<T>(out), g, c, si, ti.get(), hl.inner.entries, strm(s));
+          kernels::stencil5_chunk_pass<T>(ptr<T>(in), ptr<T>(out), g, c, so, to.get(), hl.outer.entries, strm(s));
           e1.record(strm(s));
           MXS_HIP_CHECK(hipStreamSynchronize(strm(s)));
-          unsigned got = 0;
-          MXS_HIP_CHECK(hipMemcpy(&got, ctr.get(), sizeof(unsigned), hipMemcpyDeviceToHost));
           py::dict d;
-          d["signals"] = sched.signals;
-          d["counter"] = got;
-          d["blocks"] = sched.blocks;
-          d["frame_cost"] = sched.frame_cost;
-          d["bulk_cost"] = sched.bulk_cost;
+          d["inner_blocks"] = hl.inner.blocks;
+          d["outer_blocks"] = hl.outer.blocks;
+          d["check"] = kernels::check_halo_last_schedule(hl, sh.groups, g.height, steps, ghost);
           d["js0"] = sh.js0;
           d["lag1"] = sh.lag1;
           d["fill"] = sh.fill;
@@ -241,9 +247,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
         return parse_dtype(dt) == DType::F32 ? run(float{}) : run(double{});
       },
       py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("steps"), py::arg("c_center") = 0.2,
-      py::arg("c_neighbor") = 0.2, py::arg("dtype") = "f32", py::arg("comm_wgs") = 8, py::arg("frame_rows") = 0,
-      py::arg("stream") = 0, py::arg("sum_form") = true,
-      "one frame-first pass over the core of a ghost-ring tile (None: no frame form for this depth)");
+      py::arg("c_neighbor") = 0.2, py::arg("dtype") = "f32", py::arg("outer_wgs") = 0, py::arg("stream") = 0,
+      py::arg("sum_form") = true,
+      "one interior-first pass (inner + outer chunk lists) over the core of a ghost-ring tile (None: no "
+      "chunk-list form for this depth)");
   m.def("last_pipe_lag1", &kernels::last_pipe_lag1,
         "whether the most recent stencil launch was a pipeline pass in ascending level order");
   m.def(
@@ -316,6 +323,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
       "set_comm_timeout", [](double s) { comm_timeout() = s; }, py::arg("seconds"),
       "communication watchdog: waits on RCCL streams / IPC peers fail after this many seconds (0 = forever)");
   m.def("comm_timeout", [] { return comm_timeout(); });
+  m.def("experiments_build", [] { return kExperimentsBuild; },
+        "whether this build honours the MXS_* tuning environment knobs (-DMXS_EXPERIMENTS=ON)");
   py::class_<RcclComm>(m, "RcclComm")
       .def(py::init([](py::bytes uid, int nranks, int rank) {
              return std::make_unique<RcclComm>(std::string(uid), nranks, rank);
@@ -324,6 +333,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def_static("make_unique_id", []() { return py::bytes(RcclComm::make_unique_id()); })
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("size", &RcclComm::size)
+      .def("count", &RcclComm::count, "ranks the communicator spans (ncclCommCount)")
+      .def("device", &RcclComm::device, "HIP device of this rank's end (ncclCommCuDevice)")
       .def("healthy",
            [](const RcclComm& c) {
              std::string msg;
@@ -397,16 +408,17 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        const RcclComm* comm, const std::string& dt, HaloBackend backend, bool overlap,
                        bool use_graph, bool loopback_self, StencilKind kind, double c0, double c1, int box_radius,
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
-                       py::object bootstrap, int graph_supersteps, bool sum_form, bool direct_halo, bool frame_overlap,
-                       int frame_comm_wgs, int frame_rows, double graph_max_superstep_us, bool frame_auto,
-                       bool halo_last) {
+                       py::object bootstrap, int graph_supersteps, bool sum_form, bool direct_halo,
+                       double graph_max_superstep_us, const std::string& opening, bool rehearse_peers,
+                       double min_gain) {
              SolverConfig cfg;
-             cfg.frame_auto = frame_auto;
-             cfg.halo_last = halo_last;
+             if (opening == "auto") cfg.opening = Opening::Auto;
+             else if (opening == "serial") cfg.opening = Opening::Serial;
+             else if (opening == "interior-first") cfg.opening = Opening::InteriorFirst;
+             else throw std::invalid_argument("opening must be auto, serial or interior-first, got '" + opening + "'");
+             cfg.rehearse_peers = rehearse_peers;
+             cfg.min_gain = min_gain;
              cfg.graph_max_superstep_us = graph_max_superstep_us;
-             cfg.frame_overlap = frame_overlap;
-             cfg.frame_comm_wgs = frame_comm_wgs;
-             cfg.frame_rows = frame_rows;
              cfg.bootstrap = wrap_allgather(bootstrap);
              cfg.graph_supersteps = graph_supersteps;
              cfg.direct_halo = direct_halo;
@@ -436,63 +448,69 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("box_radius") = 1, py::arg("box_weights") = std::vector<float>{}, py::arg("variant") = "auto",
            py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
            py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = false,
-           py::arg("frame_overlap") = false, py::arg("frame_comm_wgs") = -1, py::arg("frame_rows") = 0,
-           py::arg("graph_max_superstep_us") = 150.0, py::arg("frame_auto") = true, py::arg("halo_last") = false,
-           py::keep_alive<1, 7>())
+           py::arg("graph_max_superstep_us") = 150.0, py::arg("opening") = "auto", py::arg("rehearse_peers") = false,
+           py::arg("min_gain") = 0.03, py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")
       .def(
-          "frame_overlap", [](SolverHandle& h, int S) { return h.visit([S](auto& s) { return s.frame_overlap(S); }); },
-          py::arg("S"), "whether super-steps of depth S run the frame-first overlapped schedule")
-      .def(
           "halo_last", [](SolverHandle& h, int S) { return h.visit([S](auto& s) { return s.halo_last(S); }); },
-          py::arg("S"), "whether a call's opening super-step of depth S runs interior-first (halo-last)")
+          py::arg("S"), "whether a call's opening super-step of depth S runs interior-first on this rank")
+      .def("multi_rank", [](SolverHandle& h) { return h.visit([](auto& s) { return s.multi_rank(); }); },
+           "whether the solver follows the peers' schedule (remote peers or a loopback rehearsal)")
       .def("schedule_times",
            [](SolverHandle& h) {
              return h.visit([](auto& s) {
                py::dict d;
-               d["chosen"] = s.frame_choice();
-               d["serial_ms"] = s.frame_choice_serial_ms();
-               d["frame_first_ms"] = s.frame_choice_frame_ms();
                d["opening"] = s.opening_choice();
-               d["opening_serial_ms"] = s.opening_serial_ms();
-               d["opening_halo_last_ms"] = s.opening_halo_last_ms();
-               d["opening_outer_wgs"] = s.halo_last_outer_wgs(s.time_block());
+               d["reason"] = s.opening_reason();
+               d["serial_ms"] = s.opening_serial_ms();
+               d["interior_first_ms"] = s.opening_halo_last_ms();
+               d["serial_iqr_ms"] = s.opening_serial_spread_ms();
+               d["interior_first_iqr_ms"] = s.opening_halo_last_spread_ms();
+               d["samples"] = s.opening_samples();
+               d["outer_wgs"] = s.halo_last_outer_wgs(s.time_block());
                return d;
              });
            },
-           "prepare()'s measurements: steady super-steps (serial / frame-first, ms each) and a call's opening "
-           "super-step (prime + pass / interior-first, ms); 0 = not a candidate")
-      .def("frame_choice",
-           [](SolverHandle& h) {
-             return h.visit([](auto& s) {
-               return py::make_tuple(s.frame_choice(), s.frame_choice_serial_ms(), s.frame_choice_frame_ms());
-             });
-           },
-           "auto schedule choice made by prepare(): (\"\" | \"serial\" | \"frame\" | \"halo-last\", serial ms, frame ms "
-           "per super-step)")
+           "prepare()'s opening decision and the worst-rank medians / interquartile ranges (ms) it was taken "
+           "from (0 = not measured)")
+      .def("last_run_opening", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_opening(); }); },
+           "opening of the last run(): interior-first, serial, fresh, fused, direct, overlap or ''")
+      .def(
+          "inject_stall",
+          [](SolverHandle& h, const std::string& phase, double seconds) {
+            h.visit([&](auto& s) { s.inject_stall(phase, seconds); });
+          },
+          py::arg("phase"), py::arg("seconds"),
+          "fault injection: sleep `seconds` on entering `phase` (prepare, warm, run, profile_window)")
+      .def(
+          "profile_window",
+          [](SolverHandle& h, int iters) {
+            WindowPhases w;
+            {
+              py::gil_scoped_release nogil;
+              w = h.visit([iters](auto& s) { return s.profile_window(iters); });
+            }
+            py::dict d;
+            d["opening"] = w.opening;
+            d["exchanges"] = w.exchanges;
+            d["host_enqueue_us"] = w.host_enqueue_us;
+            d["gpu_span_us"] = w.gpu_span_us;
+            d["wall_us"] = w.wall_us;
+            py::list ph;
+            for (const auto& [name, t0, t1] : w.phases) ph.append(py::make_tuple(name, t0, t1));
+            d["phases"] = ph;
+            return d;
+          },
+          py::arg("iters"),
+          "collective, state-preserving: one event-timed replica of run(iters)'s opening super-step "
+          "(phases: (stream:phase, start us, end us))")
       .def("sum_form_active", [](SolverHandle& h) { return h.visit([](auto& s) { return s.sum_form_active(); }); })
       .def("sum_form_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.sum_form_note(); }); })
       .def("last_run_blocks", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_blocks(); }); },
            "(S, count) super-steps the last run() enqueued")
       .def("last_run_exchanges", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_exchanges(); }); },
            "halo exchanges the last run() enqueued (priming included)")
-      .def(
-          "frame_schedule",
-          [](SolverHandle& h, int S) -> py::object {
-            const kernels::FrameSchedule* f = h.visit([S](auto& s) { return s.frame_schedule(S); });
-            if (!f) return py::none();
-            py::dict d;
-            d["blocks"] = f->blocks;
-            d["entries"] = f->entries;
-            d["signals"] = f->signals;
-            d["comm_wgs"] = f->comm_wgs;
-            d["frame_rows"] = f->frame_rows;
-            d["frame_cost"] = f->frame_cost;
-            d["bulk_cost"] = f->bulk_cost;
-            return d;
-          },
-          py::arg("S"), "frame-first schedule of depth S (None: serial schedule)")
       .def("step", [](SolverHandle& h) { h.visit([](auto& s) { s.step(); }); })
       .def("direct_halo", [](SolverHandle& h) { return h.visit([](auto& s) { return s.direct_halo(); }); },
            "whether halos are pushed tile-to-tile by the device (IPC backend, direct mode)")

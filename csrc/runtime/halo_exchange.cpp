@@ -84,11 +84,10 @@ void HaloExchanger<T>::check() const {
 
 namespace {
 // Workgroups per copy segment of the pack / unpack launches (0 = sized from the
-// largest segment). MXS_HALO_GRID overrides it (tuning the frame-first overlap,
-// where the copies run beside the pipeline pass).
+// largest segment). MXS_HALO_GRID overrides it in an experiments build.
 int halo_grid() {
   static const int g = [] {
-    const char* e = std::getenv("MXS_HALO_GRID");
+    const char* e = experiment_env("MXS_HALO_GRID");
     return e && *e ? std::atoi(e) : 0;
   }();
   return g;

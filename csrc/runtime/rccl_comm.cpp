@@ -58,6 +58,18 @@ void RcclComm::wait(hipStream_t stream, const char* what) const {
       what, [&] { abort(); });
 }
 
+int RcclComm::count() const {
+  int n = 0;
+  MXS_RCCL_CHECK(ncclCommCount(live(), &n));
+  return n;
+}
+
+int RcclComm::device() const {
+  int d = -1;
+  MXS_RCCL_CHECK(ncclCommCuDevice(live(), &d));
+  return d;
+}
+
 void RcclComm::abort() const {
   if (comm_) (void)ncclCommAbort(comm_);
   comm_ = nullptr;

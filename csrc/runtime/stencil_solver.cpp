@@ -3,8 +3,11 @@
 #include <algorithm>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <limits>
+#include <thread>
 #include <type_traits>
 #include <utility>
 #include <vector>
@@ -44,6 +47,16 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   if (block_ > kernels::kMaxTimeBlock &&
       !(std::is_same_v<T, float> && !cfg_.overlap && tile_.width % 4 == 0))
     block_ = kernels::kMaxTimeBlock;
+  // The time block fixes the collective structure (exchanges per call, the
+  // ghost depth exchanged): with peers every rank takes the smallest one (an
+  // uneven decomposition can cap one rank's block, e.g. a width that is not a
+  // whole number of 4-lane vectors).
+  world_ = topo.size();
+  if (world_ > 1) {
+    std::vector<double> v{-double(block_)};
+    agree_max(v, "construction: time block agreement");
+    block_ = int(-v[0]);
+  }
   MXS_CHECK(block_ <= kernels::kMaxTimeBlockDeep, "time_block must be <= " << kernels::kMaxTimeBlockDeep);
   MXS_CHECK(block_ <= tile_.width && block_ <= tile_.height,
             "time_block " << block_ << " exceeds the tile (" << tile_.width << "x" << tile_.height
@@ -57,21 +70,18 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   HaloBootstrap boot;
   boot.rank = rank;
   boot.world_size = topo.size();
-  // MXS_PEER_SCHEDULE (measurement): 1 = a 1-rank RCCL-loopback solver follows
-  // the peers' schedule (prime every call, bare last pass), so one GPU can
-  // time the window shape an 8-GPU run executes; 2 = the same without the bare
-  // last pass (the round-3 schedule: n + 1 exchanges per call of n super-steps).
-  const char* peer_env = std::getenv("MXS_PEER_SCHEDULE");
-  const int peer_mode = cfg_.loopback_self && peer_env ? std::atoi(peer_env) : 0;
-  multi_rank_ = topo.size() > 1 || peer_mode == 1 || peer_mode == 2;
-  bare_tail_ = peer_mode != 2;
+  // With peers (or rehearsing them through loopback) every call primes and
+  // ends on a bare pass, and the opening is chosen as with peers.
+  multi_rank_ = world_ > 1 || (cfg_.loopback_self && cfg_.rehearse_peers);
   boot.allgather = cfg_.bootstrap;
   boot.timeout_s = comm_timeout() > 0 ? comm_timeout() : 60.0;
   ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm, &boot);
   const bool all_self_nbrs = plan.sends.empty();
   if (cfg_.direct_halo && cfg_.backend == HaloBackend::Ipc && cfg_.kind == StencilKind::Jacobi5 && !all_self_nbrs)
     direct_ = std::make_unique<IpcDirectHalo<T>>(topo, rank, tile_, buf_a_, buf_b_, cfg_.bootstrap, boot.timeout_s);
-  cfg_.bootstrap = nullptr;  // setup only; drop it (it may hold a Python callable)
+  // cfg_.bootstrap stays: it is the host agreement of backends without an RCCL
+  // communicator (agree_max). It may hold a Python callable; the solver is
+  // destroyed from Python with the GIL held.
   // Super-steps per graph launch: enough for ~1 ms of work per launch (the
   // launch gap is ~10 us), estimated at 5 T cell-iterations/s; at most 8.
   chain_ = chain_for(block_);
@@ -81,21 +91,23 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   constexpr int N = 16 / int(sizeof(T));
   fused_ = cfg_.fuse_periodic_self && all_self && cfg_.kind == StencilKind::Jacobi5 && tile_.width % N == 0 &&
            kernels::stencil5_periodic_supported<T>(tile_);
-  // Frame-first overlap: RCCL with a wire transfer, the tuned kernel forms,
+  // Interior-first opening: RCCL with a wire transfer, the tuned kernel forms,
   // every edge a neighbour's (time blocking), the thin-strip overlap off.
-  frame_allowed_ = (cfg_.frame_overlap || cfg_.frame_auto || cfg_.halo_last) && cfg_.backend == HaloBackend::Rccl &&
-                   !plan.sends.empty() && !fused_ &&
-                   cfg_.kind == StencilKind::Jacobi5 && cfg_.variant == kernels::StencilVariant::Auto &&
-                   block_ > 1 && !cfg_.overlap;
-  frame_on_ = frame_allowed_ && cfg_.frame_overlap;
-  halo_last_on_ = frame_allowed_ && cfg_.halo_last;
-  if (frame_allowed_) {
-    frame_ctl_.reset(1);
-    MXS_HIP_CHECK(hipMemsetAsync(frame_ctl_.get(), 0, sizeof(unsigned), main_.get()));
-    frame_status_.reset(1, hipHostMallocCoherent | hipHostMallocMapped);
-    *frame_status_.get() = 0;
-    const double limit = comm_timeout() > 0 ? comm_timeout() : 600.0;
-    frame_timeout_ticks_ = std::uint64_t(limit * kernels::wall_clock_hz());
+  halo_last_allowed_ = cfg_.opening != Opening::Serial && cfg_.backend == HaloBackend::Rccl && !plan.sends.empty() &&
+                       !fused_ && cfg_.kind == StencilKind::Jacobi5 &&
+                       cfg_.variant == kernels::StencilVariant::Auto && block_ > 1 && !cfg_.overlap;
+  if (world_ > 1) {  // one rank without it (thin-strip overlap on a small tile) rules it out everywhere
+    std::vector<double> v{halo_last_allowed_ ? 0.0 : 1.0};
+    agree_max(v, "construction: opening agreement");
+    halo_last_allowed_ = v[0] == 0.0;
+  }
+  halo_last_on_ = halo_last_allowed_ && cfg_.opening == Opening::InteriorFirst;
+  if (halo_last_on_) {
+    opening_choice_ = "interior-first";
+    opening_reason_ = "forced (opening = interior-first)";
+  } else if (cfg_.opening == Opening::Serial) {
+    opening_choice_ = "serial";
+    opening_reason_ = "forced (opening = serial)";
   }
   // Sum-form guard, coefficient part (the range part runs before the first pass).
   user_sum_ = cfg_.coeffs.sum_form;
@@ -160,40 +172,6 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
     direct_->wait(m);
     update(cur, nxt, S, 0, w, 0, h, m);
     direct_->push(nxt, m);
-    return;
-  }
-  if (FramePass* fp = frame_pass(S, false)) {
-    // Frame-first pass on the side stream; the main stream exchanges nxt's
-    // halo as soon as the frame is stored. One cross-stream edge per
-    // super-step: the pass waits for the main stream's latest work (the
-    // previous exchange, whose unpack filled cur's ghost ring); the caller
-    // joins the side stream back once, after its last super-step (a join per
-    // super-step cost ~15 us of queue-to-queue latency each: 240 steps 3.55 vs
-    // 3.39 ms serial with no exchange work at all, profiles/r03_probe).
-    // Submission order matters: the pass is enqueued before the counter wait
-    // (see the header).
-    fork_.record(m);
-    fork_.wait_on(side);
-    kernels::stencil5_frame_pass<T>(cur, nxt, tile_, cfg_.coeffs, fp->shape, fp->table.get(), fp->sched.entries,
-                                    frame_ctl_.get(), side);
-    side_pending_ = true;
-    kernels::wait_counter(frame_ctl_.get(), unsigned(fp->sched.signals), frame_timeout_ticks_, frame_status_.get(), m);
-    // MXS_FRAME_PROBE (timing experiments only, the field is then WRONG):
-    // 1 = skip the copies, 2 = skip the RCCL transfer, 3 = skip both.
-    static const int probe = [] {
-      const char* e = std::getenv("MXS_FRAME_PROBE");
-      return e && *e ? std::atoi(e) : 0;
-    }();
-    // One-wave copy workgroups: they fit beside a pipeline workgroup (4-wave
-    // ones were not placed until the pass ended, profiles/r03_window4).
-    ex_->set_copy_block(64);
-    if (probe == 0) {
-      ex_->exchange(nxt, m);
-    } else {
-      if (!(probe & 1)) ex_->pack(nxt, m);
-      if (!(probe & 2)) ex_->transfer(m);
-      if (!(probe & 1)) ex_->unpack(nxt, m);
-    }
     return;
   }
   if (!cfg_.overlap) {
@@ -311,8 +289,7 @@ typename StencilSolver<T>::GraphSet* StencilSolver<T>::graphs_for(int S, int cou
     if (gs->S == S) return gs->ok ? gs.get() : nullptr;
   if (int(graphs_.size()) >= kMaxGraphSets) {
     // run() is asynchronous: launches of the evicted executables may still be queued.
-    main_.sync();
-    side_.sync();
+    wait_idle("graph eviction");
     graphs_.erase(graphs_.begin());
   }
   auto gs = std::make_unique<GraphSet>();
@@ -341,45 +318,31 @@ template <typename T>
 void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
   if (count <= 0) return;
   last_blocks_.emplace_back(S, count);
-  // Interior-first opening: the call's first super-step would start with a
-  // priming exchange (with peers: every call); run it under the core chunks.
+  // The call's first super-step starts with a priming exchange (with peers:
+  // every call): interior-first when the opening is on (exactly one exchange
+  // whether or not this rank has the form, see enqueue_opening).
   if (first && halo_last_on_ && post_exchange() && !ghost_fresh_) {
-    if (HaloLastPass* hl = halo_last_pass(S, true)) {
-      enqueue_halo_last(cur_, nxt_, hl);
-      std::swap(cur_, nxt_);
-      ++last_exchanges_;
-      ghost_fresh_ = false;  // its output's ring: primed by the next super-step / call
-      if (--count == 0) return;
-    }
+    last_opening_ = halo_last_pass(S, true) ? "interior-first" : "serial";
+    enqueue_opening(S, true);
+    ++last_exchanges_;
+    ghost_fresh_ = false;  // its output's ring: primed by the next super-step / call
+    if (--count == 0) return;
   }
-  join_side();  // an interior-first opening (or frame passes) may leave side work pending
-  // Post-exchange super-steps (frame-first and serial): cur's ghost ring must
-  // be fresh before the first one; each leaves the next one's fresh. The
-  // thin-strip overlap schedule exchanges first and leaves it stale.
+  join_side();  // an interior-first opening leaves side work pending
+  // Post-exchange super-steps: cur's ghost ring must be fresh before the first
+  // one; each leaves the next one's fresh. The thin-strip overlap schedule
+  // exchanges first and leaves it stale.
   if (post_exchange() && !ghost_fresh_) {
+    if (first && last_opening_.empty()) last_opening_ = "serial";
     ex_->exchange(cur_, main_.get());
     ++last_exchanges_;
   }
+  if (first && last_opening_.empty()) last_opening_ = post_exchange() ? "fresh" : "overlap";
   last_bare = last_bare && post_exchange();
   const int full = last_bare ? count - 1 : count;  // super-steps with their exchange
   // Exchanges of the super-steps themselves (graph replays included): one each,
   // the bare tail none; the fused periodic self-exchange is no exchange at all.
   if (!fused_) last_exchanges_ += post_exchange() ? full : count;
-  auto bare_tail = [&] {
-    if (!last_bare) return;
-    enqueue_bare_pass(cur_, nxt_, S);
-    std::swap(cur_, nxt_);
-  };
-  if (frame_pass(S, true)) {  // eager launches (header)
-    for (int i = 0; i < full; ++i) {
-      enqueue_block(cur_, nxt_, S);
-      std::swap(cur_, nxt_);
-    }
-    join_side();
-    bare_tail();
-    ghost_fresh_ = !last_bare;
-    return;
-  }
   int i = 0;
   if (GraphSet* gs = full > 0 ? graphs_for(S, full) : nullptr) {
     for (; i + gs->chain <= full; i += gs->chain) {
@@ -392,13 +355,16 @@ void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
     enqueue_block(cur_, nxt_, S);
     std::swap(cur_, nxt_);
   }
-  bare_tail();
+  if (last_bare) {
+    enqueue_bare_pass(cur_, nxt_, S);
+    std::swap(cur_, nxt_);
+  }
   ghost_fresh_ = post_exchange() && !last_bare;
 }
 
-// The last super-step of a call with peers: the pass alone, on the main stream
-// (after join_side() when the frame-first schedule ran before it). Its output's
-// ghost ring stays stale; the next call's priming exchange refreshes it.
+// The last super-step of a call with peers: the pass alone, on the main stream.
+// Its output's ghost ring stays stale; the next call's priming exchange
+// refreshes it.
 template <typename T>
 void StencilSolver<T>::enqueue_bare_pass(T* cur, T* nxt, int S) {
   MXS_TRACE_RANGE("stencil.superstep_bare");
@@ -415,41 +381,55 @@ void StencilSolver<T>::prime() {
 }
 
 template <typename T>
-void StencilSolver<T>::ensure_range() {
-  if (range_checked_) return;
-  range_checked_ = true;
-  if (!(user_sum_ && sum_coeffs_ok_)) return;
-  // max|u| over the whole current buffer (core and ghost ring): with
-  // 5 |c| <= 1 no later pass can exceed it, so one check per field change.
-  if (!absmax_.get()) absmax_.reset(1);
-  kernels::absmax<T>(cur_, tile_.alloc_elems(), absmax_.get(), main_.get());
-  T m = T(0);
-  MXS_HIP_CHECK(hipMemcpyAsync(&m, absmax_.get(), sizeof(T), hipMemcpyDeviceToHost, main_.get()));
-  main_.sync();
+void StencilSolver<T>::ensure_range(bool collective) {
+  if (!(user_sum_ && sum_coeffs_ok_)) return;  // config-level: the same on every rank
+  // max|u| over the whole current buffer (core, ghost ring and the zeroed
+  // padding): with 5 |c| <= 1 no later pass can exceed it, so one local
+  // measurement per field change.
+  if (!range_checked_) {
+    if (!absmax_.get()) absmax_.reset(1);
+    kernels::absmax<T>(cur_, tile_.alloc_elems(), absmax_.get(), main_.get());
+    T m = T(0);
+    MXS_HIP_CHECK(hipMemcpyAsync(&m, absmax_.get(), sizeof(T), hipMemcpyDeviceToHost, main_.get()));
+    wait_idle("sum-form range check");
+    local_absmax_ = std::isnan(double(m)) ? std::numeric_limits<double>::infinity() : double(m);
+    range_checked_ = true;
+  }
+  // With peers the maximum is agreed over all ranks, so every tile takes the
+  // same evaluation form (the result must not depend on the decomposition):
+  // at the first check and in every collective call (prepare, warm,
+  // profile_window). A run() after one rank alone changed its field
+  // (field_changed() is per rank) re-measures locally: that rank may leave the
+  // sum form on its own (numerically safe, only the rounding differs) until
+  // the next collective call agrees again.
+  double md = local_absmax_;
+  if (world_ > 1 && (collective || !range_agreed_)) {
+    std::vector<double> v{md};
+    agree_max(v, "sum-form range agreement");
+    md = v[0];
+    range_agreed_ = true;
+  }
   const double bound = double(std::numeric_limits<T>::max()) / 4.0 / std::pow(5.0, double(block_));
-  const bool ok = std::isfinite(double(m)) && double(m) < bound;
+  const bool ok = std::isfinite(md) && md < bound;
   if (ok == cfg_.coeffs.sum_form) return;
   cfg_.coeffs.sum_form = ok;
   sum_note_ = ok ? "" : "sum form off: max|u| * 5^S would overflow the element type (per-step form)";
-  // Captured graphs and frame shapes were built for the other form.
-  main_.sync();
-  side_.sync();
+  // Captured graphs and chunk-pass shapes were built for the other form.
+  wait_idle("sum-form switch");
   graphs_.clear();
-  frames_.clear();
-  no_frame_.clear();
   halo_lasts_.clear();
   no_halo_last_.clear();
   warmed_.clear();
 }
 
 template <typename T>
-void StencilSolver<T>::begin_run() {
+void StencilSolver<T>::begin_run(bool collective) {
   // Whether a run starts with a priming exchange must be the same on every
   // rank (it is a collective). field_changed() is per rank (a caller may read
   // or write one rank's field alone), so with peers every call primes: one
   // exchange per run() / prepare() / warm() call, not per super-step.
   if (multi_rank_) ghost_fresh_ = false;
-  ensure_range();
+  ensure_range(collective);
   prime();
 }
 
@@ -458,90 +438,124 @@ void StencilSolver<T>::run(int iters) {
   MXS_TRACE_RANGE("stencil.run");
   last_blocks_.clear();
   last_exchanges_ = 0;
+  last_opening_.clear();
   if (iters <= 0) return;
-  begin_run();
+  maybe_stall("run");
+  begin_run(false);
+  if (fused_) last_opening_ = "fused";
+  if (direct_) last_opening_ = "direct";
   Group gr[2];
   split(iters, gr);
   // With peers every call primes (begin_run), so the exchange after the call's
   // last pass would be redundant: it ends on a bare pass (header).
   const int last = gr[1].count > 0 ? 1 : 0, first = gr[0].count > 0 ? 0 : 1;
-  for (int k = 0; k < 2; ++k)
-    run_group(gr[k].S, gr[k].count, multi_rank_ && bare_tail_ && k == last, k == first);
+  for (int k = 0; k < 2; ++k) run_group(gr[k].S, gr[k].count, multi_rank_ && k == last, k == first);
 }
 
 template <typename T>
-typename StencilSolver<T>::FramePass* StencilSolver<T>::frame_pass(int S, bool build) {
-  if (!frame_on_) return nullptr;
-  for (auto& f : frames_)
-    if (f->S == S) return f.get();
-  if (!build || std::find(no_frame_.begin(), no_frame_.end(), S) != no_frame_.end()) return nullptr;
-  kernels::FramePassShape shape;
-  if (!kernels::frame_pass_shape<T>(tile_, S, cfg_.coeffs, &shape)) {
-    no_frame_.push_back(S);
-    return nullptr;
-  }
-  auto env_int = [](const char* k, int dflt) {
-    const char* e = std::getenv(k);
-    return e && *e ? std::atoi(e) : dflt;
-  };
-  const int comm = cfg_.frame_comm_wgs >= 0 ? cfg_.frame_comm_wgs : env_int("MXS_FRAME_COMM_WGS", 16);
-  const int rows = cfg_.frame_rows > 0 ? cfg_.frame_rows : env_int("MXS_FRAME_ROWS", 0);
-  // Edge groups: those holding output columns of the S-wide left / right bands.
-  const int left = int(std::min<index_t>(shape.groups, (S + shape.owg - 1) / shape.owg));
-  const index_t last_w = tile_.width - (shape.groups - 1) * shape.owg;
-  const int right = last_w >= S ? 1 : 2;
-  auto fp = std::make_unique<FramePass>();
-  fp->S = S;
-  fp->shape = shape;
+void StencilSolver<T>::maybe_stall(const char* phase) const {
+  if (stall_s_ <= 0 || stall_phase_ != phase) return;
+  std::fprintf(stderr, "[fault-inject] stalling %.1f s in %s\n", stall_s_, phase);
+  std::fflush(stderr);
+  std::this_thread::sleep_for(std::chrono::duration<double>(stall_s_));
+}
+
+template <typename T>
+void StencilSolver<T>::wait_idle(const char* phase) {
   try {
-    fp->sched = kernels::make_frame_schedule(shape.groups, tile_.height, shape.blocks, shape.fill,
-                                             rows > 0 ? std::max<index_t>(rows, S) : 0, comm, left, right);
-  } catch (const std::invalid_argument&) {
-    no_frame_.push_back(S);  // more frame chunks than workgroups: serial
-    return nullptr;
+    // With an RCCL communicator and a watchdog: poll (a dead or hung peer
+    // fails the job, naming the phase, instead of blocking it).
+    if (comm_ && comm_timeout() > 0) {
+      comm_->wait(main_.get(), phase);
+      comm_->wait(side_.get(), phase);
+    }
+    // IPC waits carry their own device deadline: the streams drain either way.
+    main_.spin_sync();
+    side_.spin_sync();
+    side_pending_ = false;  // both streams drained: nothing for main to wait for
+    if (ex_) ex_->check();
+    if (direct_) direct_->check();
+  } catch (const std::exception& e) {
+    const std::string msg = e.what();
+    raise_error(msg.rfind(phase, 0) == 0 ? msg : std::string(phase) + ": " + msg);
   }
-  index_t longest = 0;
-  for (const auto& c : fp->sched.table) longest = std::max<index_t>(longest, c.r1 - c.r0);
-  if (longest * tile_.pitch * index_t(sizeof(T)) > kernels::kMaxChunkBytes) {
-    no_frame_.push_back(S);  // a chunk past the buffer-descriptor range
-    return nullptr;
-  }
-  fp->table.reset(index_t(fp->sched.table.size()));
-  MXS_HIP_CHECK(hipMemcpy(fp->table.get(), fp->sched.table.data(), fp->table.bytes(), hipMemcpyHostToDevice));
-  frames_.push_back(std::move(fp));
-  return frames_.back().get();
 }
 
 template <typename T>
-bool StencilSolver<T>::frame_overlap(int S) const {
-  if (!frame_on_) return false;
-  for (const auto& f : frames_)
-    if (f->S == S) return true;
-  return std::find(no_frame_.begin(), no_frame_.end(), S) == no_frame_.end() &&
-         kernels::frame_pass_shape<T>(tile_, S, cfg_.coeffs, nullptr);
+void StencilSolver<T>::agree_max(std::vector<double>& v, const char* phase) {
+  if (world_ <= 1 || v.empty()) return;
+  if (comm_) {
+    if (agree_buf_.size() < index_t(v.size())) agree_buf_.reset(index_t(v.size()));
+    const size_t bytes = v.size() * sizeof(double);
+    MXS_HIP_CHECK(hipMemcpyAsync(agree_buf_.get(), v.data(), bytes, hipMemcpyHostToDevice, main_.get()));
+    comm_->allreduce_max<double>(agree_buf_.get(), agree_buf_.get(), v.size(), main_.get());
+    MXS_HIP_CHECK(hipMemcpyAsync(v.data(), agree_buf_.get(), bytes, hipMemcpyDeviceToHost, main_.get()));
+    wait_idle(phase);
+    return;
+  }
+  MXS_CHECK(static_cast<bool>(cfg_.bootstrap),
+            phase << ": " << world_ << " ranks but neither an RCCL communicator nor a host allgather to agree on");
+  std::string blob(v.size() * sizeof(double), '\0');
+  std::memcpy(blob.data(), v.data(), blob.size());
+  std::vector<std::string> parts;
+  try {
+    parts = cfg_.bootstrap(blob);
+  } catch (const std::exception& e) {
+    raise_error(std::string(phase) + ": host agreement failed: " + e.what());
+  }
+  for (const auto& p : parts) {
+    MXS_CHECK(p.size() == blob.size(), phase << ": ranks disagree on the agreement's length");
+    for (size_t i = 0; i < v.size(); ++i) {
+      double x;
+      std::memcpy(&x, p.data() + i * sizeof(double), sizeof(double));
+      v[i] = std::max(v[i], x);
+    }
+  }
 }
 
-// frame_auto: median of 3 alternating timings of 2 state-preserving
-// super-steps (cur -> nxt, no swap) per schedule. Both schedules post-exchange
-// and issue the same RCCL groups in the same order, so ranks that choose
-// differently still match each other's sends and receives.
 template <typename T>
-void StencilSolver<T>::choose_schedule(int S) {
-  if (!frame_allowed_ || !cfg_.frame_auto || cfg_.frame_overlap || cfg_.halo_last || !frame_choice_.empty()) return;
-  frame_on_ = true;
-  const bool has_frame = frame_pass(S, true) != nullptr;
-  frame_on_ = false;
+void StencilSolver<T>::device_barrier(const char* phase) {
+  if (world_ <= 1 || !comm_) return;
+  std::vector<double> v{0.0};
+  agree_max(v, phase);
+}
+
+namespace {
+// Median and interquartile range of a small sample (sorted in place).
+std::pair<double, double> median_iqr(std::vector<double>& v) {
+  if (v.empty()) return {0.0, 0.0};
+  std::sort(v.begin(), v.end());
+  const size_t n = v.size();
+  return {v[n / 2], v[(3 * n) / 4 < n ? (3 * n) / 4 : n - 1] - v[n / 4]};
+}
+}  // namespace
+
+// Opening::Auto, once (the first prepare() with a form at its depth): the
+// call's opening super-step timed from drained streams after a device barrier,
+// as a timed window sees it (host clock to both streams drained again; an
+// event recorded on main before the opening would itself force the fork the
+// opening skips): prime + pass against up to three interior-first outer sets
+// (the modelled one and one XCD step either side: where the outer workgroups
+// land decides the opening; on one box 32 / 40 / 48 measured 0.296 / 0.259 /
+// 0.431 ms against 0.269 serial, profiles/r03_halolast). Every rank times the
+// same 4 openings in the same order (a candidate it lacks is replaced by the
+// serial one: the same exchanges everywhere), then the medians and spreads are
+// agreed (worst rank) and every rank adopts the same decision.
+template <typename T>
+void StencilSolver<T>::choose_opening(int S) {
+  if (!halo_last_allowed_ || cfg_.opening != Opening::Auto || !opening_choice_.empty()) return;
   halo_last_on_ = true;
   HaloLastPass* hl = halo_last_pass(S, true);
   halo_last_on_ = false;
-  if (!has_frame && !hl) return;  // nothing to choose at this depth (decided at the next prepare)
-  // Interior-first candidates: the modelled outer set and one XCD step either
-  // side. Where the outer workgroups land decides the opening (36 of them left
-  // some XCD a CU short; on one box 32 / 40 / 48 measured 0.296 / 0.259 /
-  // 0.431 ms against 0.269 serial, profiles/r03_halolast), so it is measured.
+  std::vector<double> have{hl ? 1.0 : 0.0};
+  agree_max(have, "prepare: opening agreement");
+  if (have[0] == 0.0) {
+    opening_choice_ = "serial";
+    opening_reason_ = "no rank has an interior-first form at depth " + std::to_string(S);
+    return;
+  }
   std::vector<std::unique_ptr<HaloLastPass>> alt;
-  const bool env_wgs = std::getenv("MXS_HALO_LAST_WGS") != nullptr;
-  if (hl && !env_wgs) {
+  if (hl && !experiment_env("MXS_HALO_LAST_WGS")) {
     const int m = hl->sched.outer.blocks;
     for (int d : {-kXcds, kXcds}) {
       const int k = m + d;
@@ -557,59 +571,27 @@ void StencilSolver<T>::choose_schedule(int S) {
     ex_->exchange(cur_, main_.get());
     ghost_fresh_ = true;
   }
-  // Steady super-steps: serial vs frame-first, 2 back-to-back super-steps each.
-  // Opening super-step of a call (a priming exchange, then the pass): serial
-  // vs interior-first, one super-step from drained streams, as a short timed
-  // window sees it. Alternating rounds, medians; every launch is state-preserving
-  // (cur -> nxt, cur's ring re-exchanged with the same values).
-  std::vector<double> t[2], t_open_serial;
-  std::vector<std::vector<double>> t_open(3);
-  Event e0(true), e1(true);
-  // Opening candidates are timed the way a caller's window sees them: host
-  // clock from drained streams to both drained again (an event recorded on main
-  // before the opening would itself force the fork the opening skips).
-  auto timed_host = [&](auto&& enqueue) {
-    join_side();
-    main_.sync();
-    side_.sync();
-    side_pending_ = false;
-    const auto t0 = std::chrono::steady_clock::now();
-    enqueue();
-    main_.spin_sync();
-    side_.spin_sync();
-    side_pending_ = false;
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  };
   auto timed = [&](auto&& enqueue) {
     join_side();
-    main_.sync();
-    side_.sync();
-    side_pending_ = false;
-    e0.record(main_.get());
+    wait_idle("prepare: opening timing");
+    device_barrier("prepare: opening timing");
+    const auto t0 = std::chrono::steady_clock::now();
     enqueue();
     join_side();
-    e1.record(main_.get());
-    e1.sync();
-    return double(e1.since(e0));
+    wait_idle("prepare: opening timing");
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   };
-  // A candidate without a form here is replaced by the serial one, so every
-  // rank issues the same exchanges whatever it can run.
-  for (int rep = 0; rep < 4; ++rep) {
-    for (int mode = 0; mode < 2; ++mode) {
-      frame_on_ = mode == 1 && has_frame;
-      const double ms = timed([&] {
-        for (int i = 0; i < 2; ++i) enqueue_block(cur_, nxt_, S);
-      });
-      if (rep > 0 && (mode == 0 || has_frame)) t[mode].push_back(ms / 2.0);  // round 0 warms every shape
-    }
-    frame_on_ = false;
-    const double serial_open = timed_host([&] {
+  constexpr int kCands = 3, kReps = 9;  // round 0 warms every shape
+  std::vector<double> t_serial;
+  std::vector<std::vector<double>> t_cand(kCands);
+  for (int rep = 0; rep < kReps; ++rep) {
+    const double serial = timed([&] {
       ex_->exchange(cur_, main_.get());
       enqueue_bare_pass(cur_, nxt_, S);
     });
-    if (rep > 0) t_open_serial.push_back(serial_open);
-    for (size_t c = 0; c < 3; ++c) {  // always 3 openings: the same exchanges on every rank
-      const double ms = timed_host([&] {
+    if (rep > 0) t_serial.push_back(serial);
+    for (size_t c = 0; c < size_t(kCands); ++c) {
+      const double ms = timed([&] {
         if (c < cands.size()) {
           enqueue_halo_last(cur_, nxt_, cands[c]);
         } else {
@@ -617,29 +599,39 @@ void StencilSolver<T>::choose_schedule(int S) {
           enqueue_bare_pass(cur_, nxt_, S);
         }
       });
-      if (rep > 0 && c < cands.size()) t_open[c].push_back(ms);
+      if (rep > 0 && c < cands.size()) t_cand[c].push_back(ms);
     }
   }
-  auto median = [](std::vector<double>& v) {
-    if (v.empty()) return 0.0;
-    std::sort(v.begin(), v.end());
-    return v[v.size() / 2];
-  };
-  choice_ms_[0] = median(t[0]);
-  choice_ms_[1] = median(t[1]);
-  opening_ms_[0] = median(t_open_serial);
+  constexpr double kMissing = 1e30;
+  std::vector<double> v(2 * (1 + kCands), kMissing);
+  std::tie(v[0], v[1 + kCands]) = median_iqr(t_serial);
+  for (size_t c = 0; c < cands.size(); ++c) std::tie(v[1 + c], v[2 + kCands + c]) = median_iqr(t_cand[c]);
+  agree_max(v, "prepare: opening agreement");
   size_t best = 0;
-  for (size_t c = 0; c < cands.size(); ++c)
-    if (median(t_open[c]) < median(t_open[best])) best = c;
-  opening_ms_[1] = cands.empty() ? 0.0 : median(t_open[best]);
-  if (best > 0) {  // keep the measured best outer set for S
+  for (size_t c = 1; c < size_t(kCands); ++c)
+    if (v[1 + c] < v[1 + best]) best = c;
+  const double serial = v[0], hlt = v[1 + best];
+  const double noise = std::max(v[1 + kCands], v[2 + kCands + best]);
+  const bool win = hlt < kMissing && serial - hlt >= cfg_.min_gain * serial && serial - hlt > noise;
+  opening_ms_[0] = serial;
+  opening_ms_[1] = hlt < kMissing ? hlt : 0.0;
+  opening_spread_[0] = v[1 + kCands];
+  opening_spread_[1] = hlt < kMissing ? v[2 + kCands + best] : 0.0;
+  opening_samples_ = kReps - 1;
+  if (win && best > 0 && best - 1 < alt.size()) {  // keep the measured best outer set for S
     for (auto& h : halo_lasts_)
       if (h->S == S) h = std::move(alt[best - 1]);
   }
-  frame_on_ = has_frame && choice_ms_[1] < choice_ms_[0];
-  halo_last_on_ = !cands.empty() && opening_ms_[1] < opening_ms_[0];
-  frame_choice_ = frame_on_ ? "frame" : "serial";
-  opening_choice_ = halo_last_on_ ? "halo-last" : "serial";
+  halo_last_on_ = win;
+  opening_choice_ = win ? "interior-first" : "serial";
+  char buf[256];
+  std::snprintf(buf, sizeof(buf),
+                "worst-rank medians of %d: interior-first %.4f ms, serial %.4f ms (IQR %.4f / %.4f ms): %s",
+                kReps - 1, opening_ms_[1], serial, opening_spread_[1], opening_spread_[0],
+                win ? "gain above the threshold and the spread"
+                    : (hlt >= kMissing ? "no rank-wide interior-first candidate"
+                                       : "gain below the threshold or within the spread"));
+  opening_reason_ = buf;
 }
 
 // Interior-first pass of depth S (built on first use while the schedule is on).
@@ -661,17 +653,17 @@ typename StencilSolver<T>::HaloLastPass* StencilSolver<T>::halo_last_pass(int S,
 // outer_wgs: 0 = MXS_HALO_LAST_WGS or the schedule's model.
 template <typename T>
 std::unique_ptr<typename StencilSolver<T>::HaloLastPass> StencilSolver<T>::build_halo_last(int S, int outer_wgs) {
-  kernels::FramePassShape shape;
-  if (!kernels::frame_pass_shape<T>(tile_, S, cfg_.coeffs, &shape) || shape.blocks < 2) return nullptr;
+  kernels::ChunkPassShape shape;
+  if (!kernels::chunk_pass_shape<T>(tile_, S, cfg_.coeffs, &shape) || shape.blocks < 2) return nullptr;
   // Groups whose joint windows read ghost columns (all their chunks are outer).
   std::vector<std::uint8_t> ghost(size_t(shape.groups), 0);
   for (index_t g = 0; g < shape.groups; ++g) {
     const index_t x0 = g * shape.owg - shape.read_lead;
     ghost[size_t(g)] = (x0 < 0 || x0 + shape.read_span > tile_.width) ? 1 : 0;
   }
-  auto env_num = [](const char* k, double dflt) {
-    const char* e = std::getenv(k);
-    return e && *e ? std::atof(e) : dflt;
+  auto env_num = [](const char* k, double dflt) {  // experiments build only
+    const char* e = experiment_env(k);
+    return e ? std::atof(e) : dflt;
   };
   auto hl = std::make_unique<HaloLastPass>();
   hl->S = S;
@@ -708,7 +700,7 @@ bool StencilSolver<T>::halo_last(int S) const {
   for (const auto& h : halo_lasts_)
     if (h->S == S) return true;
   return std::find(no_halo_last_.begin(), no_halo_last_.end(), S) == no_halo_last_.end() &&
-         kernels::frame_pass_shape<T>(tile_, S, cfg_.coeffs, nullptr);
+         kernels::chunk_pass_shape<T>(tile_, S, cfg_.coeffs, nullptr);
 }
 
 // One interior-first super-step, cur -> nxt. cur must be complete (the side
@@ -719,7 +711,7 @@ bool StencilSolver<T>::halo_last(int S) const {
 // first, so it holds its CUs before RCCL's kernels look for free ones; with
 // streams that share a hardware queue everything simply runs in order.
 template <typename T>
-void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl) {
+void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks* marks) {
   MXS_TRACE_RANGE("stencil.superstep_halo_last");
   hipStream_t m = main_.get(), side = side_.get();
   join_side();
@@ -732,23 +724,49 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl) {
     fork_.record(m);
     fork_.wait_on(side);
   }
-  kernels::stencil5_frame_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->inner_shape, hl->inner_table.get(),
-                                  hl->sched.inner.entries, frame_ctl_.get(), side);
+  if (marks) marks->mark("side:start", side);
+  kernels::stencil5_chunk_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->inner_shape, hl->inner_table.get(),
+                                  hl->sched.inner.entries, side);
+  if (marks) marks->mark("side:inner chunks", side);
   side_pending_ = true;
   // One-wave copy workgroups sized from the segments (they fit beside the inner
-  // launch's workgroups). MXS_HALO_LAST_COPY_WGS (experiments): 4-wave
+  // launch's workgroups). MXS_HALO_LAST_COPY_WGS (experiments build): 4-wave
   // workgroups, that many per segment; 4 per segment made the exchange so slow
   // that the 8-GPU-tile opening took 0.415 ms instead of 0.264.
   static const int copy_wgs = [] {
-    const char* e = std::getenv("MXS_HALO_LAST_COPY_WGS");
-    return e && *e ? std::atoi(e) : 0;
+    const char* e = experiment_env("MXS_HALO_LAST_COPY_WGS");
+    return e ? std::atoi(e) : 0;
   }();
   ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
   ex_->set_copy_grid(copy_wgs);
-  ex_->exchange(cur, m);
+  if (marks) {
+    marks->mark("main:start", m);
+    ex_->pack(cur, m);
+    marks->mark("main:pack", m);
+    ex_->transfer(m);
+    marks->mark("main:rccl", m);
+    ex_->unpack(cur, m);
+    marks->mark("main:unpack", m);
+  } else {
+    ex_->exchange(cur, m);
+  }
   ex_->set_copy_grid(0);
-  kernels::stencil5_frame_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->outer_shape, hl->outer_table.get(),
-                                  hl->sched.outer.entries, frame_ctl_.get(), m);
+  ex_->set_copy_block(0);
+  kernels::stencil5_chunk_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->outer_shape, hl->outer_table.get(),
+                                  hl->sched.outer.entries, m);
+  if (marks) marks->mark("main:outer chunks", m);
+}
+
+template <typename T>
+void StencilSolver<T>::enqueue_opening(int S, bool advance) {
+  if (HaloLastPass* hl = halo_last_pass(S, true)) {
+    enqueue_halo_last(cur_, nxt_, hl);
+  } else {  // no chunk-list form on this tile: the same one exchange, then the pass
+    join_side();
+    ex_->exchange(cur_, main_.get());
+    enqueue_bare_pass(cur_, nxt_, S);
+  }
+  if (advance) std::swap(cur_, nxt_);
 }
 
 template <typename T>
@@ -760,58 +778,48 @@ void StencilSolver<T>::join_side() {
 }
 
 template <typename T>
-const kernels::FrameSchedule* StencilSolver<T>::frame_schedule(int S) {
-  FramePass* f = frame_pass(S, true);
-  return f ? &f->sched : nullptr;
-}
-
-template <typename T>
 void StencilSolver<T>::prepare(int iters) {
   MXS_TRACE_RANGE("stencil.prepare");
-  begin_run();
+  maybe_stall("prepare");
+  begin_run(true);
   Group gr[2];
   split(iters, gr);
-  // frame_auto: decide the schedule at the depth of the larger group.
+  // Opening::Auto: decide the opening at the depth of the larger group.
   const Group& big = gr[0].count >= gr[1].count ? gr[0] : gr[1];
-  if (big.count > 0) choose_schedule(big.S);
+  if (big.count > 0) choose_opening(big.S);
+  // Every collective below is issued the same number of times on every rank,
+  // whatever this rank's forms and decisions: one priming exchange when the
+  // ring is stale, then per cold size one opening (one exchange) when the
+  // interior-first opening is on and one super-step (one exchange).
   for (const Group& g : gr) {
     if (g.count <= 0) continue;
-    (void)frame_pass(g.S, true);
-    const bool cold = std::find(warmed_.begin(), warmed_.end(), g.S) == warmed_.end();
-    if (HaloLastPass* hl = halo_last_pass(g.S, true); hl && cold) {
-      enqueue_halo_last(cur_, nxt_, hl);  // cur -> nxt (scratch), cur's ring re-exchanged: state unchanged
-      join_side();
-    }
     if (post_exchange() && !ghost_fresh_) {
       ex_->exchange(cur_, main_.get());
       ghost_fresh_ = true;
     }
-    if (!frame_pass(g.S, false)) (void)graphs_for(g.S, g.count);
+    (void)graphs_for(g.S, g.count);
     if (std::find(warmed_.begin(), warmed_.end(), g.S) != warmed_.end()) continue;
     // One untimed launch of every kernel of this super-step size: cur -> nxt
-    // without swapping (nxt is scratch; the exchange rewrites cur's ghost ring
+    // without swapping (nxt is scratch; the exchanges rewrite cur's ghost ring
     // with the same values a real super-step would).
-    enqueue_block(cur_, nxt_, g.S);
-    // With peers a call ends on a bare pass (run_group): after a frame-first
-    // super-step that is the other kernel.
-    if (multi_rank_ && post_exchange() && frame_pass(g.S, false)) {
+    if (halo_last_on_ && post_exchange()) {
+      enqueue_opening(g.S, false);
       join_side();
-      enqueue_bare_pass(cur_, nxt_, g.S);
     }
+    enqueue_block(cur_, nxt_, g.S);
     warmed_.push_back(g.S);
   }
   join_side();
-  main_.sync();
-  side_.sync();
+  wait_idle("prepare");
 }
 
 template <typename T>
 void StencilSolver<T>::warm(int iters, int passes) {
   MXS_TRACE_RANGE("stencil.warm");
-  begin_run();
+  maybe_stall("warm");
+  begin_run(true);
   Group gr[2];
   split(iters, gr);
-  for (const Group& g : gr) (void)frame_pass(g.S, g.count > 0);
   if (post_exchange() && !ghost_fresh_) {
     ex_->exchange(cur_, main_.get());
     ghost_fresh_ = true;
@@ -820,8 +828,91 @@ void StencilSolver<T>::warm(int iters, int passes) {
     for (const Group& g : gr)
       if (g.count > 0) enqueue_block(cur_, nxt_, g.S);  // cur -> nxt, no swap: state unchanged
   join_side();
-  main_.sync();
-  side_.sync();
+  wait_idle("warm");
+}
+
+template <typename T>
+WindowPhases StencilSolver<T>::profile_window(int iters) {
+  MXS_TRACE_RANGE("stencil.profile_window");
+  WindowPhases out;
+  if (iters <= 0) return out;
+  maybe_stall("profile_window");
+  begin_run(true);
+  Group gr[2];
+  split(iters, gr);
+  const int S = gr[0].count > 0 ? gr[0].S : gr[1].S;
+  const int supersteps = gr[0].count + gr[1].count;
+  const index_t w = tile_.width, h = tile_.height;
+  hipStream_t m = main_.get();
+  if (direct_ || (!fused_ && !post_exchange())) {
+    out.opening = direct_ ? "direct (not profiled)" : "overlap (not profiled)";
+    return out;
+  }
+  join_side();
+  wait_idle("profile_window");
+  device_barrier("profile_window");
+  Marks marks;
+  const auto t0 = std::chrono::steady_clock::now();
+  HaloLastPass* hl = nullptr;
+  if (!fused_ && halo_last_on_ && !ghost_fresh_) hl = halo_last_pass(S, true);
+  if (fused_) {  // the whole super-step is one wrap-around pass
+    out.opening = "fused";
+    marks.mark("main:start", m);
+    enqueue_block(cur_, nxt_, S);
+    marks.mark("main:pass", m);
+  } else {
+    auto exchange = [&](T* tile) {
+      ex_->pack(tile, m);
+      marks.mark("main:pack", m);
+      ex_->transfer(m);
+      marks.mark("main:rccl", m);
+      ex_->unpack(tile, m);
+      marks.mark("main:unpack", m);
+      ++out.exchanges;
+    };
+    if (hl) {
+      out.opening = "interior-first";
+      enqueue_halo_last(cur_, nxt_, hl, &marks);
+      ++out.exchanges;
+      join_side();
+    } else {
+      out.opening = ghost_fresh_ ? "fresh" : "serial";
+      marks.mark("main:start", m);
+      if (!ghost_fresh_) exchange(cur_);
+      update(cur_, nxt_, S, 0, w, 0, h, m);
+      marks.mark("main:pass", m);
+    }
+    // The window's first super-step has its own exchange unless it is the
+    // call's bare last one (peers): nxt is scratch, its ring is rewritten.
+    // Issued on every rank alike, whichever opening it ran.
+    if (!(multi_rank_ && supersteps == 1)) exchange(nxt_);
+  }
+  out.host_enqueue_us =
+      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  join_side();
+  wait_idle("profile_window");
+  out.wall_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  // Phases: each marker closes the interval since the previous marker of its stream.
+  const Event* first = nullptr;
+  for (const auto& e : marks.ev)
+    if (!first || e->since(*first) < 0) first = e.get();
+  std::vector<std::pair<std::string, double>> last_on;  // stream prefix -> last marker time
+  for (size_t i = 0; i < marks.ev.size(); ++i) {
+    const double t = double(marks.ev[i]->since(*first)) * 1e3;
+    const std::string& nm = marks.name[i];
+    const std::string stream = nm.substr(0, nm.find(':'));
+    const std::string phase = nm.substr(nm.find(':') + 1);
+    auto it = std::find_if(last_on.begin(), last_on.end(), [&](const auto& p) { return p.first == stream; });
+    if (it == last_on.end()) {
+      last_on.emplace_back(stream, t);
+    } else {
+      out.phases.emplace_back(stream + ":" + phase, it->second, t);
+      it->second = t;
+    }
+    out.gpu_span_us = std::max(out.gpu_span_us, t);
+  }
+  ghost_fresh_ = false;  // conservative: the next call re-primes
+  return out;
 }
 
 template <typename T>
@@ -838,21 +929,12 @@ void StencilSolver<T>::exchange_only() {
 
 template <typename T>
 void StencilSolver<T>::synchronize() {
-  // With a remote peer and a watchdog timeout, wait by polling so a dead or
-  // hung peer fails the job instead of blocking it (SURVEY §5.3).
-  if (comm_ && comm_timeout() > 0) comm_->wait(main_.get(), "stencil halo exchange (RCCL)");
   // Direct halo: also wait for the neighbours' pushes into our tiles, so the
   // field (ghost ring included) is final and no peer still writes into it.
   if (direct_) direct_->wait(main_.get());
-  main_.spin_sync();
-  side_.spin_sync();
-  side_pending_ = false;  // both streams drained: nothing for main to wait for
-  ex_->check();  // IPC backend: device-side waits carry their own deadline
-  if (direct_) direct_->check();
-  if (frame_status_.get()) {
-    const unsigned st = __atomic_load_n(frame_status_.get(), __ATOMIC_ACQUIRE);
-    MXS_CHECK(st == 0, "frame-first pass: the halo exchange's wait for the pass's frame counter hit its deadline");
-  }
+  // With a remote peer and a watchdog timeout, wait by polling so a dead or
+  // hung peer fails the job instead of blocking it (SURVEY §5.3).
+  wait_idle("stencil halo exchange (RCCL)");
 }
 
 template class StencilSolver<float>;

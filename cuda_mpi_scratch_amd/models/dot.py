@@ -124,6 +124,34 @@ class DotProduct:
         dt = self.ctx.allreduce_max((time.perf_counter() - t0) / reps)
         return float(res.item()), dt
 
+    def breakdown(self, reps: int = 10) -> dict:
+        """Event-timed phases of one global dot on the current stream, median over
+        ``reps`` (GPU only): ``kernel_us`` = the local reduction (counter reset +
+        reduction kernel, reference mpicuda4.cu:347-355), ``allreduce_us`` = the
+        RCCL all-reduce of the partial (mpicuda4.cu:368; 0 on one rank). The
+        wall-clock figure of :meth:`timed` also carries the host's launches
+        between reps; this separates the device's own time from it."""
+        if not self.x.is_cuda:
+            return {}
+        s = torch.cuda.current_stream()
+        ks, ars = [], []
+        for _ in range(max(1, reps)):
+            e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+            e0.record(s)
+            part = self.local()
+            e1.record(s)
+            if self.ctx.world_size > 1 and self.comm is not None:
+                self.comm.allreduce_sum(part.data_ptr(), self.total.data_ptr(), 1, "f64", s.cuda_stream)
+            e2.record(s)
+            if self.comm is not None:
+                self.comm.wait(s.cuda_stream, "dot all-reduce")
+            torch.cuda.synchronize()
+            ks.append(e0.elapsed_time(e1) * 1e3)
+            ars.append(e1.elapsed_time(e2) * 1e3)
+        ks.sort()
+        ars.sort()
+        return {"kernel_us": ks[len(ks) // 2], "allreduce_us": ars[len(ars) // 2]}
+
     @property
     def bytes_read(self) -> int:
         """HBM bytes one global dot reads (both vectors, all ranks)."""

@@ -77,20 +77,17 @@ class StencilConfig:
     # different GPUs unless MXS_IPC_CROSS_DEVICE=1 (verified only for ranks
     # sharing one GPU: halo/ipc_transport.hpp ipc_check_devices).
     direct_halo: bool | None = None
-    # RCCL backend with remote peers: frame-first overlap — each pass stores its
-    # S-deep output frame first and the next halo exchange (pack -> RCCL ->
-    # unpack) runs under the rest of the pass (runtime/stencil_solver.hpp).
-    # True forces it, False never, None (default) lets prepare() time both
-    # schedules and keep the faster (on one GPU through RCCL loopback: serial,
-    # docs/PERF.md).
-    frame_overlap: bool | None = None
-    frame_comm_wgs: int = -1         # frame-only workgroups leaving CUs to the exchange (-1 = default)
-    frame_rows: int = 0              # frame chunk height (0 = auto)
-    # Interior-first opening: a call's first super-step, which starts with a
-    # priming exchange (with peers: every call), runs its core chunks while that
-    # exchange runs on the CUs they leave free. True forces it; with
-    # frame_overlap=None prepare() times it against the serial opening.
-    halo_last: bool = False
+    # Opening super-step of a call with peers (RCCL): its priming exchange runs
+    # under the chunks that read only core cells ("interior-first") or before
+    # the pass ("serial"). "auto" (default): prepare() times both on every rank,
+    # agrees the worst-rank medians and keeps interior-first only when it wins
+    # by >= min_gain and by more than the measured spread.
+    opening: str = "auto"
+    min_gain: float = 0.03
+    # Single GPU with loopback: follow the peers' schedule (every call primes,
+    # the last pass of a call is bare, the opening is chosen as with peers), so
+    # one GPU rehearses the window an N-GPU run executes.
+    rehearse_peers: bool = False
     # Super-steps estimated longer than this run from eager launches, not a
     # hipGraph (long passes: eager measured faster). 0 = always graphs.
     graph_max_superstep_us: float = 150.0
@@ -122,6 +119,10 @@ class Stencil2D:
         self.sum_form = bool(cfg.sum_form and cfg.c_center == cfg.c_neighbor)
         if tb <= 0 and dev.type == "cuda":
             tb = hip().auto_time_block(d.width, d.height, cfg.dtype, self.sum_form)
+            # The time block sets the ghost depth and the exchanges per call: the
+            # same on every rank (an uneven decomposition gives ranks different
+            # tile sizes, and the per-tile default could differ).
+            tb = int(self.ctx.allreduce_min(tb))
         # A physical (non-periodic) edge holds fixed boundary values that the
         # S-step kernels would advance as cells: time blocking needs every edge
         # to be a neighbour's (the native solver enforces the same rule).
@@ -172,7 +173,12 @@ class Stencil2D:
             torch.cuda.synchronize()
             kind = H.StencilKind.BOX if cfg.kind == "box" else H.StencilKind.JACOBI5
             be = {"rccl": H.HaloBackend.RCCL, "local": H.HaloBackend.LOCAL, "ipc": H.HaloBackend.IPC}[backend]
-            boot = self.ctx.allgather_bytes if backend == "ipc" else None
+            # Host allgather: the IPC backend's set-up and the solver's collective
+            # agreements (time block, opening, sum-form range) without RCCL.
+            boot = None
+            if backend == "ipc" or (self.ctx.world_size > 1 and backend != "rccl"):
+                def boot(blob: bytes, _ctx=self.ctx, _H=H) -> list[bytes]:
+                    return _ctx.allgather_bytes(blob, timeout_s=_H.comm_timeout() or None)
             weights = [float(w) for w in cfg.box_weights] if cfg.kind == "box" else []
             radius = (int(round(math.sqrt(len(weights)))) - 1) // 2 if weights else 1
             self.solver = H.StencilSolver(d.topo, d.rank, self.geom, self.a.data_ptr(), self.b.data_ptr(), self.comm,
@@ -180,9 +186,7 @@ class Stencil2D:
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
                                           backend == "ipc" and cfg.direct_halo is not False,
-                                          bool(cfg.frame_overlap), cfg.frame_comm_wgs, cfg.frame_rows,
-                                          cfg.graph_max_superstep_us, cfg.frame_overlap is None and not cfg.halo_last,
-                                          cfg.halo_last)
+                                          cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
@@ -214,6 +218,7 @@ class Stencil2D:
         if self.solver is not None:
             self.solver.run(iters)
             return
+        self._last_iters = iters
         for _ in range(iters):
             self._python_step()
 
@@ -290,7 +295,7 @@ class Stencil2D:
         """(S, count) of the super-steps the last run() executed."""
         if self.solver is not None:
             return [tuple(x) for x in self.solver.last_run_blocks()]
-        return [(1, 0)]
+        return [(1, getattr(self, "_last_iters", 0))]  # the torch path: one exchange + one step per iteration
 
     def full_view(self) -> torch.Tensor:
         """(total_height, total_width) logical view: core + ghost ring."""
@@ -339,30 +344,48 @@ class Stencil2D:
         return self.solver.graph_status() if self.solver is not None else "python loop"
 
     def halo_mode(self) -> str:
-        """How the halo is refreshed each iteration."""
+        """How the last run() refreshed the halo: what it executed (its super-steps,
+        their exchanges and the opening), not what the solver could do."""
         if self.solver is None:
-            return "torch-p2p"
-        tb = self.solver.time_block()
-        blk = (f", time-blocked x{tb} (one {tb}-deep exchange + one wave-streaming pass per {tb} iterations)"
-               if tb > 1 else "")
+            return "torch-p2p (one exchange per iteration)"
+        blocks = self.last_run_blocks()
+        steps = sum(s * n for s, n in blocks)
+        passes = sum(n for _, n in blocks)
+        if not passes:
+            return "no run yet"
+        shape = " + ".join(f"{n} x {s}-step" for s, n in blocks if n)
+        what = f"{steps} iterations as {shape} pass{'es' if passes > 1 else ''}"
         if self.solver.fused_periodic():
-            return "fused-periodic (1x1 self-exchange in the kernel addressing)" + blk
+            return f"{what}; no exchange (1x1 periodic: the self-halo is the kernel's wrap-around addressing)"
+        ex = self.solver.last_run_exchanges()
+        opening = self.solver.last_run_opening()
+        how = {"rccl": "RCCL send/recv per peer (pack -> ncclSend/ncclRecv -> unpack)",
+               "ipc": "HIP IPC", "local": "local self-copy"}.get(self.backend, self.backend)
         if self.solver.direct_halo():
-            return "ipc direct (device-initiated push of each pass's edge bands into the neighbours' tiles)" + blk
-        choice = self.solver.frame_choice()[0]
-        opening = ""
-        if tb > 1 and self.solver.halo_last(tb):
-            opening = (" + interior-first opening (a call's priming exchange runs under the chunks that read only "
-                       "core cells; the ghost-ring chunks follow on the CUs left free)")
-        if tb > 1 and self.solver.frame_overlap(tb):
-            return (f"{self.backend} + frame-first overlap (each pass stores its {tb}-deep output frame first; "
-                    f"the next halo's pack -> RCCL send/recv -> unpack runs under the rest of the pass)" + opening + blk)
-        if opening:
-            return f"{self.backend}" + opening + blk
-        mode = " + overlap" if self.solver.overlapped() else ""
-        if not mode and tb > 1 and self.backend == "rccl" and choice == "serial":
-            mode = " (pass, then halo exchange; prepare() measured the overlapped schedules slower)"
-        return f"{self.backend}" + mode + blk
+            how = "HIP IPC direct push of each pass's edge bands into the neighbours' tiles"
+        text = f"{what}; {ex} halo exchange{'s' if ex != 1 else ''} by {how}"
+        if opening == "interior-first":
+            text += ("; opening interior-first (the priming exchange ran under the chunks that read only core "
+                     "cells, the ghost-ring chunks after it)")
+        elif opening == "serial":
+            text += "; opening serial (priming exchange, then the pass)"
+        elif opening == "overlap":
+            text += "; thin-strip overlap (interior on a second stream while each exchange runs)"
+        if self.solver.multi_rank() and not self.solver.direct_halo() and not self.solver.overlapped():
+            text += "; the call's last pass is bare (the next call primes)"
+        return text
+
+    def profile_window(self, iters: int) -> dict:
+        """Collective, state-preserving: one event-timed replica of ``run(iters)``'s
+        opening super-step (host enqueue, pack / RCCL / unpack, passes, tail)."""
+        if self.solver is None:
+            return {}
+        p = self.solver.profile_window(iters)
+        return {"opening": p["opening"], "exchanges": p["exchanges"],
+                "host_enqueue_us": round(p["host_enqueue_us"], 1), "gpu_span_us": round(p["gpu_span_us"], 1),
+                "wall_us": round(p["wall_us"], 1),
+                "host_overhead_us": round(p["wall_us"] - p["gpu_span_us"], 1),
+                "phases_us": {name: [round(t0, 1), round(t1, 1)] for name, t0, t1 in p["phases"]}}
 
     # ----------------------------------------------------------------- dump
     def dump_text(self, stage_arrays: list[tuple[str, torch.Tensor]], device_id: int | None = None,
@@ -412,6 +435,7 @@ def main(argv=None) -> int:
     p.add_argument("--loopback", action="store_true")
     p.add_argument("--variant", default="auto", choices=["auto", "roll", "lds"])
     p.add_argument("--time-block", type=int, default=StencilConfig.time_block)
+    p.add_argument("--opening", default="auto", choices=["auto", "serial", "interior-first"])
     p.add_argument("--seed", type=int, default=StencilConfig.seed)
     p.add_argument("--checkpoint", default=None, help="write the final field to this grid file")
     p.add_argument("--resume", default=None, help="start from this grid file (any decomposition)")
@@ -427,7 +451,7 @@ def main(argv=None) -> int:
     cfg = StencilConfig(global_width=gw, global_height=gh, dims=f"{rows}x{cols}", dtype=args.dtype,
                         backend=args.backend, overlap=False if args.no_overlap else None, graph=not args.no_graph,
                         loopback=args.loopback, variant=args.variant, time_block=args.time_block,
-                        seed=args.seed)
+                        seed=args.seed, opening=args.opening)
     st = Stencil2D(cfg, ctx)
     if args.resume:
         hdr = st.load_checkpoint(args.resume)

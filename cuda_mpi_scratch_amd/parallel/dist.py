@@ -105,15 +105,25 @@ class DistContext:
             return payload
         return bytes(store.get(k))
 
-    def allgather_bytes(self, payload: bytes, key: str | None = None) -> list[bytes]:
+    def allgather_bytes(self, payload: bytes, key: str | None = None, timeout_s: float | None = None) -> list[bytes]:
         """Every rank contributes a byte string, every rank gets all of them in rank
-        order (through the rendezvous store: control-plane sized payloads only)."""
+        order (through the rendezvous store: control-plane sized payloads only).
+        ``timeout_s``: fail (naming the missing ranks) instead of waiting for a
+        dead or hung peer up to the process group's timeout."""
         if not self.is_distributed:
             return [payload]
         store = dist.distributed_c10d._get_default_store()
         k = key or f"mxs/allgather/{next(_uid_counter)}"
         store.set(f"{k}/{self.rank}", payload)
-        return [bytes(store.get(f"{k}/{r}")) for r in range(self.world_size)]
+        keys = [f"{k}/{r}" for r in range(self.world_size)]
+        if timeout_s:
+            try:
+                store.wait(keys, datetime.timedelta(seconds=timeout_s))
+            except Exception as e:  # noqa: BLE001 - re-raised with the ranks that are missing
+                missing = [r for r, kk in enumerate(keys) if not store.check([kk])]
+                raise TimeoutError(f"host allgather {k}: ranks {missing} did not arrive within {timeout_s:g} s "
+                                   f"(a peer rank is dead or hung): {e}") from e
+        return [bytes(store.get(kk)) for kk in keys]
 
     def destroy(self) -> None:
         self._native_comm = None  # workloads still holding it keep it alive

@@ -1,0 +1,136 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces the per-experiment gpu_r0*_*.sh
+# wrappers). Every GPU step runs under its own time limit; a failing step ends
+# the script with its status, so a gpurun call never starts GPU work after a
+# fault, abort or timeout.
+#
+#   gpurun -- bash scripts/gpu_task.sh OUT TASK [ARGS...]
+#
+# OUT is a directory under gpurun_out/. Tasks:
+#   tests [PYTEST ARGS]    pytest -m gpu (verbose, per-test limit) -> OUT/pytest_gpu.txt
+#   smoke                  __graft_entry__.smoke()                  -> OUT/smoke.txt
+#   bench [BENCH ARGS]     python bench.py ARGS                      -> OUT/bench.txt (JSON line echoed)
+#   prof NAME [BENCH ARGS] rocprofv3 --kernel-trace --stats of bench.py ARGS -> OUT/prof_NAME/
+#   window TILE REPS [--serial]
+#                          interleaved single-shot bench-flow windows on TILE: RCCL loopback in the
+#                          peers' schedule (auto opening, and forced serial with --serial) against the
+#                          fused-periodic tile (no exchange) -> OUT/window_TILE.jsonl + medians
+#   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
+#   final                  tests + smoke + the driver's bench command + its kernel-trace profile
+set -uo pipefail
+OUT="gpurun_out/${1:?usage: gpu_task.sh OUT TASK [ARGS...]}"
+TASK="${2:?usage: gpu_task.sh OUT TASK [ARGS...]}"
+shift 2
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+ROOT=$(pwd)
+mkdir -p "$OUT"
+export TMPDIR=/tmp PYTHONUNBUFFERED=1
+
+step() {  # step LIMIT LOG CMD...: run CMD under LIMIT seconds, log to LOG, stop the script on failure
+  local limit=$1 log=$2
+  shift 2
+  timeout -k 10 "$limit" "$@" > "$log" 2>&1
+  local rc=$?
+  if [ "$rc" -ne 0 ]; then
+    echo "step failed (rc=$rc): $*"
+    tail -30 "$log"
+    exit "$rc"
+  fi
+}
+
+task_tests() {
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider "$@" \
+    > "$OUT/pytest_gpu.txt" 2>&1
+  local rc=$?
+  echo "pytest rc=$rc"
+  tail -3 "$OUT/pytest_gpu.txt"
+  grep -E "^(FAILED|ERROR)" "$OUT/pytest_gpu.txt" | head -20 || true
+  return "$rc"
+}
+
+task_smoke() {
+  step 300 "$OUT/smoke.txt" python -c "import __graft_entry__ as g; g.smoke()"
+  tail -1 "$OUT/smoke.txt"
+}
+
+task_bench() {
+  step 600 "$OUT/bench.txt" python bench.py "$@"
+  grep "^{" "$OUT/bench.txt" | tail -1
+}
+
+task_prof() {
+  local name=$1
+  shift
+  (cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/prof_$name" -o bench \
+    -- python3 "$ROOT/bench.py" "$@") > "$OUT/prof_$name.txt" 2>&1
+  local rc=$?
+  if [ "$rc" -ne 0 ]; then
+    echo "prof failed (rc=$rc)"
+    tail -30 "$OUT/prof_$name.txt"
+    exit "$rc"
+  fi
+  find "$OUT/prof_$name" -name "*kernel_trace.csv" -size +20M -delete
+  python scripts/prof_summary.py "$OUT/prof_$name" > "$OUT/prof_${name}_summary.md" 2>/dev/null || true
+  grep "^{" "$OUT/prof_$name.txt" | tail -1
+}
+
+task_window() {
+  local tile=$1 reps=$2 serial=${3:-}
+  local log="$OUT/window_$tile.jsonl"
+  : > "$log"
+  local modes="auto fused"
+  [ "$serial" = "--serial" ] && modes="auto serial fused"
+  for i in $(seq "$reps"); do
+    for mode in $modes; do
+      local args=(--global "$tile" --steps 20 --warmup 5 --no-extras)
+      local envs=()
+      case $mode in
+        auto) args+=(--loopback); envs=(MXS_PEER_SCHEDULE=1) ;;
+        serial) args+=(--loopback --opening serial); envs=(MXS_PEER_SCHEDULE=1) ;;
+        fused) ;;
+      esac
+      env "${envs[@]}" timeout -k 10 200 python bench.py "${args[@]}" > "$OUT/window_last.txt" 2>&1 || {
+        echo "window run failed ($mode)"
+        tail -30 "$OUT/window_last.txt"
+        exit 1
+      }
+      python - "$OUT/window_last.txt" "$mode" >> "$log" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1]); e = d["extras"]
+print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["ms_per_step"] * d["steps"], 4),
+                  "opening": e.get("opening"), "phases": e.get("window_phases")}))
+PY
+    done
+  done
+  python - "$log" <<'PY'
+import json, sys
+rs = [json.loads(l) for l in open(sys.argv[1])]
+for m in ("auto", "serial", "fused"):
+    v = sorted(r["window_ms"] for r in rs if r["mode"] == m)
+    if v:
+        print(m, "n", len(v), "median", v[len(v) // 2], "min", v[0], "max", v[-1])
+PY
+}
+
+task_py() {
+  step 900 "$OUT/py.txt" python "$@"
+  tail -20 "$OUT/py.txt"
+}
+
+task_final() {
+  task_tests || exit $?
+  task_smoke
+  task_bench --steps 20 --warmup 5
+  task_prof driver --steps 20 --warmup 5
+}
+
+case "$TASK" in
+  tests) task_tests "$@" ;;
+  smoke) task_smoke ;;
+  bench) task_bench "$@" ;;
+  prof) task_prof "$@" ;;
+  window) task_window "$@" ;;
+  py) task_py "$@" ;;
+  final) task_final ;;
+  *) echo "unknown task '$TASK'"; exit 2 ;;
+esac

@@ -32,18 +32,52 @@ def run_ranks(task: str, nprocs: int, args: dict, timeout: int = 240, gpu: bool 
     return _run_once(task, nprocs, args, timeout, gpu)
 
 
+def run_ranks_raw(task: str, nprocs: int, args: dict, timeout: int = 240, gpu: bool = False) -> list[dict]:
+    """Like run_ranks, but a failing rank is a result, not an error: per rank
+    {"rc", "stdout", "stderr", "seconds"} (failure-path tests)."""
+    import time
+
+    port = free_port()
+    procs = []
+    t0 = time.monotonic()
+    for r in range(nprocs):
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "mp_worker.py"), task, json.dumps(args)],
+                                      env=_rank_env(r, nprocs, port, gpu), stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    out = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=timeout)
+            out.append({"rc": p.returncode, "stdout": o, "stderr": e, "seconds": time.monotonic() - t0})
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                pass
+    return out
+
+
+def _rank_env(r: int, nprocs: int, port: int, gpu: bool) -> dict:
+    env = dict(os.environ)
+    env.update(RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(nprocs),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1",
+               HSA_ENABLE_IPC_MODE_LEGACY="0")
+    if not gpu:
+        env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    return env
+
+
 def _run_once(task, nprocs, args, timeout, gpu):
     port = free_port()
     procs = []
     for r in range(nprocs):
-        env = dict(os.environ)
-        env.update(RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(nprocs),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="1",
-                   HSA_ENABLE_IPC_MODE_LEGACY="0")
-        if not gpu:
-            env.update(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "mp_worker.py"), task, json.dumps(args)],
-                                      env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+                                      env=_rank_env(r, nprocs, port, gpu), stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
     results = []
     try:
         for p in procs:

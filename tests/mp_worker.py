@@ -79,21 +79,31 @@ def task_bench(args):
 
 
 def task_gpu_solver(args):
-    """Native solver on a shared GPU (IPC halo backend): random init, N iterations,
-    global grid back on rank 0."""
+    """Native solver on GPU (IPC halo backend on a shared GPU, RCCL one rank per
+    GPU): random init, N iterations, global grid back on rank 0."""
     ctx = init(backend="gloo", device="cuda")
+    if args.get("comm_timeout"):
+        from cuda_mpi_scratch_amd import hip
+
+        hip().set_comm_timeout(float(args["comm_timeout"]))
     cfg = StencilConfig(global_width=args["w"], global_height=args["h"], dims=args["dims"],
                         dtype=args.get("dtype", "f32"), seed=args.get("seed", 5), backend=args.get("backend", "auto"),
                         overlap=args.get("overlap", True), graph=args.get("graph", True),
                         time_block=args.get("time_block", 12), direct_halo=args.get("direct", None),
-                        sum_form=args.get("sum_form", True), frame_overlap=args.get("frame_overlap", None),
-                        halo_last=args.get("halo_last", False))
+                        sum_form=args.get("sum_form", True), opening=args.get("opening", "auto"),
+                        min_gain=args.get("min_gain", 0.03))
     st = Stencil2D(cfg, ctx)
+    stall = args.get("stall")
+    if stall and ctx.rank == stall["rank"]:
+        st.solver.inject_stall(stall["phase"], float(stall["seconds"]))
+    if args.get("warmup_first"):
+        st.run(args["warmup_first"])
     if args.get("prepare"):
         st.prepare(args["prepare"])
     if args.get("warm"):
         assert st.warm(args["warm"], 0.01) >= 1  # untimed, state-preserving passes (collective)
-    per_run = []
+    phases = st.profile_window(args["profile"]) if args.get("profile") else None
+    per_run, openings = [], []
     for n in args.get("runs", [args["iters"]]):
         if args.get("rank0_reads") and ctx.rank == 0:
             st.synchronize()
@@ -101,14 +111,20 @@ def task_gpu_solver(args):
         st.run(n)
         if st.solver is not None:
             per_run.append([int(st.solver.last_run_exchanges()), sum(c for _, c in st.solver.last_run_blocks())])
+            openings.append(st.solver.last_run_opening())
     st.synchronize()
     g = st.gather_global()
     out = {"rank": ctx.rank, "backend": st.backend, "halo": st.halo_mode(), "graph": st.graph_status(),
            "native": st.solver is not None, "time_block": st.time_block}
     if st.solver is not None:
-        out["choice"] = list(st.solver.frame_choice())
-        out["frame"] = bool(st.solver.frame_overlap(st.time_block))
+        out["choice"] = dict(st.solver.schedule_times())
+        out["halo_last"] = bool(st.solver.halo_last(st.time_block))
         out["exchanges"] = per_run  # halo exchanges each run() enqueued, and its super-steps
+        out["openings"] = openings
+        out["phases"] = phases
+        if st.comm is not None:
+            out["rccl_ranks"] = int(st.comm.count())
+            out["rccl_device"] = int(st.comm.device())
     if ctx.rank == 0:
         out["grid"] = g.double().tolist()
     ctx.barrier()

@@ -172,25 +172,23 @@ def test_pingpong_ipc_reference_output(gpu):
     assert r.stdout.startswith("PASSED\nMessage size(MB): 1\nRound-trip time(ms): ")
 
 
-@pytest.mark.parametrize("mode", ["--frame-overlap", "--no-frame-overlap", "--halo-last", None])
+@pytest.mark.parametrize("mode", [("--opening", "serial"), ("--opening", "interior-first"), ("--halo-last",), None])
 def test_stencil_gpu_schedules_at_production_depth(gpu, tmp_path, mode):
-    """The app's multi-GPU schedules through RCCL loopback at S = 20 (per-step
-    form): frame-first, serial, the interior-first opening and the measured
-    choice give the same checksum, bit for bit, and agree with the CPU app."""
+    """The app's multi-GPU openings through RCCL loopback at S = 20 (per-step
+    form): serial, interior-first (also as --halo-last) and the measured choice
+    give the same checksum, bit for bit, and agree with the CPU app."""
     args = ["--global", "4096x2048", "--dims", "1x1", "--dtype", "f32", "--iters", "40", "--stencil", "3"]
-    extra = ["--loopback", "--time-block", "20", "--no-sum-form", "--no-overlap"] + ([mode] if mode else [])
+    extra = ["--loopback", "--time-block", "20", "--no-sum-form", "--no-overlap"] + (list(mode) if mode else [])
     g = mpirun(1, "stencil2d", *args, "--checksum", "--warmup", "0", *extra, cwd=tmp_path)
     assert g.returncode == 0, g.stderr[-3000:]
     js = g.stdout.strip().splitlines()[-1]
     assert '"time_block": 20' in js
-    if mode == "--frame-overlap":
-        assert '"frame_first": true' in js
-    elif mode == "--no-frame-overlap":
-        assert '"frame_first": false' in js
-    elif mode == "--halo-last":
-        assert '"interior_first_opening": true' in js
+    if mode == ("--opening", "serial"):
+        assert '"interior_first_opening": false' in js and '"opening_choice": "serial"' in js
+    elif mode is not None:
+        assert '"interior_first_opening": true' in js and '"opening_choice": "interior-first"' in js
     else:
-        assert '"schedule_choice": "' in js and '"opening_choice": "' in js
+        assert '"opening_choice": "' in js and '"last_opening": "' in js
     ref = mpirun(1, "stencil2d", *args, "--checksum", "--warmup", "0", "--time-block", "1", cwd=tmp_path)
     assert ref.returncode == 0, ref.stderr[-3000:]
     assert _checksum(g.stdout) == _checksum(ref.stdout)

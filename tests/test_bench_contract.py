@@ -2,8 +2,13 @@
 from rank 0 with the BASELINE metric, whole-job value, max-over-ranks timing and
 the multi-rank extras path (ping-pong errors are reported, never fatal)."""
 import json
+import os
+import sys
 
 from tests.mp_util import run_ranks
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
 
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config"}
@@ -22,6 +27,24 @@ def test_bench_single_rank_cpu():
     r = run_ranks("bench", 1, {"argv": ["--global", "128x96", "--steps", "6", "--warmup", "2", "--no-extras"]})
     d = _check(r[0]["line"], 1, 6, 2)
     assert d["config"]["parallelism"].startswith("cart1x1")
+    ex = d["extras"]
+    # The environment is on record (the launcher's RANK etc. are not runtime knobs).
+    assert isinstance(ex["env"], dict) and all(k.startswith(bench.ENV_PREFIXES) for k in ex["env"])
+
+
+def test_bench_env_record_and_refusal(monkeypatch):
+    """Every MXS_* / NCCL_* / ... variable that is set is recorded; an experiments
+    build (where the MXS_* tuning knobs take effect) with one set refuses to
+    report a headline, a release build (where they do nothing) reports it."""
+    monkeypatch.setenv("MXS_HALO_GRID", "16")
+    monkeypatch.setenv("NCCL_PROTO", "Simple")
+    monkeypatch.setenv("MXS_IPC_CROSS_DEVICE", "1")
+    env = bench.env_record()
+    assert env["MXS_HALO_GRID"] == "16" and env["NCCL_PROTO"] == "Simple" and "PATH" not in env
+    assert "MXS_HALO_GRID" in bench.refuse_reason(True, env)
+    assert bench.refuse_reason(False, env) is None
+    monkeypatch.delenv("MXS_HALO_GRID")
+    assert bench.refuse_reason(True, bench.env_record()) is None  # runtime settings are not tuning knobs
 
 
 def test_bench_single_rank_cpu_dot_extras():
@@ -59,3 +82,6 @@ def test_bench_eight_ranks_cpu_walks_the_8gpu_path():
     ex = d["extras"]
     assert ex["tile"] == "128x32" and ex["backend"] == "torch"
     assert ex["dot_65536_f64_verified"] is True and ex["pingpong_verified"] is True
+    # Self-description keys of an N > 1 record (GPU-only ones are absent on CPU).
+    assert ex["timed_super_steps"] == [[1, 3]] and ex["halo"].startswith("torch-p2p")
+    assert "pingpong_ipc" in ex and isinstance(ex["env"], dict)

@@ -1,9 +1,9 @@
-"""Host-side work schedules of the pipeline passes (kernels/frame_schedule.hpp),
+"""Host-side work schedules of the pipeline passes (kernels/chunk_schedule.hpp),
 checked on CPU: the fill-aware shares every pipeline pass uses, and the
-frame-first chunk lists of the overlapped multi-GPU pass. Every (group, row)
-must be covered exactly once, frame chunks must come first and hold the whole
-S-deep output frame, and the cost model (rows + one pipeline fill per chunk)
-must not get worse than the equal-share rule it replaced."""
+interior-first chunk lists of the multi-GPU opening super-step. Every (group,
+row) must be covered exactly once, no inner chunk may read the ghost ring, and
+the cost model (rows + one pipeline fill per chunk) must not get worse than the
+equal-share rule it replaced."""
 import pytest
 
 from cuda_mpi_scratch_amd._native import core
@@ -53,50 +53,6 @@ def test_balanced_starts_8192_gain():
     costs = _chunk_costs(st, 9, 8192, 47)
     old = _chunk_costs(_equal_starts(9, 8192, 256), 9, 8192, 47)
     assert max(old) == 382 and max(costs) <= 340
-
-
-@pytest.mark.parametrize("groups,rows,blocks,fill", SHAPES[:6] + [(2, 600, 256, 47), (1, 128, 256, 40)])
-@pytest.mark.parametrize("comm", [0, 8])
-@pytest.mark.parametrize("frame_rows", [0, 128])
-def test_frame_schedule_covers_frame_first(groups, rows, blocks, fill, comm, frame_rows):
-    d = C.frame_schedule(groups, rows, blocks, fill, frame_rows, comm)
-    assert d["check"] == ""
-    tab = d["table"]
-    assert len(tab) == blocks and d["signals"] == sum(1 for l in tab for c in l if c[3] & 1)
-    # The first comm_wgs workgroups run one frame chunk and nothing else.
-    for w in range(d["comm_wgs"]):
-        assert len(tab[w]) == 1 and tab[w][0][3] & 1
-    # Frame chunks are each workgroup's first chunk, at most one per workgroup.
-    for l in tab:
-        assert sum(c[3] & 1 for c in l) <= 1 and all(not (c[3] & 1) for c in l[1:])
-
-
-def test_frame_schedule_8gpu_tile_costs():
-    """The 8-GPU tile (18 groups x 8192 rows): the frame is stored within ~45% of
-    the pass, and the whole pass costs at most ~6% more than the fill-aware
-    serial shares (the price of the frame chunks' own fills and the comm CUs)."""
-    d = C.frame_schedule(18, 8192, 256, 47, 0, 8)
-    serial = max(_chunk_costs(C.balanced_starts(18, 8192, 256, 47), 18, 8192, 47))
-    assert d["frame_cost"] <= 0.45 * d["bulk_cost"]
-    assert d["bulk_cost"] <= 1.06 * serial
-
-
-def test_frame_schedule_edge_groups():
-    """A last group narrower than S: both of the last two groups are edge groups."""
-    d = C.frame_schedule(6, 1000, 256, 47, 100, 4, 1, 2)
-    assert d["check"] == ""
-    framed = {c[0] for l in d["table"] for c in l if c[3] & 1 and c[2] - c[1] < 1000 and (c[1], c[2]) != (0, 100)
-              and (c[1], c[2]) != (900, 1000)}
-    assert {0, 4, 5} <= framed
-
-
-def test_frame_schedule_raises_frame_rows_to_fit():
-    """Asked for more frame chunks than workgroups, the chunks grow until they fit;
-    only a grid with more groups than twice the workgroups is refused."""
-    d = C.frame_schedule(40, 100000, 64, 47, 64, 8)
-    assert d["check"] == "" and d["signals"] <= 64 and d["frame_rows"] > 64
-    with pytest.raises(ValueError, match="frame chunks"):
-        C.frame_schedule(200, 1000, 64, 47, 0, 8)
 
 
 def _ghost(groups):

@@ -1,9 +1,12 @@
 """bench.py end to end on the path an N > 1 rank times, rehearsed on one GPU:
 the 8-GPU tile (16384 x 8192) through RCCL loopback, in the peers' schedule
-(MXS_PEER_SCHEDULE=1: every call primes, the last pass of a call is bare). The
-driver's 20-step window must be exactly one exchange + one 20-level pipeline
-pass (serial, or the interior-first opening when prepare() measured it
-faster), and the record must say so."""
+(--rehearse-peers: every call primes, the last pass of a call is bare, the
+opening is chosen as with peers). The driver's 20-step window must be exactly
+one exchange + one 20-level pipeline pass (serial, or the interior-first opening
+when prepare() measured it faster on every rank), and the record must say so:
+the executed super-steps, the agreed decision and its timings, the phase
+breakdown of an untimed replica, the RCCL communicator's rank count and the
+environment."""
 import json
 import os
 import subprocess
@@ -17,9 +20,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_bench_8gpu_tile_window_through_loopback(gpu):
-    env = dict(os.environ, MXS_PEER_SCHEDULE="1", PYTHONUNBUFFERED="1")
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--global", "16384x8192", "--loopback",
-                        "--steps", "20", "--warmup", "5", "--no-extras", "--clock-warmup-ms", "50"],
+                        "--rehearse-peers", "--steps", "20", "--warmup", "5", "--no-extras", "--clock-warmup-ms", "50"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
@@ -30,11 +33,20 @@ def test_bench_8gpu_tile_window_through_loopback(gpu):
     assert ex["timed_super_steps"] == [[20, 1]]
     assert ex["timed_exchanges"] == 1  # the priming exchange; the pass is bare
     assert ex["sum_form_used"] is True
+    # The record describes what ran: one 20-step pass, one exchange, the opening.
+    assert ex["halo"].startswith("20 iterations as 1 x 20-step pass; 1 halo exchange by RCCL")
     sc = ex["schedule_choice"]
-    assert sc["chosen"] in ("serial", "frame") and sc["opening"] in ("serial", "halo-last")
+    assert sc["opening"] in ("serial", "interior-first") and sc["samples"] == 8 and sc["reason"]
     # The window is the call's opening super-step: interior-first when measured faster.
-    assert ex["halo_last"] == (sc["opening"] == "halo-last")
+    assert ex["opening"] == sc["opening"]
     # The interior-first opening runs the chunk-list form of the same pipeline kernel.
-    assert ex["stencil_kernel"] == ("stream_pipe_sum_frame" if ex["halo_last"] else "stream_pipe_sum")
+    assert ex["stencil_kernel"] == ("stream_pipe_sum_chunks" if ex["opening"] == "interior-first"
+                                    else "stream_pipe_sum")
+    assert ex["rccl_ranks"] == 1 and len(ex["rank_devices"]) == 1
+    ph = ex["window_phases"]
+    assert ph["opening"] == ex["opening"] and ph["exchanges"] == 1
+    assert {"main:pack", "main:rccl", "main:unpack"} <= set(ph["phases_us"])
+    assert ph["gpu_span_us"] > 0 and ph["wall_us"] > 0
+    assert isinstance(ex["env"], dict) and ex["experiments_build"] is False
     # 16384 x 8192 x 20 cell-updates: one pass (~0.25 ms) + one loopback exchange.
     assert d["value"] > 5000, d

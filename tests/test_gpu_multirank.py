@@ -7,7 +7,7 @@ import pytest
 import torch
 
 from cuda_mpi_scratch_amd.ops import jacobi_reference_global, random_values
-from tests.mp_util import run_ranks
+from tests.mp_util import run_ranks, run_ranks_raw
 
 pytestmark = pytest.mark.gpu
 
@@ -54,7 +54,7 @@ def test_ipc_direct_halo_matches_global_reference(gpu, n, dims, dtype, time_bloc
     iters = sum(runs)
     res = run_ranks("gpu_solver", n, {"w": w, "h": h, "dims": dims, "iters": iters, "runs": runs, "seed": seed,
                                       "dtype": dtype, "time_block": time_block, "direct": True}, gpu=True)
-    assert all(r["backend"] == "ipc" and r["halo"].startswith("ipc direct") for r in res), res
+    assert all(r["backend"] == "ipc" and "IPC direct push" in r["halo"] for r in res), res
     got = torch.tensor(res[0]["grid"], dtype=torch.float64)
     ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed, dtype=torch.float64), iters)
     assert (got - ref).abs().max().item() < (1e-5 if dtype == "f32" else 1e-12)
@@ -66,7 +66,7 @@ def test_ipc_direct_halo_bitwise_vs_classic_exchange(gpu):
     args = {"w": 264, "h": 200, "dims": "2x2", "iters": 40, "seed": 4, "time_block": 20, "overlap": False}
     direct = run_ranks("gpu_solver", 4, dict(args, direct=True), gpu=True)
     classic = run_ranks("gpu_solver", 4, dict(args, direct=False), gpu=True)
-    assert direct[0]["halo"].startswith("ipc direct") and not classic[0]["halo"].startswith("ipc direct")
+    assert "IPC direct push" in direct[0]["halo"] and "IPC direct push" not in classic[0]["halo"]
     assert torch.equal(torch.tensor(direct[0]["grid"]), torch.tensor(classic[0]["grid"]))
 
 
@@ -111,7 +111,24 @@ def test_ipc_warm_and_prepare_leave_the_state_alone(gpu, direct):
     res = run_ranks("gpu_solver", 2, {"w": w, "h": h, "dims": "1x2", "iters": sum(runs), "runs": runs, "seed": seed,
                                       "time_block": 20, "overlap": False, "direct": direct, "prepare": 20, "warm": 20},
                     gpu=True)
-    assert all(r["backend"] == "ipc" and r["halo"].startswith("ipc direct") == direct for r in res), res
+    assert all(r["backend"] == "ipc" and ("IPC direct push" in r["halo"]) == direct for r in res), res
     got = torch.tensor(res[0]["grid"], dtype=torch.float64)
     ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), sum(runs)).double()
     assert (got - ref).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("direct", [True, False])
+def test_rank_stalled_in_prepare_fails_the_job_within_the_watchdog(gpu, direct):
+    """Fault injection: rank 1 stalls 40 s on entering prepare()
+    (after a first run, as bench.py's warm-up leaves it). Rank 0's waits with
+    collectives in flight are under the watchdog (5 s): it must fail well
+    before the stalled rank wakes, naming the phase, instead of hanging."""
+    args = {"w": 264, "h": 200, "dims": "1x2", "iters": 20, "seed": 5, "time_block": 20, "overlap": False,
+            "direct": direct, "warmup_first": 20, "prepare": 20, "comm_timeout": 5,
+            "stall": {"rank": 1, "phase": "prepare", "seconds": 40}}
+    res = run_ranks_raw("gpu_solver", 2, args, timeout=200, gpu=True)
+    r0 = res[0]
+    assert r0["rc"] != 0, r0["stdout"][-2000:]
+    assert "prepare" in r0["stderr"] and "timed out" in r0["stderr"], r0["stderr"][-3000:]
+    assert r0["seconds"] < 40, r0["seconds"]  # failed on its own, not when the peer woke
+    assert "[fault-inject] stalling" in res[1]["stderr"]

@@ -44,23 +44,69 @@ def test_pingpong_two_gpus(gpu, transport, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("n,dims", [g for g in GRIDS if g[0] <= NGPU and g[0] >= 2])
-@pytest.mark.parametrize("frame", [False, True, None, "halo-last"])
-def test_production_depth_schedules_one_rank_per_gpu(gpu, n, dims, frame):
+@pytest.mark.parametrize("opening", ["serial", "interior-first", "auto"])
+def test_production_depth_schedules_one_rank_per_gpu(gpu, n, dims, opening):
     """The bench's multi-GPU path at its depth (S = 20 pipeline, 2048 x 1024
-    tiles per rank): serial post-exchange, frame-first overlap and the measured
-    interior-first (halo-last) overlap and the measured auto choice (prepare)
-    all give the per-step result of the one-step loop."""
+    tiles per rank): the serial opening, the interior-first opening and the
+    measured choice (prepare) give the per-step result of the one-step loop;
+    the choice is the same on every rank; the RCCL communicator spans n ranks
+    on n distinct devices; the window profile replicates one exchange."""
     r, c = (int(x) for x in dims.split("x"))
     w, h, iters, seed = 2048 * c, 1024 * r, 60, 13
     res = run_ranks("gpu_solver", n, {"w": w, "h": h, "dims": dims, "iters": iters, "seed": seed, "backend": "rccl",
-                                      "time_block": 20, "overlap": False, "sum_form": False,
-                                      "frame_overlap": False if frame == "halo-last" else frame,
-                                      "halo_last": frame == "halo-last", "prepare": 20}, gpu=True, timeout=900)
+                                      "time_block": 20, "overlap": False, "sum_form": False, "opening": opening,
+                                      "prepare": 20, "profile": 20, "comm_timeout": 120}, gpu=True, timeout=900)
     assert all(x["native"] and x["time_block"] == 20 for x in res)
-    if frame is True:
-        assert all(x["frame"] for x in res)
-    if frame is None:
-        assert all(x["choice"][0] in ("serial", "frame", "halo-last") for x in res)
+    assert all(x["rccl_ranks"] == n for x in res) and len({x["rccl_device"] for x in res}) == n
+    assert len({x["choice"]["opening"] for x in res}) == 1  # one collective decision
+    assert all(x["exchanges"] == [[3, 3]] for x in res)
+    assert all(x["phases"]["exchanges"] == 1 for x in res)
     got = torch.tensor(res[0]["grid"], dtype=torch.float64)
     ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), iters).double()
     assert (got - ref).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("n,dims", [g for g in GRIDS if g[0] <= NGPU and g[0] >= 2])
+def test_uneven_decomposition_one_rank_per_gpu(gpu, n, dims):
+    """Tiles of different sizes (global 4097 x 2051: one rank's width is not a
+    whole number of 4-lane vectors, so its time block and its chunk-list forms
+    differ from its neighbours'): the ranks agree on one time block and one
+    opening, stay in step and reproduce the one-step loop."""
+    w, h, iters, seed = 4097, 2051, 45, 17
+    res = run_ranks("gpu_solver", n, {"w": w, "h": h, "dims": dims, "iters": iters, "seed": seed, "backend": "rccl",
+                                      "time_block": 20, "overlap": False, "sum_form": False, "opening": "auto",
+                                      "prepare": 20, "comm_timeout": 120}, gpu=True, timeout=900)
+    assert len({x["time_block"] for x in res}) == 1 and len({x["choice"]["opening"] for x in res}) == 1
+    got = torch.tensor(res[0]["grid"], dtype=torch.float64)
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), iters).double()
+    assert (got - ref).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("n", [k for k in (2, 4, 8) if k <= NGPU])
+def test_bench_torchrun(gpu, n):
+    """The driver's SCALE command, as the driver launches it: torchrun, one rank
+    per GPU, RCCL. The 20-step window is one exchange + one pass per rank; the
+    record names the RCCL communicator's rank count and n distinct devices; at
+    N = 8 every rank holds a 16384 x 8192 tile."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from tests.mp_util import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(root, "bench.py"),
+           "--gpus", str(n), "--steps", "20", "--warmup", "5", "--no-extras", "--comm-timeout", "120"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    ex = d["extras"]
+    assert d["n_gpus"] == n and ex["backend"] == "rccl"
+    assert ex["timed_exchanges"] == 1 and ex["timed_super_steps"] == [[20, 1]]
+    assert ex["rccl_ranks"] == n and len(set(x.split(":")[0] for x in ex["rank_devices"])) == n
+    assert ex["window_phases"]["exchanges"] == 1
+    if n == 8:
+        assert ex["tile"] == "16384x8192"
