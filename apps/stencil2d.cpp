@@ -25,6 +25,8 @@
 // --opening auto|serial|interior-first (--halo-last = interior-first; default auto: prepare() times the
 // serial and interior-first openings, agrees the worst-rank medians over all ranks and keeps the faster),
 // --no-direct-halo (IPC backend: pack -> put -> unpack instead of the device-initiated push),
+// --direct-halo on|off|validate (validate: prepare() compares the push with the backend's exchange bitwise on
+// every rank, times both, and uses it only if equal everywhere and faster),
 // --c-center C --c-neighbor C (default 0.2 / 0.2), --no-sum-form (keep the per-step evaluation in the
 // time-blocked kernels: bitwise equal to the CPU app; default: sum form when the coefficients are equal),
 // --loopback, --bind bunch|rrobin,
@@ -117,7 +119,12 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   cfg.bootstrap = [](const std::string& b) { return mpi_allgather_bytes(MPI_COMM_WORLD, b); };
   // IPC: device-initiated halo (each pass pushes its edge bands into the
   // neighbours' tiles) unless --no-direct-halo asks for pack -> put -> unpack.
-  cfg.direct_halo = backend == "ipc" && !cli.flag("no-direct-halo");
+  // --direct-halo validate (RCCL or IPC, ranks on any GPUs): prepare() checks
+  // the device-initiated push bitwise against the backend and times it.
+  const std::string direct = cli.get("direct-halo", backend == "ipc" && !cli.flag("no-direct-halo") ? "on" : "off");
+  MXS_CHECK(direct == "on" || direct == "off" || direct == "validate",
+            "--direct-halo must be on, off or validate, got " << direct);
+  cfg.direct = direct == "on" ? DirectHalo::On : direct == "validate" ? DirectHalo::Validate : DirectHalo::Off;
   // Overlap (interior on a forked stream while the halo moves) defaults on only
   // for one-exchange-per-iteration runs: with temporal blocking the exchange is
   // ~5-8% of a super-step and the concurrent thin boundary strips cost more than
@@ -255,6 +262,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
         js << ", \"interior_first_opening\": " << (solver->halo_last(solver->time_block()) ? "true" : "false");
         if (!solver->opening_choice().empty()) js << ", \"opening_choice\": \"" << solver->opening_choice() << "\"";
         js << ", \"last_opening\": \"" << solver->last_run_opening() << "\"";
+        if (!solver->direct_state().empty()) js << ", \"direct_halo\": \"" << solver->direct_state() << "\"";
       }
       if (want_sum) js << ", \"checksum\": " << app::fmt(checksum);
       js << app::meta_json(device_description(dev.device)) << "}";

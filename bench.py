@@ -263,6 +263,10 @@ def main(argv=None) -> int:
                    help="with --loopback: follow the peers' schedule (every call primes, its last pass is bare, "
                         "the opening is chosen as with peers): one GPU rehearses an N-GPU window")
     p.add_argument("--backend", default="auto", choices=["auto", "rccl", "ipc", "local", "torch"])
+    p.add_argument("--direct-halo", default="off", choices=["off", "validate"],
+                   help="N > 1: validate: prepare() compares the device-initiated push of the edge bands into the "
+                        "neighbours' tiles (HIP IPC over xGMI) bitwise with the RCCL exchange on every rank and times "
+                        "both; the push is used only if equal everywhere and faster (default off)")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-extras", action="store_true")
     p.add_argument("--clock-warmup-ms", type=float, default=200.0,
@@ -311,6 +315,7 @@ def main(argv=None) -> int:
                         graph=not args.no_graph,
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback,
                         sum_form=not args.no_sum_form, opening=args.opening, rehearse_peers=args.rehearse_peers,
+                        direct_halo=("validate" if args.direct_halo == "validate" else None),
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3)
@@ -346,6 +351,8 @@ def main(argv=None) -> int:
         extras["pipe_balanced_shares"] = bool(H.pipe_balanced())
         if st.solver is not None:
             extras["opening"] = st.solver.last_run_opening()
+            if st.solver.direct_state():
+                extras["direct_halo"] = st.solver.direct_state()
             if not st.solver.fused_periodic():
                 # Halo exchanges inside the timed window: one per super-step (with
                 # peers the call primes and ends on a bare pass).

@@ -40,8 +40,10 @@ class IpcDirectHalo {
   // Collective (calls `allgather`). `buf_a` / `buf_b`: this rank's two tiles
   // (any device pointers; their allocations are exported by IPC handle +
   // offset). Every rank must use the same ghost depths.
+  // `allow_cross_device`: ranks on other GPUs without the MXS_IPC_CROSS_DEVICE
+  // opt-in (the caller validates the transfers, StencilSolver DirectHalo::Validate).
   IpcDirectHalo(const CartTopology& topo, int rank, const TileGeom& tile, T* buf_a, T* buf_b,
-                const HostAllgather& allgather, double timeout_s = 60.0);
+                const HostAllgather& allgather, double timeout_s = 60.0, bool allow_cross_device = false);
   ~IpcDirectHalo();
   IpcDirectHalo(const IpcDirectHalo&) = delete;
   IpcDirectHalo& operator=(const IpcDirectHalo&) = delete;

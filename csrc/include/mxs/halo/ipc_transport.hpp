@@ -47,7 +47,9 @@ using HostAllgather = std::function<std::vector<std::string>(const std::string&)
 // across GPUs over xGMI. Ranks on different devices therefore refuse unless
 // MXS_IPC_CROSS_DEVICE=1 opts in (then a warning is printed). Returns whether
 // some peer is on another device.
-bool ipc_check_devices(const HostAllgather& allgather, int rank, const char* what);
+// `validated`: the caller checks the transfers itself (the solver's direct
+// halo validation), so ranks on different devices are allowed without the opt-in.
+bool ipc_check_devices(const HostAllgather& allgather, int rank, const char* what, bool validated = false);
 
 template <typename T>
 class IpcHaloTransport {

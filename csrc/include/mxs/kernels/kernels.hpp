@@ -169,6 +169,9 @@ void stencil5_chunk_pass(const T* in, T* out, const TileGeom& g, const Stencil5C
 // any element is NaN): the range check of the sum form.
 template <typename T>
 void absmax(const T* x, index_t n, T* out, hipStream_t s);
+// Number of 32-bit words that differ between a and b (bytes % 4 == 0) into
+// *out (device pointer, overwritten): the direct halo's bitwise validation.
+void count_diff(const void* a, const void* b, index_t bytes, unsigned* out, hipStream_t s);
 
 // Update an arbitrary core rectangle [x0, x1) x [y0, y1) (scalar path; used for the
 // boundary columns of the overlapped schedule and for tiny tiles).

@@ -111,6 +111,7 @@ namespace mxs {
 
 enum class StencilKind : int { Jacobi5 = 0, Box = 1 };
 enum class Opening : int { Auto = 0, Serial = 1, InteriorFirst = 2 };
+enum class DirectHalo : int { Off = 0, On = 1, Validate = 2 };
 
 // Event-timed phases of one untimed replica of a run's opening super-step
 // (StencilSolver::profile_window): what a short timed window spends where.
@@ -147,11 +148,18 @@ struct SolverConfig {
   HostAllgather bootstrap;
   // Super-steps captured per hipGraph (0 = auto: ~1 ms of work per launch).
   int graph_supersteps = 0;
-  // HaloBackend::Ipc: device-initiated halo (halo/ipc_direct.hpp) — after each
-  // pass one launch copies the output tile's edge bands straight into the
-  // neighbours' ghost rings and publishes a ready counter; the next pass waits
-  // for the neighbours' counters. Replaces pack -> put -> wait -> unpack.
-  bool direct_halo = false;
+  // Device-initiated halo (halo/ipc_direct.hpp): after each pass one launch
+  // copies the output tile's edge bands straight into the neighbours' ghost
+  // rings and publishes a ready counter; the next pass waits for the
+  // neighbours' counters. Replaces pack -> wire -> unpack.
+  //   On       : always (HaloBackend::Ipc: ranks sharing a GPU, where it is verified);
+  //   Validate : RCCL or Ipc backend, ranks on any devices: prepare() runs one
+  //              exchange through the backend and one push from the same state
+  //              and compares every received cell bitwise (agreed over ranks),
+  //              then times both openings; direct is used only when it is
+  //              bitwise equal on every rank and faster (agreed). The decision
+  //              and its reason are recorded (direct_state()).
+  DirectHalo direct = DirectHalo::Off;
   // Opening super-step of a call with peers (see above): measured (Auto),
   // always prime + pass (Serial), always interior-first where the tile has the
   // form (InteriorFirst).
@@ -227,7 +235,15 @@ class StencilSolver {
   const std::string& graph_status() const { return graph_status_; }
   const HaloPlan& plan() const { return ex_->plan(); }
   bool fused_periodic() const { return fused_; }
-  bool direct_halo() const { return direct_ != nullptr; }
+  bool direct_halo() const { return direct_on_; }
+  // The direct halo's state: "" (not configured), "on", "pending validation",
+  // "validated: ..." or "rejected: ..." (with the measured reason).
+  const std::string& direct_state() const { return direct_state_; }
+  double direct_ms() const { return direct_ms_[1]; }
+  double direct_backend_ms() const { return direct_ms_[0]; }
+  // Fault injection for the validation: this rank corrupts one received ghost
+  // cell of the direct push before the comparison (tests of the fallback).
+  void inject_direct_mismatch(bool on) { inject_mismatch_ = on; }
   bool overlapped() const { return cfg_.overlap; }
   // Whether the solver follows the peers' schedule (remote peers, or a
   // loopback rehearsal of them).
@@ -328,7 +344,7 @@ class StencilSolver {
   // Super-steps exchange AFTER their pass (the ghost ring of the next pass's
   // input): every schedule but the fused periodic, the direct IPC halo and the
   // thin-strip overlap, which exchange first.
-  bool post_exchange() const { return !fused_ && !direct_ && !cfg_.overlap; }
+  bool post_exchange() const { return !fused_ && !direct_on_ && !cfg_.overlap; }
   // Sum-form range check: local measurement after a field change, agreed
   // over ranks at the first check and whenever `collective`.
   void ensure_range(bool collective);
@@ -378,7 +394,15 @@ class StencilSolver {
   T* nxt_;
   const RcclComm* comm_ = nullptr;  // watchdog waits and collective agreement when set
   std::unique_ptr<HaloExchanger<T>> ex_;
-  std::unique_ptr<IpcDirectHalo<T>> direct_;  // SolverConfig::direct_halo
+  std::unique_ptr<IpcDirectHalo<T>> direct_;  // SolverConfig::direct (On / Validate)
+  bool direct_on_ = false;                    // super-steps use the direct push
+  std::string direct_state_;
+  double direct_ms_[2] = {0, 0};              // agreed medians: backend opening, direct opening
+  bool inject_mismatch_ = false;
+  DeviceBuffer<T> ref_;                       // validation snapshot
+  DeviceBuffer<unsigned> diff_;
+  void validate_direct(int S);                // DirectHalo::Validate, collective (prepare)
+  void poison_ghost(T* tile);                 // sentinel into every received ghost cell
   // Direct halo: refresh the current tile's ghost ring from the neighbours
   // (push of the current bands; the next pass waits for theirs).
   void prime();

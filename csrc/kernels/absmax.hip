@@ -57,7 +57,30 @@ __global__ __launch_bounds__(kAbsBlock) void absmax_kernel(const T* __restrict__
   }
 }
 
+// Words (32-bit) that differ between a and b, added into *out.
+__global__ __launch_bounds__(kAbsBlock) void count_diff_kernel(const unsigned* __restrict__ a,
+                                                               const unsigned* __restrict__ b, index_t n,
+                                                               unsigned* out) {
+  unsigned c = 0;
+  const index_t stride = index_t(gridDim.x) * kAbsBlock;
+  for (index_t i = index_t(blockIdx.x) * kAbsBlock + threadIdx.x; i < n; i += stride) c += a[i] != b[i] ? 1u : 0u;
+#pragma unroll
+  for (int off = kWaveSize / 2; off > 0; off >>= 1) c += __shfl_xor(c, off);
+  if ((threadIdx.x & (kWaveSize - 1)) == 0 && c) atomicAdd(out, c);
+}
+
 }  // namespace
+
+void count_diff(const void* a, const void* b, index_t bytes, unsigned* out, hipStream_t s) {
+  MXS_CHECK(bytes % 4 == 0, "count_diff: byte count must be a multiple of 4");
+  MXS_HIP_CHECK(hipMemsetAsync(out, 0, sizeof(unsigned), s));
+  const index_t n = bytes / 4;
+  if (n <= 0) return;
+  const int grid = int(std::min<index_t>((n + kAbsBlock * 4 - 1) / (kAbsBlock * 4), index_t(4) * device_cu_count()));
+  count_diff_kernel<<<grid, kAbsBlock, 0, s>>>(static_cast<const unsigned*>(a), static_cast<const unsigned*>(b), n,
+                                               out);
+  MXS_HIP_CHECK_LAUNCH();
+}
 
 template <typename T>
 void absmax(const T* x, index_t n, T* out, hipStream_t s) {

@@ -408,7 +408,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        const RcclComm* comm, const std::string& dt, HaloBackend backend, bool overlap,
                        bool use_graph, bool loopback_self, StencilKind kind, double c0, double c1, int box_radius,
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
-                       py::object bootstrap, int graph_supersteps, bool sum_form, bool direct_halo,
+                       py::object bootstrap, int graph_supersteps, bool sum_form, const std::string& direct_halo,
                        double graph_max_superstep_us, const std::string& opening, bool rehearse_peers,
                        double min_gain) {
              SolverConfig cfg;
@@ -421,7 +421,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
              cfg.graph_max_superstep_us = graph_max_superstep_us;
              cfg.bootstrap = wrap_allgather(bootstrap);
              cfg.graph_supersteps = graph_supersteps;
-             cfg.direct_halo = direct_halo;
+             if (direct_halo == "off") cfg.direct = DirectHalo::Off;
+             else if (direct_halo == "on") cfg.direct = DirectHalo::On;
+             else if (direct_halo == "validate") cfg.direct = DirectHalo::Validate;
+             else throw std::invalid_argument("direct_halo must be off, on or validate, got '" + direct_halo + "'");
              cfg.backend = backend;
              cfg.overlap = overlap;
              cfg.use_graph = use_graph;
@@ -447,7 +450,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("kind") = StencilKind::Jacobi5, py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2,
            py::arg("box_radius") = 1, py::arg("box_weights") = std::vector<float>{}, py::arg("variant") = "auto",
            py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
-           py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = false,
+           py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = "off",
            py::arg("graph_max_superstep_us") = 150.0, py::arg("opening") = "auto", py::arg("rehearse_peers") = false,
            py::arg("min_gain") = 0.03, py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
@@ -474,6 +477,17 @@ PYBIND11_MODULE(_mxs_hip, m) {
            },
            "prepare()'s opening decision and the worst-rank medians / interquartile ranges (ms) it was taken "
            "from (0 = not measured)")
+      .def("direct_state", [](SolverHandle& h) { return h.visit([](auto& s) { return s.direct_state(); }); },
+           "direct halo: '' (not configured), on, pending validation, validated: ..., rejected: ...")
+      .def("direct_times",
+           [](SolverHandle& h) {
+             return h.visit([](auto& s) { return py::make_tuple(s.direct_backend_ms(), s.direct_ms()); });
+           },
+           "validation timings (ms, worst-rank medians): (backend opening, direct opening); 0 = not measured")
+      .def(
+          "inject_direct_mismatch",
+          [](SolverHandle& h, bool on) { h.visit([on](auto& s) { s.inject_direct_mismatch(on); }); },
+          py::arg("on") = true, "fault injection: corrupt one received cell of the direct push before validation")
       .def("last_run_opening", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_opening(); }); },
            "opening of the last run(): interior-first, serial, fresh, fused, direct, overlap or ''")
       .def(

@@ -176,11 +176,11 @@ struct IpcDirectHalo<T>::Impl {
 
 template <typename T>
 IpcDirectHalo<T>::IpcDirectHalo(const CartTopology& topo, int rank, const TileGeom& tile, T* buf_a, T* buf_b,
-                                const HostAllgather& allgather, double timeout_s)
+                                const HostAllgather& allgather, double timeout_s, bool allow_cross_device)
     : impl_(std::make_unique<Impl>()) {
   Impl& I = *impl_;
   MXS_CHECK(bool(allgather), "IpcDirectHalo needs a host allgather bootstrap");
-  (void)ipc_check_devices(allgather, rank, "direct IPC halo");
+  (void)ipc_check_devices(allgather, rank, "direct IPC halo", allow_cross_device);
   I.a = buf_a;
   I.b = buf_b;
   I.world = topo.size();

@@ -193,7 +193,7 @@ double wall_clock_hz() {
 
 }  // namespace
 
-bool ipc_check_devices(const HostAllgather& allgather, int rank, const char* what) {
+bool ipc_check_devices(const HostAllgather& allgather, int rank, const char* what, bool validated) {
   int dev = 0;
   MXS_HIP_CHECK(hipGetDevice(&dev));
   hipUUID u{};
@@ -202,7 +202,7 @@ bool ipc_check_devices(const HostAllgather& allgather, int rank, const char* wha
   const std::vector<std::string> all = allgather(mine);
   bool cross = false;
   for (const auto& d : all) cross = cross || d != mine;
-  if (!cross) return false;
+  if (!cross || validated) return cross;
   const char* opt = std::getenv("MXS_IPC_CROSS_DEVICE");
   MXS_CHECK(opt && std::string(opt) == "1",
             what << ": ranks on different GPUs. The IPC halo is verified only for ranks sharing one GPU; use the "

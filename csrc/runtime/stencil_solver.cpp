@@ -77,8 +77,20 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   boot.timeout_s = comm_timeout() > 0 ? comm_timeout() : 60.0;
   ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm, &boot);
   const bool all_self_nbrs = plan.sends.empty();
-  if (cfg_.direct_halo && cfg_.backend == HaloBackend::Ipc && cfg_.kind == StencilKind::Jacobi5 && !all_self_nbrs)
-    direct_ = std::make_unique<IpcDirectHalo<T>>(topo, rank, tile_, buf_a_, buf_b_, cfg_.bootstrap, boot.timeout_s);
+  if (cfg_.kind == StencilKind::Jacobi5 && !all_self_nbrs) {
+    if (cfg_.direct == DirectHalo::On && cfg_.backend == HaloBackend::Ipc) {
+      direct_ = std::make_unique<IpcDirectHalo<T>>(topo, rank, tile_, buf_a_, buf_b_, cfg_.bootstrap, boot.timeout_s);
+      direct_on_ = true;
+      direct_state_ = "on";
+    } else if (cfg_.direct == DirectHalo::Validate && cfg_.backend != HaloBackend::Local) {
+      MXS_CHECK(static_cast<bool>(cfg_.bootstrap), "direct halo validation needs a host allgather (bootstrap)");
+      // Any devices: the validation in prepare() is the check the IPC
+      // backend's cross-device refusal stands in for.
+      direct_ = std::make_unique<IpcDirectHalo<T>>(topo, rank, tile_, buf_a_, buf_b_, cfg_.bootstrap, boot.timeout_s,
+                                                   /*allow_cross_device=*/true);
+      direct_state_ = "pending validation";
+    }
+  }
   // cfg_.bootstrap stays: it is the host agreement of backends without an RCCL
   // communicator (agree_max). It may hold a Python callable; the solver is
   // destroyed from Python with the GIL held.
@@ -129,7 +141,7 @@ template <typename T>
 StencilSolver<T>::~StencilSolver() {
   // Direct halo: the neighbours' last pushes write into our tiles; wait for
   // them (device deadline) before the caller may free or reuse the buffers.
-  if (direct_) {
+  if (direct_on_) {
     try {
       direct_->wait(main_.get());
     } catch (...) {
@@ -168,7 +180,7 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
     else kernels::stencil5_tb<T>(cur, nxt, tile_, S, 0, w, 0, h, cfg_.coeffs, true, m, cfg_.variant);
     return;
   }
-  if (direct_) {  // the neighbours pushed cur's ghost ring after their previous pass
+  if (direct_on_) {  // the neighbours pushed cur's ghost ring after their previous pass
     direct_->wait(m);
     update(cur, nxt, S, 0, w, 0, h, m);
     direct_->push(nxt, m);
@@ -338,11 +350,14 @@ void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
     ++last_exchanges_;
   }
   if (first && last_opening_.empty()) last_opening_ = post_exchange() ? "fresh" : "overlap";
-  last_bare = last_bare && post_exchange();
+  // Direct halo: the call primed with a push (begin_run); the last pass's
+  // push would only feed the next call, which primes again: bare too.
+  last_bare = last_bare && (post_exchange() || direct_on_);
   const int full = last_bare ? count - 1 : count;  // super-steps with their exchange
   // Exchanges of the super-steps themselves (graph replays included): one each,
   // the bare tail none; the fused periodic self-exchange is no exchange at all.
-  if (!fused_) last_exchanges_ += post_exchange() ? full : count;
+  if (direct_on_) last_exchanges_ += full + (first ? 1 : 0);  // pushes, the priming one included
+  else if (!fused_) last_exchanges_ += post_exchange() ? full : count;
   int i = 0;
   if (GraphSet* gs = full > 0 ? graphs_for(S, full) : nullptr) {
     for (; i + gs->chain <= full; i += gs->chain) {
@@ -368,6 +383,7 @@ void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
 template <typename T>
 void StencilSolver<T>::enqueue_bare_pass(T* cur, T* nxt, int S) {
   MXS_TRACE_RANGE("stencil.superstep_bare");
+  if (direct_on_) direct_->wait(main_.get());  // the neighbours' pushes of cur's ring
   update(cur, nxt, S, 0, tile_.width, 0, tile_.height, main_.get());
 }
 
@@ -377,7 +393,7 @@ void StencilSolver<T>::enqueue_bare_pass(T* cur, T* nxt, int S) {
 // current bands once; the first pass waits for the neighbours' pushes.
 template <typename T>
 void StencilSolver<T>::prime() {
-  if (direct_) direct_->push(cur_, main_.get());
+  if (direct_on_) direct_->push(cur_, main_.get());
 }
 
 template <typename T>
@@ -443,7 +459,7 @@ void StencilSolver<T>::run(int iters) {
   maybe_stall("run");
   begin_run(false);
   if (fused_) last_opening_ = "fused";
-  if (direct_) last_opening_ = "direct";
+  if (direct_on_) last_opening_ = "direct";
   Group gr[2];
   split(iters, gr);
   // With peers every call primes (begin_run), so the exchange after the call's
@@ -515,7 +531,7 @@ void StencilSolver<T>::agree_max(std::vector<double>& v, const char* phase) {
 
 template <typename T>
 void StencilSolver<T>::device_barrier(const char* phase) {
-  if (world_ <= 1 || !comm_) return;
+  if (world_ <= 1) return;
   std::vector<double> v{0.0};
   agree_max(v, phase);
 }
@@ -572,6 +588,12 @@ void StencilSolver<T>::choose_opening(int S) {
     ghost_fresh_ = true;
   }
   auto timed = [&](auto&& enqueue) {
+    // One state-preserving pass first (cur -> nxt, the same exchange): the
+    // sample then starts at the clocks a window after warm() sees, not after
+    // the idle of the previous sample's barrier (the samples spread by 8-13%
+    // of a 0.34 ms opening without it).
+    join_side();
+    enqueue_block(cur_, nxt_, S);
     join_side();
     wait_idle("prepare: opening timing");
     device_barrier("prepare: opening timing");
@@ -632,6 +654,132 @@ void StencilSolver<T>::choose_opening(int S) {
                     : (hlt >= kMissing ? "no rank-wide interior-first candidate"
                                        : "gain below the threshold or within the spread"));
   opening_reason_ = buf;
+}
+
+template <typename T>
+void StencilSolver<T>::poison_ghost(T* tile) {
+  // A value no exchange of a real field delivers: every received cell must be
+  // overwritten for the comparison to pass on both paths.
+  const T sentinel = T(-1.2345e30);
+  const HaloPlan& plan = ex_->plan();
+  for (const auto& m : plan.recvs)
+    for (const auto& seg : m.segments) kernels::fill_region<T>(tile, seg.region, sentinel, main_.get());
+  for (const auto& c : plan.self_copies) kernels::fill_region<T>(tile, c.dst, sentinel, main_.get());
+}
+
+// DirectHalo::Validate, once, inside prepare() (collective). (1) Bitwise: the
+// received ghost cells of the current tile after one exchange through the
+// backend (RCCL, or the IPC transport for ranks sharing a GPU) and after one
+// direct push, both from sentinel-filled rings, must be identical on every
+// rank (agreed). (2) Timing: the direct opening (push, wait, pass) against the
+// backend's opening (the chosen one), sampled like choose_opening and agreed.
+// Direct is switched on only if (1) holds everywhere and (2) wins by min_gain
+// beyond the spread. The current field is unchanged (its ring is re-exchanged).
+template <typename T>
+void StencilSolver<T>::validate_direct(int S) {
+  if (!direct_ || cfg_.direct != DirectHalo::Validate || direct_state_ != "pending validation") return;
+  MXS_TRACE_RANGE("stencil.validate_direct");
+  hipStream_t m = main_.get();
+  join_side();
+  if (!ref_.get()) ref_.reset(tile_.alloc_elems());
+  if (!diff_.get()) diff_.reset(1);
+  const size_t bytes = size_t(tile_.alloc_elems()) * sizeof(T);
+  poison_ghost(cur_);
+  ex_->exchange(cur_, m);
+  MXS_HIP_CHECK(hipMemcpyAsync(ref_.get(), cur_, bytes, hipMemcpyDeviceToDevice, m));
+  poison_ghost(cur_);
+  wait_idle("prepare: direct halo validation");
+  device_barrier("prepare: direct halo validation");  // every ring poisoned before any push lands
+  direct_->push(cur_, m);
+  direct_->wait(m);
+  if (inject_mismatch_) {  // fault injection: one received cell differs
+    const HaloPlan& plan = ex_->plan();
+    Array2D one = !plan.recvs.empty() ? plan.recvs[0].segments[0].region : plan.self_copies[0].dst;
+    one.width = one.height = 1;
+    kernels::fill_region<T>(cur_, one, T(42), m);
+  }
+  kernels::count_diff(cur_, ref_.get(), index_t(bytes), diff_.get(), m);
+  unsigned diff = 0;
+  MXS_HIP_CHECK(hipMemcpyAsync(&diff, diff_.get(), sizeof(unsigned), hipMemcpyDeviceToHost, m));
+  wait_idle("prepare: direct halo validation");
+  std::vector<double> bad{double(diff)};
+  agree_max(bad, "prepare: direct halo validation");
+  ex_->exchange(cur_, m);  // whatever the push delivered, the ring is the backend's again
+  ghost_fresh_ = true;
+  if (bad[0] != 0.0) {
+    direct_state_ = "rejected: the direct push differs from the " + std::string(cfg_.backend == HaloBackend::Rccl
+                                                                                  ? "RCCL" : "IPC") +
+                    " exchange in " + std::to_string(int(bad[0])) + " words on some rank";
+    wait_idle("prepare: direct halo validation");
+    return;
+  }
+  // Timing, from drained streams after a barrier, each sample behind a
+  // state-preserving pass of its own path (clocks), medians of 8 + IQR, agreed.
+  auto timed = [&](auto&& warm, auto&& enqueue) {
+    join_side();
+    warm();
+    join_side();
+    wait_idle("prepare: direct halo timing");
+    device_barrier("prepare: direct halo timing");
+    const auto t0 = std::chrono::steady_clock::now();
+    enqueue();
+    join_side();
+    wait_idle("prepare: direct halo timing");
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  };
+  constexpr int kReps = 9;
+  std::vector<double> t_backend, t_direct;
+  const index_t w = tile_.width, h = tile_.height;
+  for (int rep = 0; rep < kReps; ++rep) {
+    const double tb = timed([&] { enqueue_block(cur_, nxt_, S); },
+                            [&] {
+                              if (halo_last_on_) {
+                                enqueue_opening(S, false);
+                              } else {
+                                ex_->exchange(cur_, m);
+                                update(cur_, nxt_, S, 0, w, 0, h, m);
+                              }
+                            });
+    // Direct: the priming push of the current bands, the wait for the
+    // neighbours' pushes, the pass (a call's bare last super-step).
+    const double td = timed(
+        [&] {
+          direct_->push(cur_, m);
+          direct_->wait(m);
+          update(cur_, nxt_, S, 0, w, 0, h, m);
+        },
+        [&] {
+          direct_->push(cur_, m);
+          direct_->wait(m);
+          update(cur_, nxt_, S, 0, w, 0, h, m);
+        });
+    if (rep > 0) {
+      t_backend.push_back(tb);
+      t_direct.push_back(td);
+    }
+  }
+  std::vector<double> v(4);
+  std::tie(v[0], v[2]) = median_iqr(t_backend);
+  std::tie(v[1], v[3]) = median_iqr(t_direct);
+  agree_max(v, "prepare: direct halo timing");
+  direct_ms_[0] = v[0];
+  direct_ms_[1] = v[1];
+  const double gain = v[0] - v[1];
+  const bool win = gain >= cfg_.min_gain * v[0] && gain > std::max(v[2], v[3]);
+  char buf[256];
+  std::snprintf(buf, sizeof(buf),
+                "bitwise equal on every rank; worst-rank medians of %d openings: direct %.4f ms, %s %.4f ms "
+                "(IQR %.4f / %.4f ms)",
+                kReps - 1, v[1], cfg_.backend == HaloBackend::Rccl ? "RCCL" : "IPC", v[0], v[3], v[2]);
+  direct_state_ = std::string(win ? "validated: " : "rejected (slower): ") + buf;
+  // The timing pushes advanced the direct epochs and wrote the scratch
+  // buffer's neighbours only; the current ring is the backend's (fresh).
+  if (win) {
+    direct_on_ = true;
+    ghost_fresh_ = false;
+    graphs_.clear();  // captured for the backend's schedule
+    warmed_.clear();
+  }
 }
 
 // Interior-first pass of depth S (built on first use while the schedule is on).
@@ -787,6 +935,7 @@ void StencilSolver<T>::prepare(int iters) {
   // Opening::Auto: decide the opening at the depth of the larger group.
   const Group& big = gr[0].count >= gr[1].count ? gr[0] : gr[1];
   if (big.count > 0) choose_opening(big.S);
+  if (big.count > 0) validate_direct(big.S);
   // Every collective below is issued the same number of times on every rank,
   // whatever this rank's forms and decisions: one priming exchange when the
   // ring is stale, then per cold size one opening (one exchange) when the
@@ -844,8 +993,8 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
   const int supersteps = gr[0].count + gr[1].count;
   const index_t w = tile_.width, h = tile_.height;
   hipStream_t m = main_.get();
-  if (direct_ || (!fused_ && !post_exchange())) {
-    out.opening = direct_ ? "direct (not profiled)" : "overlap (not profiled)";
+  if (direct_on_ || (!fused_ && !post_exchange())) {
+    out.opening = direct_on_ ? "direct (not profiled)" : "overlap (not profiled)";
     return out;
   }
   join_side();
@@ -931,7 +1080,7 @@ template <typename T>
 void StencilSolver<T>::synchronize() {
   // Direct halo: also wait for the neighbours' pushes into our tiles, so the
   // field (ghost ring included) is final and no peer still writes into it.
-  if (direct_) direct_->wait(main_.get());
+  if (direct_on_) direct_->wait(main_.get());
   // With a remote peer and a watchdog timeout, wait by polling so a dead or
   // hung peer fails the job instead of blocking it.
   wait_idle("stencil halo exchange (RCCL)");

@@ -71,12 +71,14 @@ class StencilConfig:
     seed: int = 1234
     init: str = "random"             # random | rank
     graph_supersteps: int = 0        # super-steps per hipGraph launch (0 = auto, ~1 ms of work)
-    # IPC backend: device-initiated halo — each pass's output bands are pushed
-    # tile-to-tile into the neighbours' ghost rings (no pack / unpack launches).
-    # None = on whenever the backend is ipc. The IPC backend refuses ranks on
-    # different GPUs unless MXS_IPC_CROSS_DEVICE=1 (verified only for ranks
-    # sharing one GPU: halo/ipc_transport.hpp ipc_check_devices).
-    direct_halo: bool | None = None
+    # Device-initiated halo — each pass's output bands are pushed tile-to-tile
+    # into the neighbours' ghost rings (no pack / wire / unpack launches).
+    # None / True = on whenever the backend is ipc (ranks sharing a GPU; the IPC
+    # backend refuses ranks on different GPUs unless MXS_IPC_CROSS_DEVICE=1).
+    # "validate": RCCL or IPC backend, ranks on any GPUs: prepare() compares one
+    # direct push with one backend exchange bitwise on every rank and times both
+    # openings; direct runs only if equal everywhere and faster (agreed).
+    direct_halo: bool | str | None = None
     # Opening super-step of a call with peers (RCCL): its priming exchange runs
     # under the chunks that read only core cells ("interior-first") or before
     # the pass ("serial"). "auto" (default): prepare() times both on every rank,
@@ -185,7 +187,7 @@ class Stencil2D:
                                           cfg.dtype, be, overlap, cfg.graph, cfg.loopback, kind, cfg.c_center,
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
-                                          backend == "ipc" and cfg.direct_halo is not False,
+                                          self._direct_mode(backend),
                                           cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
@@ -195,6 +197,17 @@ class Stencil2D:
             self.halo = TorchHalo(self.plan, self.ctx)
 
     # ---------------------------------------------------------------- setup
+    def _direct_mode(self, backend: str) -> str:
+        """SolverConfig direct halo: "on" for IPC (default), "validate" where asked
+        (RCCL or IPC: prepare() checks it bitwise against the backend and times it),
+        else "off"."""
+        d = self.cfg.direct_halo
+        if d == "validate":
+            return "validate" if backend in ("rccl", "ipc") and self.ctx.world_size > 1 else "off"
+        if backend == "ipc" and d is not False and d != "off":
+            return "on"
+        return "off"
+
     def _init_data(self):
         d, g = self.decomp, self.geom
         if self.cfg.init == "rank":

@@ -93,6 +93,8 @@ def task_gpu_solver(args):
                         sum_form=args.get("sum_form", True), opening=args.get("opening", "auto"),
                         min_gain=args.get("min_gain", 0.03))
     st = Stencil2D(cfg, ctx)
+    if args.get("mismatch_rank") == ctx.rank:
+        st.solver.inject_direct_mismatch(True)
     stall = args.get("stall")
     if stall and ctx.rank == stall["rank"]:
         st.solver.inject_stall(stall["phase"], float(stall["seconds"]))
@@ -122,6 +124,8 @@ def task_gpu_solver(args):
         out["exchanges"] = per_run  # halo exchanges each run() enqueued, and its super-steps
         out["openings"] = openings
         out["phases"] = phases
+        out["direct_state"] = st.solver.direct_state()
+        out["direct"] = bool(st.solver.direct_halo())
         if st.comm is not None:
             out["rccl_ranks"] = int(st.comm.count())
             out["rccl_device"] = int(st.comm.device())

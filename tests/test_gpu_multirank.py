@@ -132,3 +132,32 @@ def test_rank_stalled_in_prepare_fails_the_job_within_the_watchdog(gpu, direct):
     assert "prepare" in r0["stderr"] and "timed out" in r0["stderr"], r0["stderr"][-3000:]
     assert r0["seconds"] < 40, r0["seconds"]  # failed on its own, not when the peer woke
     assert "[fault-inject] stalling" in res[1]["stderr"]
+
+
+@pytest.mark.parametrize("mismatch", [False, True])
+def test_direct_halo_validation_and_fallback(gpu, mismatch):
+    """DirectHalo validate (the mode that lets the device-initiated push run
+    between GPUs): prepare() compares one push with one exchange through the
+    backend (here the IPC transport: ranks share the GPU) bitwise on every rank
+    and times both. Equal everywhere: validated (used if faster) or rejected as
+    slower, on every rank alike. One rank's corrupted cell (fault injection):
+    every rank rejects it and keeps the backend. The field is exact either way."""
+    w, h, seed, runs = 272, 216, 23, [20, 20, 7]
+    res = run_ranks("gpu_solver", 2, {"w": w, "h": h, "dims": "1x2", "iters": sum(runs), "runs": runs, "seed": seed,
+                                      "time_block": 20, "overlap": False, "direct": "validate", "prepare": 20,
+                                      "mismatch_rank": 1 if mismatch else None, "comm_timeout": 60}, gpu=True)
+    states = [r["direct_state"] for r in res]
+    assert len({s.split(":")[0] for s in states}) == 1, states  # one collective decision
+    if mismatch:
+        assert states[0].startswith("rejected: the direct push differs"), states
+        assert not any(r["direct"] for r in res)
+    else:
+        assert states[0].startswith(("validated: bitwise equal", "rejected (slower): bitwise equal")), states
+        assert all(r["direct"] == states[0].startswith("validated") for r in res)
+        if res[0]["direct"]:
+            assert "IPC direct push" in res[0]["halo"]
+            # A one-super-step call with the direct halo: the priming push, then a bare pass.
+            assert all(r["exchanges"][0] == [1, 1] for r in res), res[0]["exchanges"]
+    got = torch.tensor(res[0]["grid"], dtype=torch.float64)
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), sum(runs)).double()
+    assert (got - ref).abs().max().item() < 1e-5

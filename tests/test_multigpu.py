@@ -82,6 +82,24 @@ def test_uneven_decomposition_one_rank_per_gpu(gpu, n, dims):
     assert (got - ref).abs().max().item() < 1e-5
 
 
+@pytest.mark.parametrize("n,dims", [g for g in GRIDS if g[0] <= NGPU and g[0] >= 2])
+def test_direct_halo_validated_between_gpus(gpu, n, dims):
+    """The device-initiated push between GPUs over xGMI, behind its runtime
+    validation: prepare() compares it bitwise with the RCCL exchange on every
+    rank; whatever it decides (validated, slower, or a mismatch), all ranks
+    decide alike and the field equals the one-step loop."""
+    r, c = (int(x) for x in dims.split("x"))
+    w, h, iters, seed = 2048 * c, 1024 * r, 60, 19
+    res = run_ranks("gpu_solver", n, {"w": w, "h": h, "dims": dims, "iters": iters, "seed": seed, "backend": "rccl",
+                                      "time_block": 20, "overlap": False, "sum_form": False, "direct": "validate",
+                                      "prepare": 20, "comm_timeout": 120}, gpu=True, timeout=900)
+    states = [x["direct_state"] for x in res]
+    assert len({s.split(":")[0] for s in states}) == 1 and not states[0].startswith("pending"), states
+    got = torch.tensor(res[0]["grid"], dtype=torch.float64)
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), iters).double()
+    assert (got - ref).abs().max().item() < 1e-5
+
+
 @pytest.mark.parametrize("n", [k for k in (2, 4, 8) if k <= NGPU])
 def test_bench_torchrun(gpu, n):
     """The driver's SCALE command, as the driver launches it: torchrun, one rank
