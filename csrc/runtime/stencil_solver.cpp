@@ -587,33 +587,39 @@ void StencilSolver<T>::choose_opening(int S) {
     ex_->exchange(cur_, main_.get());
     ghost_fresh_ = true;
   }
-  auto timed = [&](auto&& enqueue) {
-    // One state-preserving pass first (cur -> nxt, the same exchange): the
-    // sample then starts at the clocks a window after warm() sees, not after
-    // the idle of the previous sample's barrier (the samples spread by 8-13%
-    // of a 0.34 ms opening without it).
+  // GPU time of one opening, from drained streams after a device barrier and
+  // behind one state-preserving pass (cur -> nxt, the same exchange), so the
+  // sample runs at the clocks a window after warm() sees. The start event goes
+  // on the stream that receives the opening's first launch (the side stream
+  // for interior-first: an event on main would itself force the fork the
+  // opening skips), the end event on main after the join. Host-clock samples
+  // of the same openings spread by 15-18% (IQR) on one box; the GPU span
+  // still contains every gap the host leaves (RCCL's enqueue) after the first launch.
+  Event e0(true), e1(true);
+  auto timed = [&](bool starts_on_side, auto&& enqueue) {
     join_side();
     enqueue_block(cur_, nxt_, S);
     join_side();
     wait_idle("prepare: opening timing");
     device_barrier("prepare: opening timing");
-    const auto t0 = std::chrono::steady_clock::now();
+    e0.record(starts_on_side ? side_.get() : main_.get());
     enqueue();
     join_side();
+    e1.record(main_.get());
     wait_idle("prepare: opening timing");
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return double(e1.since(e0));
   };
-  constexpr int kCands = 3, kReps = 9;  // round 0 warms every shape
+  constexpr int kCands = 3, kReps = 13;  // round 0 warms every shape
   std::vector<double> t_serial;
   std::vector<std::vector<double>> t_cand(kCands);
   for (int rep = 0; rep < kReps; ++rep) {
-    const double serial = timed([&] {
+    const double serial = timed(false, [&] {
       ex_->exchange(cur_, main_.get());
       enqueue_bare_pass(cur_, nxt_, S);
     });
     if (rep > 0) t_serial.push_back(serial);
     for (size_t c = 0; c < size_t(kCands); ++c) {
-      const double ms = timed([&] {
+      const double ms = timed(c < cands.size(), [&] {
         if (c < cands.size()) {
           enqueue_halo_last(cur_, nxt_, cands[c]);
         } else {
@@ -648,7 +654,8 @@ void StencilSolver<T>::choose_opening(int S) {
   opening_choice_ = win ? "interior-first" : "serial";
   char buf[256];
   std::snprintf(buf, sizeof(buf),
-                "worst-rank medians of %d: interior-first %.4f ms, serial %.4f ms (IQR %.4f / %.4f ms): %s",
+                "worst-rank medians of %d (GPU event spans): interior-first %.4f ms, serial %.4f ms "
+                "(IQR %.4f / %.4f ms): %s",
                 kReps - 1, opening_ms_[1], serial, opening_spread_[1], opening_spread_[0],
                 win ? "gain above the threshold and the spread"
                     : (hlt >= kMissing ? "no rank-wide interior-first candidate"
@@ -713,25 +720,28 @@ void StencilSolver<T>::validate_direct(int S) {
     wait_idle("prepare: direct halo validation");
     return;
   }
-  // Timing, from drained streams after a barrier, each sample behind a
-  // state-preserving pass of its own path (clocks), medians of 8 + IQR, agreed.
-  auto timed = [&](auto&& warm, auto&& enqueue) {
+  // Timing (GPU events, as choose_opening), from drained streams after a
+  // barrier, each sample behind a state-preserving pass of its own path
+  // (clocks), medians of 8 + IQR, agreed.
+  Event e0(true), e1(true);
+  auto timed = [&](bool starts_on_side, auto&& warm, auto&& enqueue) {
     join_side();
     warm();
     join_side();
     wait_idle("prepare: direct halo timing");
     device_barrier("prepare: direct halo timing");
-    const auto t0 = std::chrono::steady_clock::now();
+    e0.record(starts_on_side ? side_.get() : m);
     enqueue();
     join_side();
+    e1.record(m);
     wait_idle("prepare: direct halo timing");
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return double(e1.since(e0));
   };
   constexpr int kReps = 9;
   std::vector<double> t_backend, t_direct;
   const index_t w = tile_.width, h = tile_.height;
   for (int rep = 0; rep < kReps; ++rep) {
-    const double tb = timed([&] { enqueue_block(cur_, nxt_, S); },
+    const double tb = timed(halo_last_on_ && halo_last_pass(S, false), [&] { enqueue_block(cur_, nxt_, S); },
                             [&] {
                               if (halo_last_on_) {
                                 enqueue_opening(S, false);
@@ -743,6 +753,7 @@ void StencilSolver<T>::validate_direct(int S) {
     // Direct: the priming push of the current bands, the wait for the
     // neighbours' pushes, the pass (a call's bare last super-step).
     const double td = timed(
+        false,
         [&] {
           direct_->push(cur_, m);
           direct_->wait(m);

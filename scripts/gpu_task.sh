@@ -7,7 +7,7 @@
 #   gpurun -- bash scripts/gpu_task.sh OUT TASK [ARGS...]
 #
 # OUT is a directory under gpurun_out/. Tasks:
-#   tests [PYTEST ARGS]    pytest -m gpu (verbose, per-test limit) -> OUT/pytest_gpu.txt
+#   tests [PATHS/ARGS]     pytest -m gpu over PATHS (default tests/; verbose, per-test limit) -> OUT/pytest_gpu.txt
 #   smoke                  __graft_entry__.smoke()                  -> OUT/smoke.txt
 #   bench [BENCH ARGS]     python bench.py ARGS                      -> OUT/bench.txt (JSON line echoed)
 #   prof NAME [BENCH ARGS] rocprofv3 --kernel-trace --stats of bench.py ARGS -> OUT/prof_NAME/
@@ -38,9 +38,11 @@ step() {  # step LIMIT LOG CMD...: run CMD under LIMIT seconds, log to LOG, stop
   fi
 }
 
-task_tests() {
-  timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 240 --timeout-method thread -p no:cacheprovider "$@" \
-    > "$OUT/pytest_gpu.txt" 2>&1
+task_tests() {  # [PATHS / PYTEST ARGS] (default: the whole suite)
+  local args=("$@")
+  [ ${#args[@]} -eq 0 ] && args=(tests)
+  timeout -k 10 1000 python -u -m pytest "${args[@]}" -m gpu -v --timeout 240 --timeout-method thread \
+    -p no:cacheprovider > "$OUT/pytest_gpu.txt" 2>&1
   local rc=$?
   echo "pytest rc=$rc"
   tail -3 "$OUT/pytest_gpu.txt"
@@ -83,13 +85,12 @@ task_window() {
   for i in $(seq "$reps"); do
     for mode in $modes; do
       local args=(--global "$tile" --steps 20 --warmup 5 --no-extras)
-      local envs=()
       case $mode in
-        auto) args+=(--loopback); envs=(MXS_PEER_SCHEDULE=1) ;;
-        serial) args+=(--loopback --opening serial); envs=(MXS_PEER_SCHEDULE=1) ;;
+        auto) args+=(--loopback --rehearse-peers) ;;
+        serial) args+=(--loopback --rehearse-peers --opening serial) ;;
         fused) ;;
       esac
-      env "${envs[@]}" timeout -k 10 200 python bench.py "${args[@]}" > "$OUT/window_last.txt" 2>&1 || {
+      timeout -k 10 200 python bench.py "${args[@]}" > "$OUT/window_last.txt" 2>&1 || {
         echo "window run failed ($mode)"
         tail -30 "$OUT/window_last.txt"
         exit 1
