@@ -168,18 +168,23 @@ def dot_extras(ctx, extras: dict, n_global: int) -> None:
     del dp
 
 
-def pingpong_extras(ctx, extras: dict, max_bytes: int, with_ipc: bool = False) -> None:
+def pingpong_extras(ctx, extras: dict, max_bytes: int, with_ipc: bool = False, loopback: bool = False) -> None:
     """BASELINE metric 2 / config 3: ranks 0 <-> 1, 8 B - 256 MiB.
 
     RCCL only by default: the headline line is printed after the extras, and a
     fault in a transport that has never crossed GPUs in this tree (HIP IPC
     between two devices; tested between processes sharing one) would take the
-    whole record with it. ``--pingpong-ipc`` adds the IPC sweep."""
+    whole record with it. ``--pingpong-ipc`` adds the IPC sweep.
+    ``loopback`` (one GPU): the same record from rank 0 with itself, RCCL self
+    send/recv and both IPC kernels on this GPU (keys as for a pair)."""
     from cuda_mpi_scratch_amd.models.pingpong import PingPong
 
     sweep = []
     gpu_plan = (("rccl", ("blocking", "async", "overlap", "bidir")),) + ((("ipc", ("device",)),) if with_ipc else ())
+    if loopback:
+        gpu_plan = (("loopback", ("blocking", "async")), ("ipc-loopback", ("device",)))
     plan = gpu_plan if torch.cuda.is_available() else (("torch", ("blocking",)),)  # CPU rehearsal: gloo send/recv
+    canonical = {"loopback": "rccl", "ipc-loopback": "ipc"}
     for transport, modes in plan:
         try:
             sizes = [b for b in PINGPONG_SIZES if b <= max_bytes]
@@ -199,8 +204,11 @@ def pingpong_extras(ctx, extras: dict, max_bytes: int, with_ipc: bool = False) -
         ctx.barrier()
     if not ctx.is_root or not sweep:
         return
+    extras["pingpong_pair"] = ("loopback: rank 0 with itself on one GPU" if loopback
+                               else "ranks 0 <-> 1" + (" (GPUs " + ", ".join(extras.get("rank_devices", [])[:2]) + ")"
+                                                       if extras.get("rank_devices") else ""))
     for rec in sweep:
-        key = f"pingpong_{rec['transport']}_{rec['mode']}"
+        key = f"pingpong_{canonical.get(rec['transport'], rec['transport'])}_{rec['mode']}"
         if rec["bytes"] == 8:
             if rec.get("timing") == "host":
                 # Blocking mode is timed by the host around launch + stream sync:
@@ -217,7 +225,7 @@ def pingpong_extras(ctx, extras: dict, max_bytes: int, with_ipc: bool = False) -
             alone = rec.get("compute_alone_us", 0.0) + rec.get("comm_alone_us", 0.0)
             if rec.get("overlapped_us"):
                 extras[f"{key}_256MiB_overlap_speedup"] = round(alone / rec["overlapped_us"], 3)
-    if not with_ipc:
+    if not with_ipc and not loopback:
         extras["pingpong_ipc"] = ("not run: the device-initiated HIP IPC transport across GPUs is opt-in "
                                   "(--pingpong-ipc); RCCL figures only")
     lat = {t: extras.get(f"pingpong_{t}_8B_latency_us") for t in ("rccl_async", "ipc_device")}
@@ -276,6 +284,9 @@ def main(argv=None) -> int:
     p.add_argument("--pingpong-max", type=int, default=256 << 20, help="largest ping-pong message (extras)")
     p.add_argument("--pingpong-ipc", action="store_true",
                    help="N >= 2 extras: also sweep the HIP IPC ping-pong transport (default: RCCL only)")
+    p.add_argument("--pingpong-loopback", action="store_true",
+                   help="N = 1 extras: the ping-pong record from rank 0 with itself (RCCL self send/recv, IPC kernels "
+                        "on one GPU) instead of the 8192^2 stencil rates")
     p.add_argument("--comm-timeout", type=float, default=300.0,
                    help="seconds a halo / all-reduce wait may take before the run fails (0 = forever)")
     args = p.parse_args(argv)
@@ -398,7 +409,9 @@ def main(argv=None) -> int:
                 stencil_rate(ctx, 32768, 32768, "f32", args.steps, args.warmup, args.clock_warmup_ms / 1e3,
                              time_block=args.time_block, sum_form=False), 2)
             torch.cuda.empty_cache()
-        if n == 1 and gpu:
+        if n == 1 and gpu and args.pingpong_loopback:
+            pingpong_extras(ctx, extras, args.pingpong_max, loopback=True)
+        elif n == 1 and gpu:
             # 480 steps: a multiple of the fp32 (20) and fp64 (16) default blocks,
             # so every pass is a full-depth (joint-window) pass.
             extras["stencil_8192sq_f32_1gpu_gcells_per_s"] = round(

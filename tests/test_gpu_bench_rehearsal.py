@@ -50,3 +50,27 @@ def test_bench_8gpu_tile_window_through_loopback(gpu):
     assert isinstance(ex["env"], dict) and ex["experiments_build"] is False
     # 16384 x 8192 x 20 cell-updates: one pass (~0.25 ms) + one loopback exchange.
     assert d["value"] > 5000, d
+
+
+def test_bench_pingpong_and_dot_record_keys_through_loopback(gpu):
+    """The N >= 2 extras' record shape, rehearsed on one GPU (--pingpong-loopback:
+    rank 0 with itself, RCCL self send/recv and both IPC kernels on this GPU):
+    RCCL and IPC 8 B latencies side by side (both event-timed), the blocking
+    mode labelled as a host round trip, and the dot's event-timed kernel time
+    next to its wall time."""
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--global", "1024x1024", "--steps", "4",
+                        "--warmup", "1", "--pingpong-loopback", "--pingpong-max", str(1 << 20), "--dot-n",
+                        str(1 << 22), "--clock-warmup-ms", "0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    ex = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["extras"]
+    assert ex["pingpong_pair"].startswith("loopback")
+    lat = ex["pingpong_8B_latency_us"]
+    assert set(lat) == {"rccl_async", "ipc_device"} and all(v > 0 for v in lat.values()), lat
+    assert ex["pingpong_rccl_async_8B_latency_us"] == lat["rccl_async"]
+    assert ex["pingpong_rccl_blocking_8B_host_rtt_us"] > 0 and "pingpong_rccl_blocking_8B_latency_us" not in ex
+    assert ex["pingpong_rccl_async_1MiB_gbps"] > 0 and ex["pingpong_verified"] is True
+    assert "pingpong_ipc" not in ex  # the note is for pairs without --pingpong-ipc
+    assert ex["dot_4194304_f64_verified"] is True
+    assert ex["dot_4194304_f64_kernel_us"] > 0 and ex["dot_4194304_f64_us"] > 0
