@@ -258,7 +258,8 @@ class StencilSolver {
   double opening_serial_ms() const { return opening_ms_[0]; }
   double opening_halo_last_ms() const { return opening_ms_[1]; }
   double opening_serial_spread_ms() const { return opening_spread_[0]; }
-  double opening_halo_last_spread_ms() const { return opening_spread_[1]; }
+  double opening_ratio() const { return opening_ratio_; }
+  double opening_ratio_iqr() const { return opening_spread_[1]; }
   int opening_samples() const { return opening_samples_; }
   // Workgroups of the outer (ghost-ring) launch of the interior-first opening
   // at depth S (0: none built).
@@ -350,7 +351,8 @@ class StencilSolver {
   void ensure_range(bool collective);
   void begin_run(bool collective);           // range check + prime
   double opening_ms_[2] = {0, 0};            // agreed medians: prime + pass, interior-first (ms)
-  double opening_spread_[2] = {0, 0};        // agreed interquartile ranges (ms)
+  double opening_spread_[2] = {0, 0};        // agreed IQRs: serial (ms), paired ratio
+  double opening_ratio_ = 0;                 // agreed median paired ratio interior-first / serial
   int opening_samples_ = 0;
   std::string opening_choice_;               // "" before prepare() decided, "serial" or "interior-first"
   std::string opening_reason_;

@@ -469,14 +469,15 @@ PYBIND11_MODULE(_mxs_hip, m) {
                d["serial_ms"] = s.opening_serial_ms();
                d["interior_first_ms"] = s.opening_halo_last_ms();
                d["serial_iqr_ms"] = s.opening_serial_spread_ms();
-               d["interior_first_iqr_ms"] = s.opening_halo_last_spread_ms();
+               d["ratio"] = s.opening_ratio();
+               d["ratio_iqr"] = s.opening_ratio_iqr();
                d["samples"] = s.opening_samples();
                d["outer_wgs"] = s.halo_last_outer_wgs(s.time_block());
                return d;
              });
            },
-           "prepare()'s opening decision and the worst-rank medians / interquartile ranges (ms) it was taken "
-           "from (0 = not measured)")
+           "prepare()'s opening decision: the worst-rank median paired ratio interior-first / serial and its "
+           "IQR it was taken from, and the medians (ms; 0 = not measured)")
       .def("direct_state", [](SolverHandle& h) { return h.visit([](auto& s) { return s.direct_state(); }); },
            "direct halo: '' (not configured), on, pending validation, validated: ..., rejected: ...")
       .def("direct_times",

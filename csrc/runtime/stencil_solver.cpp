@@ -611,7 +611,7 @@ void StencilSolver<T>::choose_opening(int S) {
   };
   constexpr int kCands = 3, kReps = 13;  // round 0 warms every shape
   std::vector<double> t_serial;
-  std::vector<std::vector<double>> t_cand(kCands);
+  std::vector<std::vector<double>> t_cand(kCands), ratio(kCands);
   for (int rep = 0; rep < kReps; ++rep) {
     const double serial = timed(false, [&] {
       ex_->exchange(cur_, main_.get());
@@ -627,39 +627,56 @@ void StencilSolver<T>::choose_opening(int S) {
           enqueue_bare_pass(cur_, nxt_, S);
         }
       });
-      if (rep > 0 && c < cands.size()) t_cand[c].push_back(ms);
+      if (rep > 0 && c < cands.size()) {
+        t_cand[c].push_back(ms);
+        ratio[c].push_back(ms / std::max(serial, 1e-9));  // paired with this round's serial sample
+      }
     }
   }
+  // The decision rests on the paired ratios (candidate / serial of the same
+  // round): the clock drifts between rounds by far more than the openings
+  // differ (IQR of either series alone 11% of a 0.29 ms opening on one box),
+  // and a round's two samples see the same clock. Agreed over ranks: the worst
+  // median ratio and the widest spread. Interior-first wins when the median
+  // ratio is at most 1 - min_gain and its notch (median + 1.58 IQR / sqrt(n),
+  // the 95% interval of a median) stays below 1.
   constexpr double kMissing = 1e30;
-  std::vector<double> v(2 * (1 + kCands), kMissing);
-  std::tie(v[0], v[1 + kCands]) = median_iqr(t_serial);
-  for (size_t c = 0; c < cands.size(); ++c) std::tie(v[1 + c], v[2 + kCands + c]) = median_iqr(t_cand[c]);
+  std::vector<double> v(4 * kCands + 2, kMissing);
+  std::tie(v[0], v[1]) = median_iqr(t_serial);
+  for (size_t c = 0; c < cands.size(); ++c) {
+    v[2 + c] = median_iqr(t_cand[c]).first;
+    std::tie(v[2 + kCands + c], v[2 + 2 * kCands + c]) = median_iqr(ratio[c]);
+  }
   agree_max(v, "prepare: opening agreement");
   size_t best = 0;
   for (size_t c = 1; c < size_t(kCands); ++c)
-    if (v[1 + c] < v[1 + best]) best = c;
-  const double serial = v[0], hlt = v[1 + best];
-  const double noise = std::max(v[1 + kCands], v[2 + kCands + best]);
-  const bool win = hlt < kMissing && serial - hlt >= cfg_.min_gain * serial && serial - hlt > noise;
+    if (v[2 + kCands + c] < v[2 + kCands + best]) best = c;
+  const double serial = v[0], hlt = v[2 + best], r = v[2 + kCands + best], r_iqr = v[2 + 2 * kCands + best];
+  const int n = kReps - 1;
+  const double notch = r + 1.58 * r_iqr / std::sqrt(double(n));
+  const bool win = r < kMissing && r <= 1.0 - cfg_.min_gain && notch < 1.0;
   opening_ms_[0] = serial;
   opening_ms_[1] = hlt < kMissing ? hlt : 0.0;
-  opening_spread_[0] = v[1 + kCands];
-  opening_spread_[1] = hlt < kMissing ? v[2 + kCands + best] : 0.0;
-  opening_samples_ = kReps - 1;
+  opening_spread_[0] = v[1];
+  opening_spread_[1] = r < kMissing ? r_iqr : 0.0;
+  opening_ratio_ = r < kMissing ? r : 0.0;
+  opening_samples_ = n;
   if (win && best > 0 && best - 1 < alt.size()) {  // keep the measured best outer set for S
     for (auto& h : halo_lasts_)
       if (h->S == S) h = std::move(alt[best - 1]);
   }
   halo_last_on_ = win;
   opening_choice_ = win ? "interior-first" : "serial";
-  char buf[256];
-  std::snprintf(buf, sizeof(buf),
-                "worst-rank medians of %d (GPU event spans): interior-first %.4f ms, serial %.4f ms "
-                "(IQR %.4f / %.4f ms): %s",
-                kReps - 1, opening_ms_[1], serial, opening_spread_[1], opening_spread_[0],
-                win ? "gain above the threshold and the spread"
-                    : (hlt >= kMissing ? "no rank-wide interior-first candidate"
-                                       : "gain below the threshold or within the spread"));
+  char buf[320];
+  if (r >= kMissing) {
+    std::snprintf(buf, sizeof(buf), "no rank-wide interior-first candidate (serial median %.4f ms)", serial);
+  } else {
+    std::snprintf(buf, sizeof(buf),
+                  "worst-rank paired ratio interior-first / serial over %d rounds (GPU event spans): median %.3f, "
+                  "IQR %.3f, notch %.3f (switch at <= %.3f with notch < 1); medians %.4f / %.4f ms: %s",
+                  n, r, r_iqr, notch, 1.0 - cfg_.min_gain, hlt, serial,
+                  win ? "interior-first" : "serial kept");
+  }
   opening_reason_ = buf;
 }
 
@@ -737,8 +754,8 @@ void StencilSolver<T>::validate_direct(int S) {
     wait_idle("prepare: direct halo timing");
     return double(e1.since(e0));
   };
-  constexpr int kReps = 9;
-  std::vector<double> t_backend, t_direct;
+  constexpr int kReps = 13;
+  std::vector<double> t_backend, t_direct, ratio;
   const index_t w = tile_.width, h = tile_.height;
   for (int rep = 0; rep < kReps; ++rep) {
     const double tb = timed(halo_last_on_ && halo_last_pass(S, false), [&] { enqueue_block(cur_, nxt_, S); },
@@ -767,21 +784,24 @@ void StencilSolver<T>::validate_direct(int S) {
     if (rep > 0) {
       t_backend.push_back(tb);
       t_direct.push_back(td);
+      ratio.push_back(td / std::max(tb, 1e-9));  // paired: the same round's clock (choose_opening)
     }
   }
   std::vector<double> v(4);
-  std::tie(v[0], v[2]) = median_iqr(t_backend);
-  std::tie(v[1], v[3]) = median_iqr(t_direct);
+  v[0] = median_iqr(t_backend).first;
+  v[1] = median_iqr(t_direct).first;
+  std::tie(v[2], v[3]) = median_iqr(ratio);
   agree_max(v, "prepare: direct halo timing");
   direct_ms_[0] = v[0];
   direct_ms_[1] = v[1];
-  const double gain = v[0] - v[1];
-  const bool win = gain >= cfg_.min_gain * v[0] && gain > std::max(v[2], v[3]);
-  char buf[256];
+  const int n = kReps - 1;
+  const double notch = v[2] + 1.58 * v[3] / std::sqrt(double(n));
+  const bool win = v[2] <= 1.0 - cfg_.min_gain && notch < 1.0;
+  char buf[320];
   std::snprintf(buf, sizeof(buf),
-                "bitwise equal on every rank; worst-rank medians of %d openings: direct %.4f ms, %s %.4f ms "
-                "(IQR %.4f / %.4f ms)",
-                kReps - 1, v[1], cfg_.backend == HaloBackend::Rccl ? "RCCL" : "IPC", v[0], v[3], v[2]);
+                "bitwise equal on every rank; worst-rank paired ratio direct / %s over %d rounds: median %.3f, "
+                "IQR %.3f, notch %.3f; medians %.4f / %.4f ms",
+                cfg_.backend == HaloBackend::Rccl ? "RCCL" : "IPC", n, v[2], v[3], notch, v[1], v[0]);
   direct_state_ = std::string(win ? "validated: " : "rejected (slower): ") + buf;
   // The timing pushes advanced the direct epochs and wrote the scratch
   // buffer's neighbours only; the current ring is the backend's (fresh).

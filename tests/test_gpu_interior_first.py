@@ -215,11 +215,10 @@ def test_auto_opening_is_recorded_thresholded_and_exact(gpu):
     auto.prepare(20)
     t = auto.solver.schedule_times()
     assert t["opening"] in ("serial", "interior-first") and t["samples"] == 12
-    assert t["serial_ms"] > 0 and t["interior_first_ms"] > 0 and t["serial_iqr_ms"] >= 0
-    gain = t["serial_ms"] - t["interior_first_ms"]
-    wins = gain >= 0.03 * t["serial_ms"] and gain > max(t["serial_iqr_ms"], t["interior_first_iqr_ms"])
+    assert t["serial_ms"] > 0 and t["interior_first_ms"] > 0 and t["ratio"] > 0 and t["ratio_iqr"] >= 0
+    wins = t["ratio"] <= 0.97 and t["ratio"] + 1.58 * t["ratio_iqr"] / math.sqrt(12) < 1.0
     assert (t["opening"] == "interior-first") == wins == auto.solver.halo_last(20)
-    assert "worst-rank medians" in t["reason"]
+    assert "paired ratio" in t["reason"]
     auto.run(20)
     assert auto.solver.last_run_opening() == t["opening"]
     auto.run(40)
