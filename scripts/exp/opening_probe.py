@@ -1,0 +1,51 @@
+"""The opening decision on the 8-GPU tile through RCCL loopback in the peers'
+schedule: prepare()'s agreed numbers (paired ratio, notch, reason) for a few
+fresh solvers, and event-timed replicas (profile_window) of the serial and the
+interior-first openings, interleaved, as the bench records them.
+
+usage: python scripts/exp/opening_probe.py [TILE] [SOLVERS] [REPLICAS]"""
+import json
+import sys
+
+sys.path.insert(0, ".")
+
+import torch  # noqa: E402
+
+from cuda_mpi_scratch_amd.models.stencil2d import Stencil2D, StencilConfig  # noqa: E402
+
+
+def main() -> int:
+    tile = sys.argv[1] if len(sys.argv) > 1 else "16384x8192"
+    solvers = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    reps = int(sys.argv[3]) if len(sys.argv) > 3 else 12
+    w, h = (int(x) for x in tile.split("x"))
+    kw = dict(global_width=w, global_height=h, dims="1x1", dtype="f32", backend="rccl", loopback=True,
+              rehearse_peers=True, seed=5)
+    for i in range(solvers):
+        st = Stencil2D(StencilConfig(**kw))
+        st.run(20)
+        st.prepare(20)
+        print(json.dumps({"solver": i, **st.solver.schedule_times()}), flush=True)
+        del st
+        torch.cuda.empty_cache()
+    sts = {o: Stencil2D(StencilConfig(opening=o, **kw)) for o in ("serial", "interior-first")}
+    for st in sts.values():
+        st.run(20)
+        st.prepare(20)
+        st.warm(20, 0.2)
+    spans = {o: [] for o in sts}
+    for _ in range(reps):
+        for o, st in sts.items():
+            p = st.profile_window(20)
+            spans[o].append(p["gpu_span_us"])
+    for o, v in spans.items():
+        v = sorted(v)
+        print(json.dumps({"opening": o, "gpu_span_us_median": v[len(v) // 2], "min": v[0], "max": v[-1]}))
+    ratio = sorted(a / b for a, b in zip(spans["interior-first"], spans["serial"]))
+    print(json.dumps({"paired_ratio_median": round(ratio[len(ratio) // 2], 4), "min": round(ratio[0], 4),
+                      "max": round(ratio[-1], 4)}))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
