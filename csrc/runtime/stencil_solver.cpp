@@ -595,7 +595,11 @@ void StencilSolver<T>::choose_opening(int S) {
   // opening skips), the end event on main after the join. Host-clock samples
   // of the same openings spread by 15-18% (IQR) on one box; the GPU span
   // still contains every gap the host leaves (RCCL's enqueue) after the first launch.
-  Event e0(true), e1(true);
+  // The end is the later of an event on each stream, with no join between
+  // them: a window ends when both streams have drained (synchronize()), and a
+  // cross-stream join (~15 us) would be charged to the interior-first opening
+  // alone (it measured 1.0x serial that way, 0.92x as the window runs it).
+  Event e0(true), e1(true), e2(true);
   auto timed = [&](bool starts_on_side, auto&& enqueue) {
     join_side();
     enqueue_block(cur_, nxt_, S);
@@ -604,10 +608,10 @@ void StencilSolver<T>::choose_opening(int S) {
     device_barrier("prepare: opening timing");
     e0.record(starts_on_side ? side_.get() : main_.get());
     enqueue();
-    join_side();
     e1.record(main_.get());
+    e2.record(side_.get());
     wait_idle("prepare: opening timing");
-    return double(e1.since(e0));
+    return std::max(double(e1.since(e0)), double(e2.since(e0)));
   };
   constexpr int kCands = 3, kReps = 13;  // round 0 warms every shape
   std::vector<double> t_serial;
@@ -740,7 +744,7 @@ void StencilSolver<T>::validate_direct(int S) {
   // Timing (GPU events, as choose_opening), from drained streams after a
   // barrier, each sample behind a state-preserving pass of its own path
   // (clocks), medians of 8 + IQR, agreed.
-  Event e0(true), e1(true);
+  Event e0(true), e1(true), e2(true);
   auto timed = [&](bool starts_on_side, auto&& warm, auto&& enqueue) {
     join_side();
     warm();
@@ -749,10 +753,10 @@ void StencilSolver<T>::validate_direct(int S) {
     device_barrier("prepare: direct halo timing");
     e0.record(starts_on_side ? side_.get() : m);
     enqueue();
-    join_side();
-    e1.record(m);
+    e1.record(m);  // both streams' ends, no join (choose_opening)
+    e2.record(side_.get());
     wait_idle("prepare: direct halo timing");
-    return double(e1.since(e0));
+    return std::max(double(e1.since(e0)), double(e2.since(e0)));
   };
   constexpr int kReps = 13;
   std::vector<double> t_backend, t_direct, ratio;
