@@ -67,6 +67,9 @@ class RcclComm {
   // fails on an RCCL async error, or after comm_timeout() seconds (the
   // communicator is aborted first so the error path cannot block on it).
   void wait(hipStream_t stream, const char* what) const;
+  // The same for several streams in one poll loop (each stream is queried until
+  // it has drained; a window's end is noticed one poll after its last kernel).
+  void wait_all(const hipStream_t* streams, int n, const char* what) const;
 
   // Ranks the communicator really spans (ncclCommCount) and the HIP device
   // this rank's end of it runs on (ncclCommCuDevice): the run records quote

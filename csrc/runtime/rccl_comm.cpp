@@ -36,17 +36,27 @@ bool RcclComm::healthy(std::string* msg) const {
   return true;
 }
 
-void RcclComm::wait(hipStream_t stream, const char* what) const {
+void RcclComm::wait(hipStream_t stream, const char* what) const { wait_all(&stream, 1, what); }
+
+void RcclComm::wait_all(const hipStream_t* streams, int n, const char* what) const {
   // The stream is polled on every spin; the communicator's async error state
   // (a call into RCCL) only once per millisecond: querying it on every spin
   // delayed noticing the completion of a 20-step window by ~100 us.
   using clock = std::chrono::steady_clock;
   auto next_check = clock::now();
+  int done = 0;  // streams [0, done) have drained
   wait_with_timeout(
       [&] {
-        const hipError_t q = hipStreamQuery(stream);
-        if (q == hipSuccess) return true;
-        if (q != hipErrorNotReady) MXS_HIP_CHECK(q);
+        while (done < n) {
+          const hipError_t q = hipStreamQuery(streams[done]);
+          if (q == hipSuccess) {
+            ++done;
+            continue;
+          }
+          if (q != hipErrorNotReady) MXS_HIP_CHECK(q);
+          break;
+        }
+        if (done == n) return true;
         const auto now = clock::now();
         if (now >= next_check) {
           next_check = now + std::chrono::milliseconds(1);

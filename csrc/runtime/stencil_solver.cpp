@@ -482,12 +482,13 @@ void StencilSolver<T>::wait_idle(const char* phase) {
     // With an RCCL communicator and a watchdog: poll (a dead or hung peer
     // fails the job, naming the phase, instead of blocking it).
     if (comm_ && comm_timeout() > 0) {
-      comm_->wait(main_.get(), phase);
-      comm_->wait(side_.get(), phase);
+      const hipStream_t both[2] = {main_.get(), side_.get()};
+      comm_->wait_all(both, 2, phase);
+    } else {
+      // IPC waits carry their own device deadline: the streams drain either way.
+      main_.spin_sync();
+      side_.spin_sync();
     }
-    // IPC waits carry their own device deadline: the streams drain either way.
-    main_.spin_sync();
-    side_.spin_sync();
     side_pending_ = false;  // both streams drained: nothing for main to wait for
     if (ex_) ex_->check();
     if (direct_) direct_->check();
