@@ -57,9 +57,10 @@ Extras (not the headline number, BASELINE configs 2/3/5):
     single-pass device reduction + RCCL all-reduce of the partial (GB/s read);
   * N = 1: 8192^2 fp32 and fp64 single-GPU stencil rates;
   * N >= 2: GPU-GPU ping-pong between ranks 0 and 1, 8 B - 256 MiB, RCCL
-    blocking / async / overlap / bidir; the device-initiated HIP IPC transport
-    only with --pingpong-ipc (opt-in: its cross-GPU coherence is verified only by
-    the multi-GPU tests, and a fault there would take the record with it). Summary
+    blocking / async / overlap / bidir, then the device-initiated HIP IPC
+    transport between the same two GPUs in two isolated child processes (its
+    cross-GPU coherence is checked by the echo; a failure ends a child, never
+    this record); both 8 B latencies side by side in pingpong_8B_latency_us. Summary
     (latency at 8 B, GB/s at 1 MiB / 16 MiB / 256 MiB) in extras, the full
     sweep in gpurun_out/bench_pingpong_n<N>.json.
 """
@@ -226,8 +227,8 @@ def pingpong_extras(ctx, extras: dict, max_bytes: int, with_ipc: bool = False, l
             if rec.get("overlapped_us"):
                 extras[f"{key}_256MiB_overlap_speedup"] = round(alone / rec["overlapped_us"], 3)
     if not with_ipc and not loopback:
-        extras["pingpong_ipc"] = ("not run: the device-initiated HIP IPC transport across GPUs is opt-in "
-                                  "(--pingpong-ipc); RCCL figures only")
+        extras["pingpong_ipc"] = ("in-process sweep off (--pingpong-ipc); the device-initiated transport runs "
+                                  "isolated in child processes after this sweep")
     lat = {t: extras.get(f"pingpong_{t}_8B_latency_us") for t in ("rccl_async", "ipc_device")}
     extras["pingpong_8B_latency_us"] = {k: v for k, v in lat.items() if v is not None}
     extras["pingpong_verified"] = all(r.get("passed", False) for r in sweep)
@@ -239,6 +240,65 @@ def pingpong_extras(ctx, extras: dict, max_bytes: int, with_ipc: bool = False, l
         extras["pingpong_sweep_file"] = path
     except OSError as e:
         extras["pingpong_sweep_file_error"] = str(e)[:120]
+
+
+def pingpong_ipc_isolated(ctx, extras: dict, max_bytes: int, timeout_s: float = 180.0) -> None:
+    """The device-initiated IPC ping-pong between the GPUs of ranks 0 and 1, run
+    in two child processes (one per GPU, their own rendezvous, gloo control
+    plane): whatever the transport does across GPUs — a wrong flag, a deadline,
+    a fault — ends a child, not this rank, and lands in the record as an error
+    next to the RCCL figures. Collective over all ranks (only 0 and 1 launch)."""
+    import socket
+    import subprocess
+
+    port = None
+    if ctx.rank == 0:
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = str(sk.getsockname()[1]).encode()
+    port = ctx.broadcast_bytes(port, src=0, key="mxs/bench/ipc_pingpong_port").decode()
+    out = os.path.join("gpurun_out", "bench_pingpong_ipc.jsonl")
+    err = None
+    if ctx.rank < 2:
+        if ctx.rank == 0:
+            os.makedirs("gpurun_out", exist_ok=True)
+            if os.path.exists(out):
+                os.remove(out)
+        env = dict(os.environ, RANK=str(ctx.rank), WORLD_SIZE="2", LOCAL_RANK=str(ctx.device.index),
+                   LOCAL_WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=port, MXS_IPC_CROSS_DEVICE="1",
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cmd = [sys.executable, "-m", "cuda_mpi_scratch_amd.models.pingpong", "--transport", "ipc", "--mode", "async",
+               "--sweep", f"8:{max_bytes}", "--reps", "50", "--warmup", "5", "--pg-backend", "gloo"]
+        if ctx.rank == 0:
+            cmd += ["--json", out]
+        try:
+            r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s,
+                               cwd=os.path.dirname(os.path.abspath(__file__)))
+            if r.returncode != 0:
+                err = f"rank {ctx.rank} child rc={r.returncode}: {r.stderr.strip()[-300:]}"
+        except subprocess.TimeoutExpired:
+            err = f"rank {ctx.rank} child timed out after {timeout_s:g} s"
+    errs = [e.decode() for e in ctx.allgather_bytes((err or "").encode(), key="mxs/bench/ipc_pingpong_err") if e]
+    if not ctx.is_root:
+        return
+    if errs:
+        extras["pingpong_ipc_error"] = "; ".join(errs)[:400]
+        return
+    try:
+        recs = [json.loads(line) for line in open(out)]
+    except OSError as e:
+        extras["pingpong_ipc_error"] = f"no records: {e}"[:200]
+        return
+    for rec in recs:
+        if rec["bytes"] == 8:
+            extras["pingpong_ipc_device_8B_latency_us"] = round(rec["latency_us"], 2)
+        for label, nb in SUMMARY_SIZES.items():
+            if rec["bytes"] == nb:
+                extras[f"pingpong_ipc_device_{label}_gbps"] = round(rec["gbps"], 2)
+    extras["pingpong_ipc_verified"] = all(r.get("passed", False) for r in recs)
+    extras["pingpong_ipc_sweep_file"] = out
+    extras["pingpong_ipc"] = ("device-initiated HIP IPC between the GPUs of ranks 0 and 1, run isolated in two "
+                              "child processes (a failure there cannot take this record)")
 
 
 def main(argv=None) -> int:
@@ -284,6 +344,8 @@ def main(argv=None) -> int:
     p.add_argument("--pingpong-max", type=int, default=256 << 20, help="largest ping-pong message (extras)")
     p.add_argument("--pingpong-ipc", action="store_true",
                    help="N >= 2 extras: also sweep the HIP IPC ping-pong transport (default: RCCL only)")
+    p.add_argument("--no-pingpong-ipc", action="store_true",
+                   help="N >= 2 extras: skip the isolated device-initiated IPC ping-pong (child processes)")
     p.add_argument("--pingpong-loopback", action="store_true",
                    help="N = 1 extras: the ping-pong record from rank 0 with itself (RCCL self send/recv, IPC kernels "
                         "on one GPU) instead of the 8192^2 stencil rates")
@@ -422,6 +484,17 @@ def main(argv=None) -> int:
                              sum_form=not args.no_sum_form), 2)
         else:
             pingpong_extras(ctx, extras, args.pingpong_max, args.pingpong_ipc)
+            if gpu and n >= 2 and not args.pingpong_ipc and not args.no_pingpong_ipc:
+                _sync()
+                ctx.barrier()
+                try:
+                    pingpong_ipc_isolated(ctx, extras, min(args.pingpong_max, 256 << 20))
+                except Exception as e:  # noqa: BLE001 - reported, never fatal for the headline
+                    extras["pingpong_ipc_error"] = str(e)[:200]
+                if ctx.is_root:
+                    lat = extras.setdefault("pingpong_8B_latency_us", {})
+                    if "pingpong_ipc_device_8B_latency_us" in extras:
+                        lat["ipc_device"] = extras["pingpong_ipc_device_8B_latency_us"]
         ctx.barrier()
 
     if ctx.is_root:

@@ -176,8 +176,11 @@ def main(argv=None) -> int:
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--json", default=None)
+    p.add_argument("--pg-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                   help="torch.distributed backend of the control plane (gloo: no RCCL communicator is created, "
+                        "e.g. for the IPC transport alone)")
     args = p.parse_args(argv)
-    ctx = dist_init()
+    ctx = dist_init(backend=args.pg_backend)
     sizes = [args.n_doubles * 8] if args.n_doubles else parse_sweep(args.sweep)
     pp = PingPong(ctx, args.transport, max(sizes))
     for nb in sizes:

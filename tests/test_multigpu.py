@@ -128,3 +128,32 @@ def test_bench_torchrun(gpu, n):
     assert ex["window_phases"]["exchanges"] == 1
     if n == 8:
         assert ex["tile"] == "16384x8192"
+
+
+@pytest.mark.skipif(NGPU < 2, reason="needs >= 2 GPUs")
+def test_bench_pingpong_extras_two_gpus(gpu):
+    """The N = 2 record's ping-pong: RCCL modes in process, the device-initiated
+    IPC transport between the two GPUs in isolated child processes; both 8 B
+    latencies side by side (or the IPC error, never a lost record)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from tests.mp_util import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(root, "bench.py"), "--gpus", "2",
+           "--global", "4096x4096", "--steps", "20", "--warmup", "5", "--dot-n", str(1 << 24),
+           "--pingpong-max", str(1 << 24), "--comm-timeout", "120"]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", PYTHONUNBUFFERED="1")
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    ex = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["extras"]
+    assert ex["pingpong_rccl_async_8B_latency_us"] > 0 and ex["pingpong_verified"] is True
+    assert "pingpong_ipc_device_8B_latency_us" in ex or "pingpong_ipc_error" in ex
+    if "pingpong_ipc_device_8B_latency_us" in ex:
+        assert ex["pingpong_ipc_verified"] is True
+        assert set(ex["pingpong_8B_latency_us"]) == {"rccl_async", "ipc_device"}
+    assert ex["dot_16777216_f64_kernel_us"] > 0 and ex["dot_16777216_f64_allreduce_us"] > 0
