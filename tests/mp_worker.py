@@ -78,6 +78,19 @@ def task_bench(args):
     return {"rank": int(os.environ["RANK"]), "rc": rc, "line": lines[-1] if lines else None}
 
 
+def task_ipc_pingpong_isolated(args):
+    """bench.py's isolated IPC ping-pong (child processes) from two ranks."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    ctx = init(backend="gloo", device="cuda")
+    extras = {}
+    bench.pingpong_ipc_isolated(ctx, extras, args["max_bytes"], timeout_s=120.0)
+    ctx.barrier()
+    ctx.destroy()
+    return {"rank": ctx.rank, "extras": extras}
+
+
 def task_gpu_solver(args):
     """Native solver on GPU (IPC halo backend on a shared GPU, RCCL one rank per
     GPU): random init, N iterations, global grid back on rank 0."""

@@ -161,3 +161,15 @@ def test_direct_halo_validation_and_fallback(gpu, mismatch):
     got = torch.tensor(res[0]["grid"], dtype=torch.float64)
     ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), sum(runs)).double()
     assert (got - ref).abs().max().item() < 1e-5
+
+
+def test_bench_isolated_ipc_pingpong_two_ranks(gpu):
+    """bench.py's N >= 2 IPC ping-pong runs in two child processes with their own
+    rendezvous (here both on this GPU): rank 0's record gets the latency, the
+    bandwidths and the verification, the ranks' own processes never touch it."""
+    res = run_ranks("ipc_pingpong_isolated", 2, {"max_bytes": 1 << 20}, gpu=True, timeout=300)
+    ex = res[0]["extras"]
+    assert "pingpong_ipc_error" not in ex, ex
+    assert ex["pingpong_ipc_device_8B_latency_us"] > 0 and ex["pingpong_ipc_device_1MiB_gbps"] > 0
+    assert ex["pingpong_ipc_verified"] is True and "isolated" in ex["pingpong_ipc"]
+    assert res[1]["extras"] == {}
