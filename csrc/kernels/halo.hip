@@ -37,9 +37,10 @@ constexpr int kBlock = 256;
 // ~4 us memory latency; profiles/r02_tile). Each in-flight element keeps its
 // value and its destination pointer only (not its coordinates): the kernel
 // stays at <= 32 VGPRs, so a copy wave fits beside a pipeline workgroup
-// (2 waves x 240 VGPRs per SIMD) and the frame-first schedule's pack / unpack
-// run while the pass does (at 34 VGPRs -> 40 allocated they could not be
-// placed until the pass ended, profiles/r03_frame).
+// (2 waves x 240 VGPRs per SIMD) and the interior-first opening's pack / unpack
+// run while the inner chunks do (at 34 VGPRs -> 40 allocated they could not be
+// placed until the pass ended, measured with round 3's frame-first pass,
+// profiles/r03_frame).
 constexpr int kInFlight = 4;
 
 template <typename V, typename Src, typename Dst>
@@ -74,8 +75,8 @@ __device__ __forceinline__ void copy_2d(index_t width, index_t height, Src&& src
 template <typename T>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_vgpr(32))) void copy2d_batch_kernel(
     T* __restrict__ s0, T* __restrict__ s1, T* __restrict__ s2, Copy2DBatch b) {
-  // Highest wave priority: in the frame-first schedule the pack / unpack run
-  // while the pipeline pass still fills every CU (a copy wave fits beside a
+  // Highest wave priority: in the interior-first opening the pack / unpack run
+  // while the inner chunk launch still fills most CUs (a copy wave fits beside a
   // pipeline workgroup: 20 VGPRs), and the pass's VALU-bound waves, which
   // raise their own priority as they progress (stencil_device.hpp), otherwise
   // win every issue slot: the pack crawled until the pass ended (140 us for

@@ -157,7 +157,7 @@ PYBIND11_MODULE(_mxs_core, m) {
 
   m.def("balanced_starts", &kernels::balanced_starts, py::arg("groups"), py::arg("rows"), py::arg("blocks"),
         py::arg("fill"), "fill-aware linear starts of the pipeline workgroups' shares (blocks + 1 entries)");
-  // Interior-first (halo-last) schedule of the pre-exchange overlapped pass.
+  // Interior-first (halo-last) schedule of the multi-GPU opening super-step.
   m.def(
       "halo_last_schedule",
       [](std::int64_t groups, std::int64_t rows, int blocks, std::int64_t fill, std::int64_t depth,
