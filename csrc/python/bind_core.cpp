@@ -10,6 +10,7 @@
 #include "mxs/grid/regions.hpp"
 #include "mxs/halo/plan.hpp"
 #include "mxs/kernels/chunk_schedule.hpp"
+#include "mxs/runtime/decision.hpp"
 #include "mxs/topo/cart.hpp"
 
 namespace py = pybind11;
@@ -155,6 +156,20 @@ PYBIND11_MODULE(_mxs_core, m) {
   m.def("make_halo_plan", &make_halo_plan, py::arg("topo"), py::arg("rank"), py::arg("tile"),
         py::arg("corners") = true, py::arg("loopback_self") = false);
 
+  m.def(
+      "paired_decision",
+      [](std::vector<double> ratios, double min_gain) {
+        const int n = int(ratios.size());
+        const auto [med, iqr] = median_iqr(ratios);
+        py::dict d;
+        d["median"] = med;
+        d["iqr"] = iqr;
+        d["notch"] = median_notch(med, iqr, n);
+        d["win"] = paired_win(med, iqr, n, min_gain);
+        return d;
+      },
+      py::arg("ratios"), py::arg("min_gain") = 0.03,
+      "the solver's opening / direct-halo rule on per-round ratios candidate / baseline (runtime/decision.hpp)");
   m.def("balanced_starts", &kernels::balanced_starts, py::arg("groups"), py::arg("rows"), py::arg("blocks"),
         py::arg("fill"), "fill-aware linear starts of the pipeline workgroups' shares (blocks + 1 entries)");
   // Interior-first (halo-last) schedule of the multi-GPU opening super-step.

@@ -14,6 +14,7 @@
 
 #include "mxs/core/fault.hpp"
 #include "mxs/core/trace.hpp"
+#include "mxs/runtime/decision.hpp"
 
 namespace mxs {
 
@@ -537,16 +538,6 @@ void StencilSolver<T>::device_barrier(const char* phase) {
   agree_max(v, phase);
 }
 
-namespace {
-// Median and interquartile range of a small sample (sorted in place).
-std::pair<double, double> median_iqr(std::vector<double>& v) {
-  if (v.empty()) return {0.0, 0.0};
-  std::sort(v.begin(), v.end());
-  const size_t n = v.size();
-  return {v[n / 2], v[(3 * n) / 4 < n ? (3 * n) / 4 : n - 1] - v[n / 4]};
-}
-}  // namespace
-
 // Opening::Auto, once (the first prepare() with a form at its depth): the
 // call's opening super-step timed from drained streams after a device barrier,
 // as a timed window sees it (host clock to both streams drained again; an
@@ -658,8 +649,8 @@ void StencilSolver<T>::choose_opening(int S) {
     if (v[2 + kCands + c] < v[2 + kCands + best]) best = c;
   const double serial = v[0], hlt = v[2 + best], r = v[2 + kCands + best], r_iqr = v[2 + 2 * kCands + best];
   const int n = kReps - 1;
-  const double notch = r + 1.58 * r_iqr / std::sqrt(double(n));
-  const bool win = r < kMissing && r <= 1.0 - cfg_.min_gain && notch < 1.0;
+  const double notch = median_notch(r, r_iqr, n);
+  const bool win = r < kMissing && paired_win(r, r_iqr, n, cfg_.min_gain);
   opening_ms_[0] = serial;
   opening_ms_[1] = hlt < kMissing ? hlt : 0.0;
   opening_spread_[0] = v[1];
@@ -800,8 +791,8 @@ void StencilSolver<T>::validate_direct(int S) {
   direct_ms_[0] = v[0];
   direct_ms_[1] = v[1];
   const int n = kReps - 1;
-  const double notch = v[2] + 1.58 * v[3] / std::sqrt(double(n));
-  const bool win = v[2] <= 1.0 - cfg_.min_gain && notch < 1.0;
+  const double notch = median_notch(v[2], v[3], n);
+  const bool win = paired_win(v[2], v[3], n, cfg_.min_gain);
   char buf[320];
   std::snprintf(buf, sizeof(buf),
                 "bitwise equal on every rank; worst-rank paired ratio direct / %s over %d rounds: median %.3f, "
