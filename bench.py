@@ -331,6 +331,9 @@ def main(argv=None) -> int:
                    help="with --loopback: follow the peers' schedule (every call primes, its last pass is bare, "
                         "the opening is chosen as with peers): one GPU rehearses an N-GPU window")
     p.add_argument("--backend", default="auto", choices=["auto", "rccl", "ipc", "local", "torch"])
+    p.add_argument("--halo-max-ctas", type=int, default=0,
+                   help="N > 1: the halo exchange on an RCCL communicator split off with at most this many "
+                        "workgroups per kernel (0 = RCCL's default)")
     p.add_argument("--direct-halo", default="off", choices=["off", "validate"],
                    help="N > 1: validate: prepare() compares the device-initiated push of the edge bands into the "
                         "neighbours' tiles (HIP IPC over xGMI) bitwise with the RCCL exchange on every rank and times "
@@ -389,6 +392,7 @@ def main(argv=None) -> int:
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback,
                         sum_form=not args.no_sum_form, opening=args.opening, rehearse_peers=args.rehearse_peers,
                         direct_halo=("validate" if args.direct_halo == "validate" else None),
+                        halo_max_ctas=args.halo_max_ctas,
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3)
@@ -424,6 +428,10 @@ def main(argv=None) -> int:
         extras["pipe_balanced_shares"] = bool(H.pipe_balanced())
         if st.solver is not None:
             extras["opening"] = st.solver.last_run_opening()
+            if args.halo_max_ctas:
+                extras["halo_max_ctas"] = int(st.solver.halo_max_ctas())
+                if st.solver.halo_comm_note():
+                    extras["halo_comm_note"] = st.solver.halo_comm_note()
             if st.solver.direct_state():
                 extras["direct_halo"] = st.solver.direct_state()
             if not st.solver.fused_periodic():

@@ -10,6 +10,7 @@
 
 #include <rccl/rccl.h>
 
+#include <memory>
 #include <sstream>
 #include <string>
 #include <type_traits>
@@ -71,6 +72,14 @@ class RcclComm {
   // it has drained; a window's end is noticed one poll after its last kernel).
   void wait_all(const hipStream_t* streams, int n, const char* what) const;
 
+  // A communicator over the same ranks whose kernels use at most `max_ctas`
+  // workgroups (ncclCommSplit with ncclConfig_t::maxCTAs; collective). The
+  // halo exchange of the interior-first opening runs on the CUs the inner
+  // chunk launch leaves free (32-48 of 256): a cap keeps RCCL's kernels from
+  // queueing behind it. Throws when the RCCL in use rejects the config.
+  std::unique_ptr<RcclComm> split_with_max_ctas(int max_ctas) const;
+  int max_ctas() const { return max_ctas_; }
+
   // Ranks the communicator really spans (ncclCommCount) and the HIP device
   // this rank's end of it runs on (ncclCommCuDevice): the run records quote
   // these, not the launcher's view.
@@ -103,10 +112,12 @@ class RcclComm {
     MXS_CHECK(comm_ != nullptr, "RCCL communicator aborted (an earlier wait timed out or failed)");
     return comm_;
   }
+  RcclComm() = default;
   // Mutable: a watchdog timeout inside a const wait() aborts and clears it.
   mutable ncclComm_t comm_ = nullptr;
   int rank_ = 0;
   int nranks_ = 1;
+  int max_ctas_ = 0;  // 0: RCCL's default
 };
 
 }  // namespace mxs

@@ -167,6 +167,9 @@ struct SolverConfig {
   // Auto: interior-first must beat serial by at least this fraction (and by
   // more than the measured spread) to be chosen.
   double min_gain = 0.03;
+  // RCCL backend: run the halo exchange on a communicator split off `comm`
+  // with at most this many workgroups per RCCL kernel (0 = RCCL's default).
+  int halo_max_ctas = 0;
   // A 1-rank RCCL-loopback solver follows the peers' schedule (every call
   // primes, its last pass is bare, the opening is chosen as with peers), so
   // one GPU rehearses the window shape an N-GPU run executes.
@@ -281,6 +284,10 @@ class StencilSolver {
   // "fresh" (no priming exchange needed), "fused", "direct" or "" (no run).
   const std::string& last_run_opening() const { return last_opening_; }
   int time_block() const { return block_; }
+  // The halo communicator's CTA cap (0: RCCL's default) and why it is not the
+  // requested one ("" when it is).
+  int halo_max_ctas() const { return halo_comm_ ? halo_comm_->max_ctas() : 0; }
+  const std::string& halo_comm_note() const { return halo_comm_note_; }
   int graph_supersteps() const { return chain_; }
   index_t cells_per_iteration() const { return tile_.width * tile_.height; }
 
@@ -395,6 +402,8 @@ class StencilSolver {
   T* cur_;
   T* nxt_;
   const RcclComm* comm_ = nullptr;  // watchdog waits and collective agreement when set
+  std::unique_ptr<RcclComm> halo_comm_;  // SolverConfig::halo_max_ctas (comm_ points to it)
+  std::string halo_comm_note_;
   std::unique_ptr<HaloExchanger<T>> ex_;
   std::unique_ptr<IpcDirectHalo<T>> direct_;  // SolverConfig::direct (On / Validate)
   bool direct_on_ = false;                    // super-steps use the direct push

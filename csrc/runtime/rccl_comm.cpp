@@ -68,6 +68,20 @@ void RcclComm::wait_all(const hipStream_t* streams, int n, const char* what) con
       what, [&] { abort(); });
 }
 
+std::unique_ptr<RcclComm> RcclComm::split_with_max_ctas(int max_ctas) const {
+  MXS_CHECK(max_ctas > 0, "split_with_max_ctas: cap must be positive, got " << max_ctas);
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.maxCTAs = max_ctas;
+  cfg.minCTAs = 1;
+  std::unique_ptr<RcclComm> c(new RcclComm());
+  c->rank_ = rank_;
+  c->nranks_ = nranks_;
+  c->max_ctas_ = max_ctas;
+  MXS_RCCL_CHECK(ncclCommSplit(live(), 0, rank_, &c->comm_, &cfg));
+  MXS_CHECK(c->comm_ != nullptr, "ncclCommSplit returned no communicator");
+  return c;
+}
+
 int RcclComm::count() const {
   int n = 0;
   MXS_RCCL_CHECK(ncclCommCount(live(), &n));

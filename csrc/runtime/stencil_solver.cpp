@@ -76,7 +76,17 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   multi_rank_ = world_ > 1 || (cfg_.loopback_self && cfg_.rehearse_peers);
   boot.allgather = cfg_.bootstrap;
   boot.timeout_s = comm_timeout() > 0 ? comm_timeout() : 60.0;
-  ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm, &boot);
+  // The halo's own communicator with a CTA cap (collective: the condition is
+  // config-level, the same on every rank).
+  if (cfg_.halo_max_ctas > 0 && comm_ && cfg_.backend == HaloBackend::Rccl) {
+    try {
+      halo_comm_ = comm_->split_with_max_ctas(cfg_.halo_max_ctas);
+      comm_ = halo_comm_.get();
+    } catch (const std::exception& e) {
+      halo_comm_note_ = std::string("CTA cap not applied: ") + e.what();
+    }
+  }
+  ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm_, &boot);
   const bool all_self_nbrs = plan.sends.empty();
   if (cfg_.kind == StencilKind::Jacobi5 && !all_self_nbrs) {
     if (cfg_.direct == DirectHalo::On && cfg_.backend == HaloBackend::Ipc) {

@@ -90,6 +90,10 @@ class StencilConfig:
     # the last pass of a call is bare, the opening is chosen as with peers), so
     # one GPU rehearses the window an N-GPU run executes.
     rehearse_peers: bool = False
+    # RCCL backend: the halo exchange on its own communicator whose kernels use
+    # at most this many workgroups (0 = RCCL's default): the interior-first
+    # opening's exchange runs on the 32-48 CUs the inner launch leaves free.
+    halo_max_ctas: int = 0
     # Super-steps estimated longer than this run from eager launches, not a
     # hipGraph (long passes: eager measured faster). 0 = always graphs.
     graph_max_superstep_us: float = 150.0
@@ -188,7 +192,8 @@ class Stencil2D:
                                           cfg.c_neighbor, radius, weights, cfg.variant, cfg.fuse_periodic,
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
                                           self._direct_mode(backend),
-                                          cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain)
+                                          cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain,
+                                          cfg.halo_max_ctas)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
