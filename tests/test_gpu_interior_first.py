@@ -338,3 +338,19 @@ def test_profile_window_phases_and_state(gpu, opening, fused):
     else:
         assert p["opening"] == "serial" and p["exchanges"] == 1
         assert ph["main:pack"][1] <= ph["main:rccl"][1] <= ph["main:unpack"][1] <= ph["main:pass"][1]
+
+
+def test_halo_communicator_with_cta_cap(gpu):
+    """--halo-max-ctas: the halo exchange on an RCCL communicator split off with
+    a CTA cap (ncclCommSplit + ncclConfig_t::maxCTAs). The split works on this
+    RCCL and the field is bitwise the uncapped schedule's."""
+    a = _loopback(16384, 8192, seed=81, opening="interior-first", rehearse_peers=True, time_block=20,
+                  halo_max_ctas=16)
+    b = _loopback(16384, 8192, seed=81, opening="serial", time_block=20)
+    assert a.solver.halo_max_ctas() == 16, a.solver.halo_comm_note()
+    for n in (20, 40):
+        a.run(n)
+        b.run(n)
+    a.synchronize()
+    b.synchronize()
+    assert torch.equal(a.core_view(), b.core_view())
