@@ -25,6 +25,7 @@
 // --opening auto|serial|interior-first (--halo-last = interior-first; default auto: prepare() times the
 // serial and interior-first openings, agrees the worst-rank medians over all ranks and keeps the faster),
 // --no-direct-halo (IPC backend: pack -> put -> unpack instead of the device-initiated push),
+// --halo-max-ctas N (RCCL: the halo exchange on a communicator split off with at most N workgroups per kernel),
 // --direct-halo on|off|validate (validate: prepare() compares the push with the backend's exchange bitwise on
 // every rank, times both, and uses it only if equal everywhere and faster),
 // --c-center C --c-neighbor C (default 0.2 / 0.2), --no-sum-form (keep the per-step evaluation in the
@@ -140,6 +141,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   MXS_CHECK(opening == "auto" || opening == "serial" || opening == "interior-first",
             "--opening must be auto, serial or interior-first, got " << opening);
   cfg.opening = opening == "serial" ? Opening::Serial : opening == "interior-first" ? Opening::InteriorFirst : Opening::Auto;
+  cfg.halo_max_ctas = int(cli.get_int("halo-max-ctas", 0));  // RCCL: the halo on a CTA-capped communicator
   cfg.loopback_self = loopback;
   cfg.coeffs = {c_center, c_neighbor, sum_form};
   cfg.time_block = time_block;
