@@ -71,7 +71,7 @@ int run(MpiEnv& env, const Cli& cli, index_t n_global) {
       std::cout << os.str() << std::flush;
     }
     std::string ar = cli.get("allreduce", "auto");
-    if (ar == "auto") ar = (size > 1 && env.local_size() <= dev.devices_used) ? "rccl" : "mpi";
+    if (ar == "auto") ar = (size > 1 && !dev.shared) ? "rccl" : "mpi";
     std::unique_ptr<RcclComm> comm;
     if (ar == "rccl" && mode != kernels::DotReduce::HostPartials) {
       std::string uid = rank == 0 ? RcclComm::make_unique_id() : std::string(sizeof(ncclUniqueId), '\0');

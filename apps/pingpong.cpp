@@ -123,7 +123,7 @@ int main(int argc, char** argv) {
   else sizes = parse_sweep(cli.get("sweep", "8:268435456"));
   std::string transport = cli.get("transport", "auto");
   if (cli.flag("host-copy")) transport = "mpi-staged";
-  if (transport == "auto") transport = env.size() >= 2 ? (env.local_size() > dev.devices_used ? "mpi-staged" : "rccl")
+  if (transport == "auto") transport = env.size() >= 2 ? (dev.shared ? "mpi-staged" : "rccl")
                                                          : "loopback";
   const std::string mode = cli.get("mode", "blocking");
   const int warmup = int(cli.get_int("warmup", 5)), reps = int(cli.get_int("reps", 20));

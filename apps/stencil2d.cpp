@@ -84,7 +84,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   const bool loopback = cli.flag("loopback");
   if (backend == "auto") {
     if (env.size() == 1) backend = loopback ? "rccl" : "local";
-    else if (env.local_size() > dev.devices_used) backend = "ipc";  // GPUs shared: RCCL refuses
+    else if (dev.shared) backend = "ipc";  // GPUs shared: RCCL refuses
     else backend = "rccl";
   }
   // Temporal blocking (timed runs on the solver backends): S Jacobi steps per
@@ -132,9 +132,9 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   // they hide (docs/PERF.md). Ranks sharing a GPU never overlap by default: their
   // cross-process waits plus the forked branch oversubscribe the GPU's queues and
   // get time-sliced (measured: 3-28 vs ~3000 Gcells/s).
-  const bool shared_gpu = env.local_size() > dev.devices_used;
+  const bool shared_gpu = dev.shared;
   // Ranks sharing a GPU: each persistent stencil kernel takes its share of the chip.
-  kernels::set_gpu_share(shared_gpu ? std::max(1, env.local_size() / std::max(1, dev.devices_used)) : 1);
+  kernels::set_gpu_share(dev.sharing);
   cfg.overlap = cli.flag("overlap") || (!cli.flag("no-overlap") && !shared_gpu && time_block == 1);
   cfg.use_graph = !cli.flag("no-graph");
   const std::string opening = cli.flag("halo-last") ? "interior-first" : cli.get("opening", "auto");

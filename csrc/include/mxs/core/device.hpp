@@ -19,6 +19,11 @@ struct DeviceBinding {
   int devices_visible = 0;
   int devices_used = 0;
   std::string mode;  // "bunch" | "rrobin"
+  // Some other rank of the job runs on this rank's GPU (device UUIDs compared
+  // over all ranks, not counts: a launcher that gives each rank one visible
+  // device makes every rank see "1 device" on distinct GPUs).
+  bool shared = false;
+  int sharing = 1;  // ranks on this GPU, this one included
 };
 
 // Selects and sets (hipSetDevice) this rank's GPU. mode "bunch": local_rank % n;

@@ -33,6 +33,13 @@ DeviceBinding bind_device(const MpiEnv& env, const std::string& mode) {
   else
     b.device = b.local_rank % b.devices_used;
   MXS_HIP_CHECK(hipSetDevice(b.device));
+  hipUUID u{};
+  MXS_HIP_CHECK(hipDeviceGetUuid(&u, b.device));
+  const std::string mine(u.bytes, sizeof(u.bytes));
+  int same = 0;
+  for (const auto& other : mpi_allgather_bytes(MPI_COMM_WORLD, mine)) same += other == mine ? 1 : 0;
+  b.sharing = same;
+  b.shared = same > 1;
   return b;
 }
 

@@ -21,7 +21,6 @@ from __future__ import annotations
 import argparse
 import json
 import math
-import os
 import sys
 import time
 from dataclasses import asdict, dataclass, field
@@ -147,8 +146,11 @@ class Stencil2D:
         self._init_data()
         self.iteration = 0  # Jacobi iterations applied to the field (checkpoint header)
 
-        local = int(os.environ.get("LOCAL_WORLD_SIZE", self.ctx.world_size))
-        self.shared_gpu = dev.type == "cuda" and local > max(1, torch.cuda.device_count())
+        # Ranks on this rank's GPU (device UUIDs compared over all ranks, not
+        # counts: a launcher that gives each rank one visible device makes every
+        # rank see "1 device" on distinct GPUs, and RCCL is then the backend).
+        self.gpu_sharing = gpu_sharing(self.ctx, dev)
+        self.shared_gpu = self.gpu_sharing > 1
         backend = cfg.backend
         if dev.type != "cuda":
             backend = "torch"
@@ -173,7 +175,7 @@ class Stencil2D:
             H = hip()
             # Ranks sharing this GPU: each persistent kernel takes its share of
             # the chip, so all of them are resident at once.
-            H.set_gpu_share(max(1, local // max(1, torch.cuda.device_count())) if self.shared_gpu else 1)
+            H.set_gpu_share(self.gpu_sharing)
             if backend == "rccl":
                 self.comm = self.ctx.native_comm()
             torch.cuda.synchronize()
@@ -425,6 +427,18 @@ class Stencil2D:
             if i + 1 < len(stage_arrays):
                 text += "\n"
         return text
+
+
+def gpu_sharing(ctx: DistContext, dev: torch.device) -> int:
+    """How many ranks of ``ctx`` run on ``dev``'s GPU (this one included), by
+    device UUID (collective when distributed)."""
+    if dev.type != "cuda":
+        return 1
+    props = torch.cuda.get_device_properties(dev)
+    ident = str(getattr(props, "uuid", "") or getattr(props, "pci_bus_id", "") or dev.index).encode()
+    if not ctx.is_distributed:
+        return 1
+    return sum(1 for other in ctx.allgather_bytes(ident) if other == ident)
 
 
 def format_tile(arr: torch.Tensor) -> str:
