@@ -83,9 +83,9 @@ def task_ipc_pingpong_isolated(args):
     sys.path.insert(0, ROOT)
     import bench
 
-    ctx = init(backend="gloo", device="cuda")
+    ctx = init(backend="gloo", device=args.get("device", "cuda"))
     extras = {}
-    bench.pingpong_ipc_isolated(ctx, extras, args["max_bytes"], timeout_s=120.0)
+    bench.pingpong_ipc_isolated(ctx, extras, args["max_bytes"], timeout_s=float(args.get("timeout_s", 120.0)))
     ctx.barrier()
     ctx.destroy()
     return {"rank": ctx.rank, "extras": extras}

@@ -85,3 +85,13 @@ def test_bench_eight_ranks_cpu_walks_the_8gpu_path():
     # Self-description keys of an N > 1 record (GPU-only ones are absent on CPU).
     assert ex["timed_super_steps"] == [[1, 3]] and ex["halo"].startswith("torch-p2p")
     assert "pingpong_ipc" in ex and isinstance(ex["env"], dict)
+
+
+def test_isolated_ipc_pingpong_failure_is_recorded_not_fatal():
+    """bench.py's N >= 2 IPC ping-pong runs in child processes: when they fail
+    (here: no GPU at all), both ranks carry on and rank 0's record names the
+    error instead of losing the run."""
+    r = run_ranks("ipc_pingpong_isolated", 2, {"max_bytes": 4096, "device": "cpu", "timeout_s": 120})
+    ex = r[0]["extras"]
+    assert "pingpong_ipc_error" in ex and "child" in ex["pingpong_ipc_error"], ex
+    assert "pingpong_ipc_device_8B_latency_us" not in ex and r[1]["extras"] == {}
