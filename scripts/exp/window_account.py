@@ -48,9 +48,13 @@ def run(args) -> int:
         t_sync = time.monotonic_ns()
         torch.cuda.synchronize()
         t1 = time.monotonic_ns()
-        print(json.dumps({"window": i, "t0": t0, "run_returned": t_run, "sync_returned": t_sync, "t1": t1,
-                          "opening": st.solver.last_run_opening()}), flush=True)
+        rec = {"window": i, "t0": t0, "run_returned": t_run, "sync_returned": t_sync, "t1": t1,
+               "opening": st.solver.last_run_opening()}
         st.warm(20, 0.02)  # clocks back up between windows (bench runs 200 ms of this before its one window)
+        if args.replica:  # the same super-step, event-timed (no profiler): its GPU span
+            rec["replica"] = st.profile_window(20)
+            st.warm(20, 0.02)
+        print(json.dumps(rec), flush=True)
     return 0
 
 
@@ -90,15 +94,40 @@ def analyse(args) -> int:
     return 0
 
 
+def analyse_host(path: str) -> int:
+    """Without a profiler (rocprofv3's instrumentation adds ~100 us of host time
+    per window): host stamps of each window next to the GPU span of an
+    event-timed replica of the same super-step."""
+    rows = [json.loads(l) for l in open(path) if l.startswith('{"window"')]
+    keys = ["window", "run() host", "run() -> sync returned", "sync returned -> t1", "replica GPU span",
+            "window - GPU span"]
+    vals = []
+    for r in rows:
+        span = r["replica"]["gpu_span_us"]
+        w = (r["t1"] - r["t0"]) / 1e3
+        vals.append([w, (r["run_returned"] - r["t0"]) / 1e3, (r["sync_returned"] - r["run_returned"]) / 1e3,
+                     (r["t1"] - r["sync_returned"]) / 1e3, span, w - span])
+    med = [sorted(v[k] for v in vals)[len(vals) // 2] for k in range(len(keys))]
+    print(f"# window accounting without a profiler: {len(rows)} windows ({rows[0]['opening']}), medians (us)\n")
+    print("| " + " | ".join(keys) + " |")
+    print("|" + "---|" * len(keys))
+    print("| " + " | ".join(f"{m:.1f}" for m in med) + " |")
+    return 0
+
+
 def main() -> int:
     p = argparse.ArgumentParser()
     p.add_argument("tile", nargs="?", default="16384x8192")
     p.add_argument("windows", nargs="?", type=int, default=12)
     p.add_argument("--opening", default="auto")
     p.add_argument("--fused", action="store_true")
+    p.add_argument("--replica", action="store_true", help="run mode: also an event-timed replica per window")
+    p.add_argument("--host", help="analysis without a trace: the stamps + replicas of a --replica run")
     p.add_argument("--db")
     p.add_argument("--stamps")
     a = p.parse_args()
+    if a.host:
+        return analyse_host(a.host)
     return analyse(a) if a.db else run(a)
 
 
