@@ -334,6 +334,9 @@ def main(argv=None) -> int:
     p.add_argument("--halo-max-ctas", type=int, default=0,
                    help="N > 1: the halo exchange on an RCCL communicator split off with at most this many "
                         "workgroups per kernel (0 = RCCL's default)")
+    p.add_argument("--opening-graph", action="store_true",
+                   help="N > 1: replay the interior-first opening's main-stream chain (pack, RCCL, unpack, outer "
+                        "chunks) from a hipGraph captured in prepare()")
     p.add_argument("--direct-halo", default="off", choices=["off", "validate"],
                    help="N > 1: validate: prepare() compares the device-initiated push of the edge bands into the "
                         "neighbours' tiles (HIP IPC over xGMI) bitwise with the RCCL exchange on every rank and times "
@@ -392,7 +395,7 @@ def main(argv=None) -> int:
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback,
                         sum_form=not args.no_sum_form, opening=args.opening, rehearse_peers=args.rehearse_peers,
                         direct_halo=("validate" if args.direct_halo == "validate" else None),
-                        halo_max_ctas=args.halo_max_ctas,
+                        halo_max_ctas=args.halo_max_ctas, opening_graph=args.opening_graph,
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3)
@@ -428,6 +431,8 @@ def main(argv=None) -> int:
         extras["pipe_balanced_shares"] = bool(H.pipe_balanced())
         if st.solver is not None:
             extras["opening"] = st.solver.last_run_opening()
+            if args.opening_graph:
+                extras["opening_graph"] = st.solver.opening_graph_state()
             if args.halo_max_ctas:
                 extras["halo_max_ctas"] = int(st.solver.halo_max_ctas())
                 if st.solver.halo_comm_note():

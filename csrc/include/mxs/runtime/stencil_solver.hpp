@@ -167,6 +167,11 @@ struct SolverConfig {
   // Auto: interior-first must beat serial by at least this fraction (and by
   // more than the measured spread) to be chosen.
   double min_gain = 0.03;
+  // Interior-first opening: replay its main-stream chain (pack -> RCCL ->
+  // unpack -> outer chunks) from a hipGraph captured in prepare(), so the host
+  // issues one launch after the inner chunks instead of the RCCL group calls
+  // and three launches (the outer chunks can start as soon as the unpack ends).
+  bool opening_graph = false;
   // RCCL backend: run the halo exchange on a communicator split off `comm`
   // with at most this many workgroups per RCCL kernel (0 = RCCL's default).
   int halo_max_ctas = 0;
@@ -287,6 +292,13 @@ class StencilSolver {
   // The halo communicator's CTA cap (0: RCCL's default) and why it is not the
   // requested one ("" when it is).
   int halo_max_ctas() const { return halo_comm_ ? halo_comm_->max_ctas() : 0; }
+  // SolverConfig::opening_graph: "off", "not used yet", "captured" or "capture failed".
+  std::string opening_graph_state() const {
+    if (!cfg_.opening_graph) return "off";
+    for (const auto& hl : halo_lasts_)
+      if (hl && hl->chain_tried) return hl->chain_ok ? "captured" : "capture failed";
+    return "not used yet";
+  }
   const std::string& halo_comm_note() const { return halo_comm_note_; }
   int graph_supersteps() const { return chain_; }
   index_t cells_per_iteration() const { return tile_.width * tile_.height; }
@@ -337,7 +349,12 @@ class StencilSolver {
     kernels::ChunkPassShape inner_shape, outer_shape;  // blocks = workgroups of each launch
     kernels::HaloLastSchedule sched;
     DeviceBuffer<kernels::PassChunk> inner_table, outer_table;
+    // SolverConfig::opening_graph: the main stream's part (pack -> RCCL ->
+    // unpack -> outer chunks) captured once per buffer orientation.
+    GraphExec chain[2];
+    bool chain_tried = false, chain_ok = false;
   };
+  bool capture_chain(HaloLastPass* hl);
   HaloLastPass* halo_last_pass(int S, bool build);  // nullptr: not in use / no form for S
   std::unique_ptr<HaloLastPass> build_halo_last(int S, int outer_wgs);  // nullptr: no form for S
   void enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks* marks = nullptr);

@@ -900,6 +900,11 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
   MXS_TRACE_RANGE("stencil.superstep_halo_last");
   hipStream_t m = main_.get(), side = side_.get();
   join_side();
+  if (!marks && cfg_.opening_graph && !hl->chain_tried) {
+    // Captured at first use (prepare()'s untimed warm pass of the opening).
+    hl->chain_tried = true;
+    hl->chain_ok = capture_chain(hl);
+  }
   // The inner launch reads cur: it must follow everything enqueued on main.
   // When main has drained (a call after synchronize()) the fork is skipped: a
   // cross-stream wait costs ~15 us of queue-to-queue latency, and the timed
@@ -922,6 +927,12 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
     const char* e = experiment_env("MXS_HALO_LAST_COPY_WGS");
     return e ? std::atoi(e) : 0;
   }();
+  if (!marks && hl->chain_ok) {
+    // The main stream's chain from its graph: one launch instead of the RCCL
+    // group calls and three kernel launches.
+    hl->chain[cur == buf_a_ ? 0 : 1].launch(m);
+    return;
+  }
   ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
   ex_->set_copy_grid(copy_wgs);
   if (marks) {
@@ -940,6 +951,48 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
   kernels::stencil5_chunk_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->outer_shape, hl->outer_table.get(),
                                   hl->sched.outer.entries, m);
   if (marks) marks->mark("main:outer chunks", m);
+}
+
+template <typename T>
+bool StencilSolver<T>::capture_chain(HaloLastPass* hl) {
+  MXS_TRACE_RANGE("stencil.graph_capture_opening");
+  hipStream_t m = main_.get();
+  for (int k = 0; k < 2; ++k) {
+    T* cur = k == 0 ? buf_a_ : buf_b_;
+    T* nxt = k == 0 ? buf_b_ : buf_a_;
+    hipGraph_t g = nullptr;
+    if (hipStreamBeginCapture(m, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+      (void)hipGetLastError();
+      return false;
+    }
+    bool ok = true;
+    try {
+      static const int copy_wgs = [] {
+        const char* e = experiment_env("MXS_HALO_LAST_COPY_WGS");
+        return e ? std::atoi(e) : 0;
+      }();
+      ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
+      ex_->set_copy_grid(copy_wgs);
+      ex_->exchange(cur, m);
+      ex_->set_copy_grid(0);
+      ex_->set_copy_block(0);
+      kernels::stencil5_chunk_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->outer_shape, hl->outer_table.get(),
+                                      hl->sched.outer.entries, m);
+    } catch (const std::exception&) {
+      ok = false;
+      ex_->set_copy_grid(0);
+      ex_->set_copy_block(0);
+    }
+    const hipError_t end = hipStreamEndCapture(m, &g);
+    if (!ok || end != hipSuccess || g == nullptr) {
+      (void)hipGetLastError();
+      if (g) (void)hipGraphDestroy(g);
+      return false;
+    }
+    if (!hl->chain[k].adopt(g)) return false;
+    hl->chain[k].upload(m);
+  }
+  return true;
 }
 
 template <typename T>

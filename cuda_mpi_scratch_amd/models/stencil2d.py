@@ -93,6 +93,9 @@ class StencilConfig:
     # at most this many workgroups (0 = RCCL's default): the interior-first
     # opening's exchange runs on the 32-48 CUs the inner launch leaves free.
     halo_max_ctas: int = 0
+    # Interior-first opening: replay the main stream's chain (pack, RCCL,
+    # unpack, outer chunks) from a hipGraph captured in prepare().
+    opening_graph: bool = False
     # Super-steps estimated longer than this run from eager launches, not a
     # hipGraph (long passes: eager measured faster). 0 = always graphs.
     graph_max_superstep_us: float = 150.0
@@ -195,7 +198,7 @@ class Stencil2D:
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
                                           self._direct_mode(backend),
                                           cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain,
-                                          cfg.halo_max_ctas)
+                                          cfg.halo_max_ctas, cfg.opening_graph)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()

@@ -11,10 +11,12 @@
 #   smoke                  __graft_entry__.smoke()                  -> OUT/smoke.txt
 #   bench [BENCH ARGS]     python bench.py ARGS                      -> OUT/bench.txt (JSON line echoed)
 #   prof NAME [BENCH ARGS] rocprofv3 --kernel-trace --stats of bench.py ARGS -> OUT/prof_NAME/
-#   window TILE REPS [--serial]
+#   window TILE REPS [--serial | MODES...]
 #                          interleaved single-shot bench-flow windows on TILE: RCCL loopback in the
-#                          peers' schedule (auto opening, and forced serial with --serial) against the
-#                          fused-periodic tile (no exchange) -> OUT/window_TILE.jsonl + medians
+#                          peers' schedule against the fused-periodic tile (no exchange). MODES (default
+#                          "auto fused"; --serial = "auto serial fused"): auto, serial, ifirst (forced
+#                          interior-first), graph (interior-first, its main-stream chain as a hipGraph),
+#                          fused -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
 #   final                  tests + smoke + the driver's bench command + its kernel-trace profile
 set -uo pipefail
@@ -77,18 +79,22 @@ task_prof() {
 }
 
 task_window() {
-  local tile=$1 reps=$2 serial=${3:-}
+  local tile=$1 reps=$2
+  shift 2
   local log="$OUT/window_$tile.jsonl"
   : > "$log"
   local modes="auto fused"
-  [ "$serial" = "--serial" ] && modes="auto serial fused"
+  if [ "${1:-}" = "--serial" ]; then modes="auto serial fused"; elif [ $# -gt 0 ]; then modes="$*"; fi
   for i in $(seq "$reps"); do
     for mode in $modes; do
       local args=(--global "$tile" --steps 20 --warmup 5 --no-extras)
       case $mode in
         auto) args+=(--loopback --rehearse-peers) ;;
         serial) args+=(--loopback --rehearse-peers --opening serial) ;;
+        ifirst) args+=(--loopback --rehearse-peers --opening interior-first) ;;
+        graph) args+=(--loopback --rehearse-peers --opening interior-first --opening-graph) ;;
         fused) ;;
+        *) echo "unknown window mode '$mode'"; exit 2 ;;
       esac
       timeout -k 10 200 python bench.py "${args[@]}" > "$OUT/window_last.txt" 2>&1 || {
         echo "window run failed ($mode)"
@@ -99,14 +105,15 @@ task_window() {
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1]); e = d["extras"]
 print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["ms_per_step"] * d["steps"], 4),
-                  "opening": e.get("opening"), "phases": e.get("window_phases")}))
+                  "opening": e.get("opening"), "opening_graph": e.get("opening_graph"),
+                  "phases": e.get("window_phases")}))
 PY
     done
   done
   python - "$log" <<'PY'
 import json, sys
 rs = [json.loads(l) for l in open(sys.argv[1])]
-for m in ("auto", "serial", "fused"):
+for m in ("auto", "serial", "ifirst", "graph", "fused"):
     v = sorted(r["window_ms"] for r in rs if r["mode"] == m)
     if v:
         print(m, "n", len(v), "median", v[len(v) // 2], "min", v[0], "max", v[-1])
