@@ -337,6 +337,8 @@ def main(argv=None) -> int:
     p.add_argument("--opening-graph", action="store_true",
                    help="N > 1: replay the interior-first opening's main-stream chain (pack, RCCL, unpack, outer "
                         "chunks) from a hipGraph captured in prepare()")
+    p.add_argument("--no-fused-pack", action="store_true",
+                   help="N > 1: pack the halo with its own launch before each exchange instead of in the pass")
     p.add_argument("--direct-halo", default="off", choices=["off", "validate"],
                    help="N > 1: validate: prepare() compares the device-initiated push of the edge bands into the "
                         "neighbours' tiles (HIP IPC over xGMI) bitwise with the RCCL exchange on every rank and times "
@@ -396,6 +398,7 @@ def main(argv=None) -> int:
                         sum_form=not args.no_sum_form, opening=args.opening, rehearse_peers=args.rehearse_peers,
                         direct_halo=("validate" if args.direct_halo == "validate" else None),
                         halo_max_ctas=args.halo_max_ctas, opening_graph=args.opening_graph,
+                        fused_pack=not args.no_fused_pack,
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3)
@@ -443,6 +446,9 @@ def main(argv=None) -> int:
                 # Halo exchanges inside the timed window: one per super-step (with
                 # peers the call primes and ends on a bare pass).
                 extras["timed_exchanges"] = int(st.solver.last_run_exchanges())
+                # Of those, the exchanges whose pack the preceding pass wrote (fused pack).
+                extras["timed_fused_packs"] = int(st.solver.last_run_fused_packs())
+                extras["fused_pack"] = bool(st.solver.fused_pack())
                 extras["schedule_choice"] = {k: (round(v, 4) if isinstance(v, float) else v)
                                              for k, v in st.solver.schedule_times().items()}
         # Who ran: the RCCL communicator's own view (not the launcher's) and every rank's device.

@@ -71,6 +71,14 @@ class HaloExchanger {
   void pack(T* tile, hipStream_t stream);
   void transfer(hipStream_t stream);
   void unpack(T* tile, hipStream_t stream);
+  // An exchange whose send buffer already holds the tile's bands (a pipeline
+  // pass with the fused pack wrote them): transfer + unpack.
+  void exchange_packed(T* tile, hipStream_t stream);
+  // The plan's send windows in core coordinates of tile `g`, for the fused
+  // pack (kernels::PackSegs); false when the plan cannot take it: no remote
+  // peers, self copies (they stay in the pack launch), more than
+  // kernels::kMaxPackSegs windows.
+  bool pack_windows(const TileGeom& g, kernels::PackSegs* out) const;
 
   const HaloPlan& plan() const { return plan_; }
   HaloBackend backend() const { return backend_; }

@@ -172,6 +172,13 @@ struct SolverConfig {
   // issues one launch after the inner chunks instead of the RCCL group calls
   // and three launches (the outer chunks can start as soon as the unpack ends).
   bool opening_graph = false;
+  // Fused halo pack: the whole-core pipeline passes of the post-exchange
+  // schedules (the bare pass, the interior-first opening's outer chunks, the
+  // steady super-steps) also write their send bands into the exchange's send
+  // buffer, so the next exchange is RCCL + unpack (no pack launch). Applies
+  // where the plan has remote peers and the pass takes a pipeline form (fp32
+  // S > 16, fp64 S 9..16 on whole vectors); other passes keep the pack launch.
+  bool fused_pack = true;
   // RCCL backend: run the halo exchange on a communicator split off `comm`
   // with at most this many workgroups per RCCL kernel (0 = RCCL's default).
   int halo_max_ctas = 0;
@@ -225,6 +232,7 @@ class StencilSolver {
   void field_changed() {
     ghost_fresh_ = false;
     range_checked_ = false;
+    packed_ = nullptr;
   }
   // Fault injection (like the apps' --fault-inject): the host
   // sleeps `seconds` on entering `phase` ("prepare", "warm", "run",
@@ -269,6 +277,8 @@ class StencilSolver {
   double opening_ratio() const { return opening_ratio_; }
   double opening_ratio_iqr() const { return opening_spread_[1]; }
   int opening_samples() const { return opening_samples_; }
+  // This rank's paired ratios of every candidate (outer workgroups, ratios per round).
+  const std::vector<std::pair<int, std::vector<double>>>& opening_ratio_samples() const { return opening_ratio_samples_; }
   // Workgroups of the outer (ghost-ring) launch of the interior-first opening
   // at depth S (0: none built).
   int halo_last_outer_wgs(int S) const {
@@ -300,6 +310,10 @@ class StencilSolver {
     return "not used yet";
   }
   const std::string& halo_comm_note() const { return halo_comm_note_; }
+  // SolverConfig::fused_pack in effect (the plan's windows can take it).
+  bool fused_pack() const { return pack_.send != nullptr; }
+  // Exchanges of the last run() whose pack was fused into the preceding pass.
+  int last_run_fused_packs() const { return last_fused_packs_; }
   int graph_supersteps() const { return chain_; }
   index_t cells_per_iteration() const { return tile_.width * tile_.height; }
 
@@ -307,6 +321,17 @@ class StencilSolver {
   void enqueue_block(T* cur, T* nxt, int S);  // S <= block_ iterations, one exchange
   // `steps` iterations over core rows [r0, r1) x cols [c0, c1).
   void update(const T* in, T* out, int steps, index_t c0, index_t c1, index_t r0, index_t r1, hipStream_t s);
+  // Fused halo pack state. packed_: the buffer whose send bands the exchange's
+  // send buffer holds (nullptr: none / unknown). Every pass notes what it wrote
+  // (note_written); exchange() skips the pack launch when the send buffer
+  // already holds the tile's bands.
+  void core_pass(T* cur, T* nxt, int S, hipStream_t s, bool pack = true);  // whole core, fused pack if available
+  void note_written(T* out, bool packed) { packed_ = packed ? out : (packed_ == out ? nullptr : packed_); }
+  void exchange(T* tile, hipStream_t s);
+  void ensure_packed(T* tile, hipStream_t s);  // the send buffer holds tile's bands afterwards
+  kernels::PackTarget<T> pack_;  // send == nullptr: the fused pack is off
+  T* packed_ = nullptr;
+  int last_fused_packs_ = 0;
   // Graphs of `chain` consecutive super-steps of size S, one per buffer
   // orientation: g[0] starts from buf_a_, g[1] from buf_b_.
   struct GraphSet {
@@ -314,6 +339,8 @@ class StencilSolver {
     int chain = 1;
     bool ok = false;
     GraphExec g[2];
+    T* packed_after[2] = {nullptr, nullptr};  // packed_ after a replay of g[k]
+    int fused_packs = 0;                      // exchanges per replay whose pack was fused
   };
   // Graphs for super-step size S, captured on first use with a chain of at
   // most `count` super-steps (nullptr: graphs off or capture failed).
@@ -353,6 +380,10 @@ class StencilSolver {
     // unpack -> outer chunks) captured once per buffer orientation.
     GraphExec chain[2];
     bool chain_tried = false, chain_ok = false;
+    // The outer chunks take the fused pack: the inner chunks store no cell of
+    // a send window (checked on the host), so no launch writes the send buffer
+    // while RCCL reads it and the outer launch alone writes every send band.
+    bool outer_packs = false;
   };
   bool capture_chain(HaloLastPass* hl);
   HaloLastPass* halo_last_pass(int S, bool build);  // nullptr: not in use / no form for S
@@ -378,6 +409,7 @@ class StencilSolver {
   double opening_spread_[2] = {0, 0};        // agreed IQRs: serial (ms), paired ratio
   double opening_ratio_ = 0;                 // agreed median paired ratio interior-first / serial
   int opening_samples_ = 0;
+  std::vector<std::pair<int, std::vector<double>>> opening_ratio_samples_;
   std::string opening_choice_;               // "" before prepare() decided, "serial" or "interior-first"
   std::string opening_reason_;
   void choose_opening(int S);                // Opening::Auto: time both, agree, keep the faster

@@ -410,8 +410,9 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
                        py::object bootstrap, int graph_supersteps, bool sum_form, const std::string& direct_halo,
                        double graph_max_superstep_us, const std::string& opening, bool rehearse_peers,
-                       double min_gain, int halo_max_ctas, bool opening_graph) {
+                       double min_gain, int halo_max_ctas, bool opening_graph, bool fused_pack) {
              SolverConfig cfg;
+             cfg.fused_pack = fused_pack;
              cfg.halo_max_ctas = halo_max_ctas;
              cfg.opening_graph = opening_graph;
              if (opening == "auto") cfg.opening = Opening::Auto;
@@ -454,7 +455,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
            py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = "off",
            py::arg("graph_max_superstep_us") = 150.0, py::arg("opening") = "auto", py::arg("rehearse_peers") = false,
-           py::arg("min_gain") = 0.03, py::arg("halo_max_ctas") = 0, py::arg("opening_graph") = false,
+           py::arg("min_gain") = 0.03, py::arg("halo_max_ctas") = 0, py::arg("opening_graph") = false, py::arg("fused_pack") = true,
            py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")
@@ -476,6 +477,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
                d["ratio_iqr"] = s.opening_ratio_iqr();
                d["samples"] = s.opening_samples();
                d["outer_wgs"] = s.halo_last_outer_wgs(s.time_block());
+               // This rank's paired ratios per candidate outer set (diagnostics).
+               py::list rs;
+               for (const auto& c : s.opening_ratio_samples()) rs.append(py::make_tuple(c.first, c.second));
+               d["candidate_ratios"] = rs;
                return d;
              });
            },
@@ -495,6 +500,11 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def("halo_max_ctas", [](SolverHandle& h) { return h.visit([](auto& s) { return s.halo_max_ctas(); }); },
            "CTA cap of the halo's RCCL communicator (0: RCCL's default)")
       .def("halo_comm_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.halo_comm_note(); }); })
+      .def("fused_pack", [](SolverHandle& h) { return h.visit([](auto& s) { return s.fused_pack(); }); },
+           "whether the passes write the send bands into the exchange's send buffer (SolverConfig::fused_pack)")
+      .def("last_run_fused_packs",
+           [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_fused_packs(); }); },
+           "exchanges of the last run() whose pack was fused into the preceding pass")
       .def("opening_graph_state",
            [](SolverHandle& h) { return h.visit([](auto& s) { return s.opening_graph_state(); }); })
       .def("last_run_opening", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_opening(); }); },

@@ -114,6 +114,15 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   constexpr int N = 16 / int(sizeof(T));
   fused_ = cfg_.fuse_periodic_self && all_self && cfg_.kind == StencilKind::Jacobi5 && tile_.width % N == 0 &&
            kernels::stencil5_periodic_supported<T>(tile_);
+  // Fused halo pack: the plan's send windows as core rectangles (a per-rank
+  // property: it changes which launches run, not the collectives).
+  if (cfg_.fused_pack && cfg_.kind == StencilKind::Jacobi5 && !fused_) {
+    kernels::PackSegs segs;
+    if (ex_->pack_windows(tile_, &segs) && kernels::pack_segs_ok<T>(tile_, segs)) {
+      pack_.send = ex_->send_buffer();
+      pack_.segs = segs;
+    }
+  }
   // Interior-first opening: RCCL with a wire transfer, the tuned kernel forms,
   // every edge a neighbour's (time blocking), the thin-strip overlap off.
   halo_last_allowed_ = cfg_.opening != Opening::Serial && cfg_.backend == HaloBackend::Rccl && !plan.sends.empty() &&
@@ -177,6 +186,37 @@ void StencilSolver<T>::update(const T* in, T* out, int steps, index_t c0, index_
   }
 }
 
+template <typename T>
+void StencilSolver<T>::core_pass(T* cur, T* nxt, int S, hipStream_t s, bool pack) {
+  if (pack && pack_.send && cfg_.kind == StencilKind::Jacobi5 && S > 1) {
+    kernels::PackTarget<T> pk = pack_;
+    kernels::stencil5_tb<T>(cur, nxt, tile_, S, 0, tile_.width, 0, tile_.height, cfg_.coeffs, false, s, cfg_.variant,
+                            &pk);
+    note_written(nxt, pk.applied);
+    return;
+  }
+  update(cur, nxt, S, 0, tile_.width, 0, tile_.height, s);
+  note_written(nxt, false);
+}
+
+template <typename T>
+void StencilSolver<T>::exchange(T* tile, hipStream_t s) {
+  if (pack_.send && packed_ == tile) {
+    ex_->exchange_packed(tile, s);
+    ++last_fused_packs_;
+    return;
+  }
+  ex_->exchange(tile, s);
+  packed_ = tile;  // the pack launch wrote tile's bands
+}
+
+template <typename T>
+void StencilSolver<T>::ensure_packed(T* tile, hipStream_t s) {
+  if (!pack_.send || packed_ == tile) return;
+  ex_->pack(tile, s);
+  packed_ = tile;
+}
+
 // Stream roles: the MAIN stream (the capture origin, high priority) carries the
 // exchange chain pack -> RCCL -> unpack and the boundary update; the interior
 // sweep forks onto the SIDE stream. RCCL calls must sit on the capture-origin
@@ -194,6 +234,7 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
   if (direct_on_) {  // the neighbours pushed cur's ghost ring after their previous pass
     direct_->wait(m);
     update(cur, nxt, S, 0, w, 0, h, m);
+    note_written(nxt, false);
     direct_->push(nxt, m);
     return;
   }
@@ -202,11 +243,14 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
     // sees to it), then the exchange of its output. The pass is on the GPU
     // before the host has enqueued the RCCL group (~25 us of host time that
     // a pre-exchange super-step leaves the GPU idle for).
-    update(cur, nxt, S, 0, w, 0, h, m);
+    core_pass(cur, nxt, S, m);  // writes nxt's send bands too when the pack is fused
     ex_->set_copy_block(0);  // alone on the GPU: the default (256-thread) copies
-    ex_->exchange(nxt, m);
+    exchange(nxt, m);
     return;
   }
+  // The thin-strip overlap exchanges before the pass and splits the pass into
+  // launches that do not pack: explicit packs.
+  note_written(nxt, false);
   const index_t d = std::max(radius_, S);  // dependency depth of the super-step
   constexpr index_t N = 16 / index_t(sizeof(T));
   // Temporally blocked Jacobi: the kernels take any vector-aligned column range,
@@ -220,6 +264,7 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
     update(cur, nxt, S, dl, dr, d, h - d, side);
     interior_.record(side);
     ex_->exchange(cur, m);
+    packed_ = cur;
     update(cur, nxt, S, 0, w, 0, d, m);
     update(cur, nxt, S, 0, w, h - d, h, m);
     update(cur, nxt, S, 0, dl, d, h - d, m);
@@ -232,6 +277,7 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
   update(cur, nxt, S, 0, w, d, h - d, side);  // interior (its edge columns are redone below)
   interior_.record(side);
   ex_->exchange(cur, m);
+  packed_ = cur;
   interior_.wait_on(m);
   update(cur, nxt, S, 0, w, 0, d, m);
   update(cur, nxt, S, 0, w, h - d, h, m);
@@ -270,6 +316,13 @@ bool StencilSolver<T>::capture(GraphSet& gs) {
       return false;
     }
     bool ok = true;
+    // The captured launches must not depend on what the send buffer holds when
+    // a replay starts: capture from "unknown" (a super-step packs before it
+    // exchanges unless its own pass fused the pack) and record the state a
+    // replay leaves.
+    T* const saved = packed_;
+    const int fused_before = last_fused_packs_;
+    packed_ = nullptr;
     try {
       for (int c = 0; c < gs.chain; ++c) {  // chain consecutive super-steps per graph
         enqueue_block(a, b, gs.S);
@@ -279,6 +332,10 @@ bool StencilSolver<T>::capture(GraphSet& gs) {
       graph_status_ = std::string("capture failed: ") + e.what();
       ok = false;
     }
+    gs.packed_after[k] = packed_;
+    gs.fused_packs = last_fused_packs_ - fused_before;
+    packed_ = saved;
+    last_fused_packs_ = fused_before;
     const hipError_t end = hipStreamEndCapture(main_.get(), &g);
     if (!ok || end != hipSuccess || g == nullptr) {
       (void)hipGetLastError();
@@ -357,7 +414,7 @@ void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
   // exchanges first and leaves it stale.
   if (post_exchange() && !ghost_fresh_) {
     if (first && last_opening_.empty()) last_opening_ = "serial";
-    ex_->exchange(cur_, main_.get());
+    exchange(cur_, main_.get());
     ++last_exchanges_;
   }
   if (first && last_opening_.empty()) last_opening_ = post_exchange() ? "fresh" : "overlap";
@@ -373,7 +430,10 @@ void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
   if (GraphSet* gs = full > 0 ? graphs_for(S, full) : nullptr) {
     for (; i + gs->chain <= full; i += gs->chain) {
       MXS_TRACE_RANGE("stencil.graph_launch");
-      gs->g[cur_ == buf_a_ ? 0 : 1].launch(main_.get());
+      const int k = cur_ == buf_a_ ? 0 : 1;
+      gs->g[k].launch(main_.get());
+      packed_ = gs->packed_after[k];
+      last_fused_packs_ += gs->fused_packs;
       if (gs->chain % 2) std::swap(cur_, nxt_);  // an odd chain ends on the other buffer
     }
   }
@@ -395,7 +455,9 @@ template <typename T>
 void StencilSolver<T>::enqueue_bare_pass(T* cur, T* nxt, int S) {
   MXS_TRACE_RANGE("stencil.superstep_bare");
   if (direct_on_) direct_->wait(main_.get());  // the neighbours' pushes of cur's ring
-  update(cur, nxt, S, 0, tile_.width, 0, tile_.height, main_.get());
+  // With the fused pack the bare pass leaves its send bands packed: the next
+  // call's priming exchange is RCCL + unpack.
+  core_pass(cur, nxt, S, main_.get(), !direct_on_);
 }
 
 // Direct halo: every pass pushes its output bands, so the current tile's ghost
@@ -465,6 +527,7 @@ void StencilSolver<T>::run(int iters) {
   MXS_TRACE_RANGE("stencil.run");
   last_blocks_.clear();
   last_exchanges_ = 0;
+  last_fused_packs_ = 0;
   last_opening_.clear();
   if (iters <= 0) return;
   maybe_stall("run");
@@ -586,7 +649,7 @@ void StencilSolver<T>::choose_opening(int S) {
   if (hl) cands.push_back(hl);
   for (auto& h : alt) cands.push_back(h.get());
   if (!ghost_fresh_) {
-    ex_->exchange(cur_, main_.get());
+    exchange(cur_, main_.get());
     ghost_fresh_ = true;
   }
   // GPU time of one opening, from drained streams after a device barrier and
@@ -606,6 +669,7 @@ void StencilSolver<T>::choose_opening(int S) {
     join_side();
     enqueue_block(cur_, nxt_, S);
     join_side();
+    ensure_packed(cur_, main_.get());  // as a window finds it: the last pass packed the field's bands
     wait_idle("prepare: opening timing");
     device_barrier("prepare: opening timing");
     e0.record(starts_on_side ? side_.get() : main_.get());
@@ -620,7 +684,7 @@ void StencilSolver<T>::choose_opening(int S) {
   std::vector<std::vector<double>> t_cand(kCands), ratio(kCands);
   for (int rep = 0; rep < kReps; ++rep) {
     const double serial = timed(false, [&] {
-      ex_->exchange(cur_, main_.get());
+      exchange(cur_, main_.get());
       enqueue_bare_pass(cur_, nxt_, S);
     });
     if (rep > 0) t_serial.push_back(serial);
@@ -629,7 +693,7 @@ void StencilSolver<T>::choose_opening(int S) {
         if (c < cands.size()) {
           enqueue_halo_last(cur_, nxt_, cands[c]);
         } else {
-          ex_->exchange(cur_, main_.get());
+          exchange(cur_, main_.get());
           enqueue_bare_pass(cur_, nxt_, S);
         }
       });
@@ -667,6 +731,8 @@ void StencilSolver<T>::choose_opening(int S) {
   opening_spread_[1] = r < kMissing ? r_iqr : 0.0;
   opening_ratio_ = r < kMissing ? r : 0.0;
   opening_samples_ = n;
+  opening_ratio_samples_.clear();
+  for (size_t c = 0; c < cands.size(); ++c) opening_ratio_samples_.emplace_back(cands[c]->sched.outer.blocks, ratio[c]);
   if (win && best > 0 && best - 1 < alt.size()) {  // keep the measured best outer set for S
     for (auto& h : halo_lasts_)
       if (h->S == S) h = std::move(alt[best - 1]);
@@ -715,7 +781,7 @@ void StencilSolver<T>::validate_direct(int S) {
   if (!diff_.get()) diff_.reset(1);
   const size_t bytes = size_t(tile_.alloc_elems()) * sizeof(T);
   poison_ghost(cur_);
-  ex_->exchange(cur_, m);
+  exchange(cur_, m);
   MXS_HIP_CHECK(hipMemcpyAsync(ref_.get(), cur_, bytes, hipMemcpyDeviceToDevice, m));
   poison_ghost(cur_);
   wait_idle("prepare: direct halo validation");
@@ -734,7 +800,7 @@ void StencilSolver<T>::validate_direct(int S) {
   wait_idle("prepare: direct halo validation");
   std::vector<double> bad{double(diff)};
   agree_max(bad, "prepare: direct halo validation");
-  ex_->exchange(cur_, m);  // whatever the push delivered, the ring is the backend's again
+  exchange(cur_, m);  // whatever the push delivered, the ring is the backend's again
   ghost_fresh_ = true;
   if (bad[0] != 0.0) {
     direct_state_ = "rejected: the direct push differs from the " + std::string(cfg_.backend == HaloBackend::Rccl
@@ -764,15 +830,20 @@ void StencilSolver<T>::validate_direct(int S) {
   std::vector<double> t_backend, t_direct, ratio;
   const index_t w = tile_.width, h = tile_.height;
   for (int rep = 0; rep < kReps; ++rep) {
-    const double tb = timed(halo_last_on_ && halo_last_pass(S, false), [&] { enqueue_block(cur_, nxt_, S); },
-                            [&] {
-                              if (halo_last_on_) {
-                                enqueue_opening(S, false);
-                              } else {
-                                ex_->exchange(cur_, m);
-                                update(cur_, nxt_, S, 0, w, 0, h, m);
-                              }
-                            });
+    const double tb = timed(
+        halo_last_on_ && halo_last_pass(S, false),
+        [&] {
+          enqueue_block(cur_, nxt_, S);
+          ensure_packed(cur_, m);
+        },
+        [&] {
+          if (halo_last_on_) {
+            enqueue_opening(S, false);
+          } else {
+            exchange(cur_, m);
+            core_pass(cur_, nxt_, S, m);
+          }
+        });
     // Direct: the priming push of the current bands, the wait for the
     // neighbours' pushes, the pass (a call's bare last super-step).
     const double td = timed(
@@ -781,11 +852,13 @@ void StencilSolver<T>::validate_direct(int S) {
           direct_->push(cur_, m);
           direct_->wait(m);
           update(cur_, nxt_, S, 0, w, 0, h, m);
+          note_written(nxt_, false);
         },
         [&] {
           direct_->push(cur_, m);
           direct_->wait(m);
           update(cur_, nxt_, S, 0, w, 0, h, m);
+          note_written(nxt_, false);
         });
     if (rep > 0) {
       t_backend.push_back(tb);
@@ -870,6 +943,20 @@ std::unique_ptr<typename StencilSolver<T>::HaloLastPass> StencilSolver<T>::build
   hl->inner_shape.blocks = hl->sched.inner.blocks;
   hl->outer_shape = shape;
   hl->outer_shape.blocks = hl->sched.outer.blocks;
+  // The fused pack goes to the outer launch only if no inner chunk stores a
+  // cell of a send window (a ghost ring deeper than the pass could put one
+  // there, and the inner launch runs while RCCL reads the send buffer).
+  if (pack_.send) {
+    hl->outer_packs = true;
+    for (const auto& c : hl->sched.inner.table) {
+      if (c.r1 <= c.r0) continue;
+      const index_t x0 = index_t(c.group) * shape.owg, x1 = std::min<index_t>(x0 + shape.owg, tile_.width);
+      for (int k = 0; k < pack_.segs.n; ++k) {
+        const kernels::PackSeg& q = pack_.segs.seg[k];
+        if (x0 < q.x0 + q.w && q.x0 < x1 && c.r0 < q.y0 + q.h && q.y0 < c.r1) hl->outer_packs = false;
+      }
+    }
+  }
   hl->inner_table.reset(index_t(hl->sched.inner.table.size()));
   hl->outer_table.reset(index_t(hl->sched.outer.table.size()));
   MXS_HIP_CHECK(hipMemcpy(hl->inner_table.get(), hl->sched.inner.table.data(), hl->inner_table.bytes(),
@@ -915,10 +1002,25 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
     fork_.wait_on(side);
   }
   if (marks) marks->mark("side:start", side);
+  // The inner chunks never take the fused pack: RCCL reads the send buffer
+  // while they run.
   kernels::stencil5_chunk_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->inner_shape, hl->inner_table.get(),
                                   hl->sched.inner.entries, side);
   if (marks) marks->mark("side:inner chunks", side);
   side_pending_ = true;
+  const bool fuse = hl->outer_packs && pack_.send != nullptr;
+  if (!marks && hl->chain_ok) {
+    // The main stream's chain from its graph: one launch instead of the RCCL
+    // group calls and the kernel launches. Captured without the pack launch
+    // when the outer chunks fuse it: the send buffer must hold cur's bands.
+    if (fuse) {
+      if (packed_ == cur) ++last_fused_packs_;
+      ensure_packed(cur, m);
+    }
+    hl->chain[cur == buf_a_ ? 0 : 1].launch(m);
+    packed_ = fuse ? nxt : cur;
+    return;
+  }
   // One-wave copy workgroups sized from the segments (they fit beside the inner
   // launch's workgroups). MXS_HALO_LAST_COPY_WGS (experiments build): 4-wave
   // workgroups, that many per segment; 4 per segment made the exchange so slow
@@ -927,29 +1029,30 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
     const char* e = experiment_env("MXS_HALO_LAST_COPY_WGS");
     return e ? std::atoi(e) : 0;
   }();
-  if (!marks && hl->chain_ok) {
-    // The main stream's chain from its graph: one launch instead of the RCCL
-    // group calls and three kernel launches.
-    hl->chain[cur == buf_a_ ? 0 : 1].launch(m);
-    return;
-  }
   ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
   ex_->set_copy_grid(copy_wgs);
   if (marks) {
     marks->mark("main:start", m);
-    ex_->pack(cur, m);
-    marks->mark("main:pack", m);
+    if (pack_.send && packed_ == cur) {  // the pass before packed cur's bands
+      ++last_fused_packs_;
+    } else {
+      ex_->pack(cur, m);
+      marks->mark("main:pack", m);
+      packed_ = cur;
+    }
     ex_->transfer(m);
     marks->mark("main:rccl", m);
     ex_->unpack(cur, m);
     marks->mark("main:unpack", m);
   } else {
-    ex_->exchange(cur, m);
+    exchange(cur, m);
   }
   ex_->set_copy_grid(0);
   ex_->set_copy_block(0);
+  kernels::PackTarget<T> pk = pack_;
   kernels::stencil5_chunk_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->outer_shape, hl->outer_table.get(),
-                                  hl->sched.outer.entries, m);
+                                  hl->sched.outer.entries, m, fuse ? &pk : nullptr);
+  note_written(nxt, fuse && pk.applied);
   if (marks) marks->mark("main:outer chunks", m);
 }
 
@@ -957,13 +1060,18 @@ template <typename T>
 bool StencilSolver<T>::capture_chain(HaloLastPass* hl) {
   MXS_TRACE_RANGE("stencil.graph_capture_opening");
   hipStream_t m = main_.get();
-  for (int k = 0; k < 2; ++k) {
+  const bool fuse = hl->outer_packs && pack_.send != nullptr;
+  T* const saved = packed_;
+  const int fused_before = last_fused_packs_;
+  bool all = true;
+  for (int k = 0; k < 2 && all; ++k) {
     T* cur = k == 0 ? buf_a_ : buf_b_;
     T* nxt = k == 0 ? buf_b_ : buf_a_;
     hipGraph_t g = nullptr;
     if (hipStreamBeginCapture(m, hipStreamCaptureModeThreadLocal) != hipSuccess) {
       (void)hipGetLastError();
-      return false;
+      all = false;
+      break;
     }
     bool ok = true;
     try {
@@ -971,13 +1079,17 @@ bool StencilSolver<T>::capture_chain(HaloLastPass* hl) {
         const char* e = experiment_env("MXS_HALO_LAST_COPY_WGS");
         return e ? std::atoi(e) : 0;
       }();
+      // With the fused pack the chain starts at the transfer (the launch site
+      // sees to the send buffer), else with the pack launch.
+      packed_ = fuse ? cur : nullptr;
       ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
       ex_->set_copy_grid(copy_wgs);
-      ex_->exchange(cur, m);
+      exchange(cur, m);
       ex_->set_copy_grid(0);
       ex_->set_copy_block(0);
+      kernels::PackTarget<T> pk = pack_;
       kernels::stencil5_chunk_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->outer_shape, hl->outer_table.get(),
-                                      hl->sched.outer.entries, m);
+                                      hl->sched.outer.entries, m, fuse ? &pk : nullptr);
     } catch (const std::exception&) {
       ok = false;
       ex_->set_copy_grid(0);
@@ -987,12 +1099,18 @@ bool StencilSolver<T>::capture_chain(HaloLastPass* hl) {
     if (!ok || end != hipSuccess || g == nullptr) {
       (void)hipGetLastError();
       if (g) (void)hipGraphDestroy(g);
-      return false;
+      all = false;
+      break;
     }
-    if (!hl->chain[k].adopt(g)) return false;
+    if (!hl->chain[k].adopt(g)) {
+      all = false;
+      break;
+    }
     hl->chain[k].upload(m);
   }
-  return true;
+  packed_ = saved;
+  last_fused_packs_ = fused_before;
+  return all;
 }
 
 template <typename T>
@@ -1001,7 +1119,7 @@ void StencilSolver<T>::enqueue_opening(int S, bool advance) {
     enqueue_halo_last(cur_, nxt_, hl);
   } else {  // no chunk-list form on this tile: the same one exchange, then the pass
     join_side();
-    ex_->exchange(cur_, main_.get());
+    exchange(cur_, main_.get());
     enqueue_bare_pass(cur_, nxt_, S);
   }
   if (advance) std::swap(cur_, nxt_);
@@ -1033,7 +1151,7 @@ void StencilSolver<T>::prepare(int iters) {
   for (const Group& g : gr) {
     if (g.count <= 0) continue;
     if (post_exchange() && !ghost_fresh_) {
-      ex_->exchange(cur_, main_.get());
+      exchange(cur_, main_.get());
       ghost_fresh_ = true;
     }
     (void)graphs_for(g.S, g.count);
@@ -1049,6 +1167,9 @@ void StencilSolver<T>::prepare(int iters) {
     warmed_.push_back(g.S);
   }
   join_side();
+  // The warm-up passes wrote the scratch buffer's bands into the send buffer:
+  // back to the field's, as the call before left them (its last pass packed).
+  if (post_exchange()) ensure_packed(cur_, main_.get());
   wait_idle("prepare");
 }
 
@@ -1060,13 +1181,14 @@ void StencilSolver<T>::warm(int iters, int passes) {
   Group gr[2];
   split(iters, gr);
   if (post_exchange() && !ghost_fresh_) {
-    ex_->exchange(cur_, main_.get());
+    exchange(cur_, main_.get());
     ghost_fresh_ = true;
   }
   for (int p = 0; p < passes; ++p)
     for (const Group& g : gr)
       if (g.count > 0) enqueue_block(cur_, nxt_, g.S);  // cur -> nxt, no swap: state unchanged
   join_side();
+  if (post_exchange()) ensure_packed(cur_, main_.get());  // as prepare()
   wait_idle("warm");
 }
 
@@ -1101,8 +1223,13 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
     marks.mark("main:pass", m);
   } else {
     auto exchange = [&](T* tile) {
-      ex_->pack(tile, m);
-      marks.mark("main:pack", m);
+      if (pack_.send && packed_ == tile) {  // the pass before packed it (as in the window)
+        ++last_fused_packs_;
+      } else {
+        ex_->pack(tile, m);
+        marks.mark("main:pack", m);
+        packed_ = tile;
+      }
       ex_->transfer(m);
       marks.mark("main:rccl", m);
       ex_->unpack(tile, m);
@@ -1118,7 +1245,7 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
       out.opening = ghost_fresh_ ? "fresh" : "serial";
       marks.mark("main:start", m);
       if (!ghost_fresh_) exchange(cur_);
-      update(cur_, nxt_, S, 0, w, 0, h, m);
+      core_pass(cur_, nxt_, S, m);
       marks.mark("main:pass", m);
     }
     // The window's first super-step has its own exchange unless it is the
@@ -1131,6 +1258,10 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
   join_side();
   wait_idle("profile_window");
   out.wall_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  if (!fused_ && post_exchange()) {  // the replica packed the scratch buffer's bands (as prepare())
+    ensure_packed(cur_, m);
+    wait_idle("profile_window");
+  }
   // Phases: each marker closes the interval since the previous marker of its stream.
   const Event* first = nullptr;
   for (const auto& e : marks.ev)
@@ -1162,7 +1293,7 @@ void StencilSolver<T>::step() {
 template <typename T>
 void StencilSolver<T>::exchange_only() {
   join_side();
-  ex_->exchange(cur_, main_.get());
+  exchange(cur_, main_.get());
   ghost_fresh_ = true;
 }
 

@@ -96,6 +96,9 @@ class StencilConfig:
     # Interior-first opening: replay the main stream's chain (pack, RCCL,
     # unpack, outer chunks) from a hipGraph captured in prepare().
     opening_graph: bool = False
+    # Fused halo pack: the pipeline passes also write their send bands into the
+    # exchange's send buffer, so the next exchange is RCCL + unpack.
+    fused_pack: bool = True
     # Super-steps estimated longer than this run from eager launches, not a
     # hipGraph (long passes: eager measured faster). 0 = always graphs.
     graph_max_superstep_us: float = 150.0
@@ -198,7 +201,7 @@ class Stencil2D:
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
                                           self._direct_mode(backend),
                                           cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain,
-                                          cfg.halo_max_ctas, cfg.opening_graph)
+                                          cfg.halo_max_ctas, cfg.opening_graph, cfg.fused_pack)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
@@ -387,6 +390,10 @@ class Stencil2D:
         if self.solver.direct_halo():
             how = "HIP IPC direct push of each pass's edge bands into the neighbours' tiles"
         text = f"{what}; {ex} halo exchange{'s' if ex != 1 else ''} by {how}"
+        fp = self.solver.last_run_fused_packs()
+        if fp:
+            text += (f" ({fp} of them with the pack fused into the preceding pass: the pass wrote its send bands "
+                     "into the send buffer)")
         if opening == "interior-first":
             text += ("; opening interior-first (the priming exchange ran under the chunks that read only core "
                      "cells, the ghost-ring chunks after it)")

@@ -16,7 +16,7 @@
 #                          peers' schedule against the fused-periodic tile (no exchange). MODES (default
 #                          "auto fused"; --serial = "auto serial fused"): auto, serial, ifirst (forced
 #                          interior-first), graph (interior-first, its main-stream chain as a hipGraph),
-#                          fused -> OUT/window_TILE.jsonl + medians
+#                          fused; a -nofp suffix adds --no-fused-pack -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
 #   final                  tests + smoke + the driver's bench command + its kernel-trace profile
 set -uo pipefail
@@ -88,7 +88,8 @@ task_window() {
   for i in $(seq "$reps"); do
     for mode in $modes; do
       local args=(--global "$tile" --steps 20 --warmup 5 --no-extras)
-      case $mode in
+      case $mode in *-nofp) args+=(--no-fused-pack) ;; esac
+      case ${mode%-nofp} in
         auto) args+=(--loopback --rehearse-peers) ;;
         serial) args+=(--loopback --rehearse-peers --opening serial) ;;
         ifirst) args+=(--loopback --rehearse-peers --opening interior-first) ;;
@@ -106,6 +107,7 @@ import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1]); e = d["extras"]
 print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["ms_per_step"] * d["steps"], 4),
                   "opening": e.get("opening"), "opening_graph": e.get("opening_graph"),
+                  "fused_packs": e.get("timed_fused_packs"),
                   "phases": e.get("window_phases")}))
 PY
     done
@@ -113,7 +115,7 @@ PY
   python - "$log" <<'PY'
 import json, sys
 rs = [json.loads(l) for l in open(sys.argv[1])]
-for m in ("auto", "serial", "ifirst", "graph", "fused"):
+for m in sorted({r["mode"] for r in rs}):
     v = sorted(r["window_ms"] for r in rs if r["mode"] == m)
     if v:
         print(m, "n", len(v), "median", v[len(v) // 2], "min", v[0], "max", v[-1])

@@ -376,3 +376,70 @@ def test_opening_graph_bitwise_both_orientations(gpu, runs):
     a.synchronize()
     b.synchronize()
     assert torch.equal(a.core_view(), b.core_view())
+
+
+@pytest.mark.parametrize("w,h,dtype,S,opening,runs", [
+    (16384, 8192, "f32", 20, "interior-first", (20, 20, 40)),   # the 8-GPU tile, the driver's window
+    (16384, 8192, "f32", 20, "serial", (20, 60)),
+    (4096, 2048, "f32", 24, "interior-first", (48, 24)),
+    (4000, 1536, "f32", 24, "serial", (24, 72)),                 # ragged last column group
+    (4096, 2048, "f64", 16, "interior-first", (32, 16)),         # fp64 wide lanes (8-byte cells, 2 per vector)
+    (4096, 2048, "f32", 12, "serial", (24,)),                    # S = 12: no pipeline form, the pack launch stays
+])
+def test_fused_pack_bitwise_vs_pack_launch(gpu, w, h, dtype, S, opening, runs):
+    """Fused halo pack: the pipeline passes write their send bands into the
+    exchange's send buffer, so each exchange after such a pass is RCCL +
+    unpack. Against the same schedule with the pack launch (fused_pack=False):
+    the field is bitwise equal after every call, and every exchange of the peers'
+    schedule whose preceding pass takes a pipeline form skips its pack launch."""
+    kw = dict(seed=w + h + 7, opening=opening, rehearse_peers=True, time_block=S)
+    a = _loopback(w, h, dtype, fused_pack=True, **kw)
+    b = _loopback(w, h, dtype, fused_pack=False, **kw)
+    pipeline = S > 16 or dtype == "f64"  # the passes take a pipeline form (which writes the bands)
+    assert a.solver.fused_pack() and not b.solver.fused_pack()
+    for i, n in enumerate(runs):
+        a.run(n)
+        b.run(n)
+        ex = a.solver.last_run_exchanges()
+        assert ex == b.solver.last_run_exchanges() == n // S
+        fp = a.solver.last_run_fused_packs()
+        if pipeline:
+            # The first call's priming exchange follows the initial data (packed by a launch).
+            assert fp == (ex - 1 if i == 0 else ex), (i, n, fp, ex)
+            if i > 0:
+                assert "pack fused" in a.halo_mode()
+        else:
+            assert fp == 0
+        assert b.solver.last_run_fused_packs() == 0
+        a.synchronize()
+        b.synchronize()
+        assert torch.equal(a.core_view(), b.core_view()), (i, n)
+
+
+def test_fused_pack_after_field_change_and_prepare(gpu):
+    """The send buffer's state follows the field: a caller's write
+    (field_changed) forces the pack launch again, prepare() / warm() leave the
+    field's bands packed (their warm-up passes write the scratch buffer), and
+    the result stays bitwise that of the pack-launch schedule."""
+    kw = dict(seed=91, opening="interior-first", rehearse_peers=True, time_block=20)
+    a = _loopback(16384, 8192, fused_pack=True, **kw)
+    b = _loopback(16384, 8192, fused_pack=False, **kw)
+    for st in (a, b):
+        st.run(20)
+        st.prepare(20)
+        st.warm(20, 0.01)
+    a.run(20)
+    assert a.solver.last_run_fused_packs() == 1
+    for st in (a, b):
+        st.synchronize()
+        st.core_view().mul_(0.5)
+        torch.cuda.synchronize()
+        st.field_changed()
+        st.run(20)
+    assert a.solver.last_run_fused_packs() == 0  # the caller's write: packed by a launch again
+    a.run(40)
+    b.run(40)
+    assert a.solver.last_run_fused_packs() == 2
+    a.synchronize()
+    b.synchronize()
+    assert torch.equal(a.core_view(), b.core_view())
