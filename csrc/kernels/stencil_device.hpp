@@ -1405,7 +1405,8 @@ struct PipeShares {
 // workgroup stored and that lie in a send window are copied from the tile into
 // the packed send buffer, 16 bytes per lane. The caller's __syncthreads() makes
 // the stage-1 waves' stores visible to every wave of the workgroup (one CU, one
-// L1). Window columns and the rectangle's columns are whole 16-byte vectors
+// L1; each wave first waits for its own stores to be acknowledged). Window
+// columns and the rectangle's columns are whole 16-byte vectors
 // (host-checked), so a vector is inside a window or outside it.
 template <typename T>
 __device__ __forceinline__ void pack_rect(const T* __restrict__ core, index_t pitch, T* __restrict__ send,
@@ -1481,6 +1482,7 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
   }
   if constexpr (!WRAP) {
     if (pack.n > 0) {  // fused halo pack of the cells this workgroup stored (kernel-uniform)
+      __builtin_amdgcn_s_waitcnt(0);  // this wave's tile stores acknowledged (vmcnt counts stores on gfx9)
       __syncthreads();
       constexpr index_t GW = JOINT ? index_t(OWG) : index_t(G) * OW;  // output columns per group
 #pragma unroll 1
@@ -1525,6 +1527,7 @@ __global__ __launch_bounds__(2 * kWavesPerBlock * kWaveSize) void stencil5_pipe_
                                                    x_end, y_begin + c.r0, y_begin + c.r1, c0, c1, ring, stage, strip);
   }
   if (pack.n > 0) {  // fused halo pack (see stencil5_stream_pipe_kernel)
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
 #pragma unroll 1
     for (int e = 0; e < entries; ++e) {

@@ -45,7 +45,8 @@ def run(args) -> int:
         t0 = time.monotonic_ns()
         st.run(20)
         t_run = time.monotonic_ns()
-        st.synchronize()
+        if not args.torch_sync_only:
+            st.synchronize()
         t_sync = time.monotonic_ns()
         torch.cuda.synchronize()
         t1 = time.monotonic_ns()
@@ -123,6 +124,8 @@ def main() -> int:
     p.add_argument("--opening", default="auto")
     p.add_argument("--fused", action="store_true")
     p.add_argument("--graph", action="store_true", help="the opening's main-stream chain from a hipGraph")
+    p.add_argument("--torch-sync-only", action="store_true",
+                   help="end the window with torch.cuda.synchronize() alone (no solver.synchronize() poll)")
     p.add_argument("--replica", action="store_true", help="run mode: also an event-timed replica per window")
     p.add_argument("--host", help="analysis without a trace: the stamps + replicas of a --replica run")
     p.add_argument("--db")
