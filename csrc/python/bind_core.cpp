@@ -155,6 +155,16 @@ PYBIND11_MODULE(_mxs_core, m) {
       .def_readonly("recv_elems", &HaloPlan::recv_elems);
   m.def("make_halo_plan", &make_halo_plan, py::arg("topo"), py::arg("rank"), py::arg("tile"),
         py::arg("corners") = true, py::arg("loopback_self") = false);
+  m.def(
+      "send_windows",
+      [](const HaloPlan& p) {
+        py::list out;
+        for (const auto& w : send_windows(p)) out.append(py::make_tuple(w.x0, w.y0, w.w, w.h, w.off));
+        return out;
+      },
+      py::arg("plan"),
+      "the plan's send windows (x0, y0, w, h, offset) in core coordinates, for the fused pack; [] when the plan "
+      "has self copies or no remote peer");
 
   m.def(
       "paired_decision",

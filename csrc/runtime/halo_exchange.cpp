@@ -140,21 +140,11 @@ void HaloExchanger<T>::exchange_packed(T* tile, hipStream_t stream) {
 
 template <typename T>
 bool HaloExchanger<T>::pack_windows(const TileGeom& g, kernels::PackSegs* out) const {
-  if (plan_.sends.empty() || !plan_.self_copies.empty()) return false;
+  if (!(g == plan_.tile)) return false;
+  const std::vector<SendWindow> ws = send_windows(plan_);
+  if (ws.empty() || ws.size() > size_t(kernels::kMaxPackSegs)) return false;
   kernels::PackSegs p;
-  const Array2D core = g.core();
-  for (const auto& m : plan_.sends)
-    for (const auto& seg : m.segments) {
-      if (seg.region.empty()) continue;
-      if (p.n == kernels::kMaxPackSegs || seg.region.row_stride != g.pitch) return false;
-      kernels::PackSeg& q = p.seg[p.n++];
-      q.x0 = seg.region.x_offset - core.x_offset;
-      q.y0 = seg.region.y_offset - core.y_offset;
-      q.w = seg.region.width;
-      q.h = seg.region.height;
-      q.off = seg.offset;
-    }
-  if (p.n == 0) return false;
+  for (const auto& w : ws) p.seg[p.n++] = kernels::PackSeg{w.x0, w.y0, w.w, w.h, w.off};
   *out = p;
   return true;
 }
