@@ -107,7 +107,8 @@ def _sync():
         torch.cuda.synchronize()
 
 
-def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0) -> float:
+def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync: str = "solver",
+              comm_timeout: float = 300.0) -> float:
     """K steps bracketed by barrier + device synchronisation on both sides; the
     max over ranks. Each rank's clock stops when its own device work is done,
     before the closing barrier: a 20-step window at N = 8 is one ~0.3 ms pass,
@@ -121,11 +122,24 @@ def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0) -> float:
     _sync()
     ctx.barrier()
     _sync()
-    t0 = time.perf_counter()
-    st.run(steps)
-    st.synchronize()  # polls under the communication watchdog when a peer can hang
-    _sync()
-    t1 = time.perf_counter()
+    if window_sync == "torch":
+        # The window ends at torch.cuda.synchronize() alone (it waits for every
+        # stream of the device, the solver's included); a timer thread armed
+        # before t0 aborts the halo's RCCL communicators if the wait outlives
+        # the deadline (parallel/watchdog.py), and the solver's own check of
+        # its streams and RCCL's async errors follows outside the window.
+        with st.watchdog(comm_timeout, "timed window"):
+            t0 = time.perf_counter()
+            st.run(steps)
+            _sync()
+            t1 = time.perf_counter()
+        st.synchronize()
+    else:
+        t0 = time.perf_counter()
+        st.run(steps)
+        st.synchronize()  # polls under the communication watchdog when a peer can hang
+        _sync()
+        t1 = time.perf_counter()
     ctx.barrier()
     return ctx.allreduce_max(t1 - t0)
 
@@ -337,6 +351,10 @@ def main(argv=None) -> int:
     p.add_argument("--opening-graph", action="store_true",
                    help="N > 1: replay the interior-first opening's main-stream chain (pack, RCCL, unpack, outer "
                         "chunks) from a hipGraph captured in prepare()")
+    p.add_argument("--window-sync", default="solver", choices=["solver", "torch"],
+                   help="how the timed window ends: solver = solver.synchronize() (stream polls under the RCCL "
+                        "watchdog) then torch.cuda.synchronize(); torch = torch.cuda.synchronize() alone under a "
+                        "timer-thread watchdog that aborts the communicators past --comm-timeout")
     p.add_argument("--no-fused-pack", action="store_true",
                    help="N > 1: pack the halo with its own launch before each exchange instead of in the pass")
     p.add_argument("--direct-halo", default="off", choices=["off", "validate"],
@@ -401,7 +419,8 @@ def main(argv=None) -> int:
                         fused_pack=not args.no_fused_pack,
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
-    dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3)
+    dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3, args.window_sync,
+                   args.comm_timeout)
     timed_blocks = st.last_run_blocks()  # the super-steps the timed window executed
     value = st.cells_per_step * args.steps / dt / 1e9
     halo = st.halo_mode()  # what the timed run() executed
@@ -419,6 +438,7 @@ def main(argv=None) -> int:
                                    "c_neighbor = 0.2; range-guarded: 5|c| <= 1, max|u| 5^S < FLT_MAX/4)"
                                    if sum_used else "per step: fma(c_n, (n+s)+(w+e), c_c*c)"),
                     "clock_warmup_ms": args.clock_warmup_ms,
+                    "window_sync": args.window_sync,
                     "tile": f"{st.decomp.width}x{st.decomp.height}",
                     "process_grid": f"{rows} rows x {cols} cols of ranks",
                     "env": env}

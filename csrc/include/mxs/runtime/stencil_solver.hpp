@@ -310,6 +310,11 @@ class StencilSolver {
     return "not used yet";
   }
   const std::string& halo_comm_note() const { return halo_comm_note_; }
+  // Abort the halo's own communicator (SolverConfig::halo_max_ctas), from any
+  // thread: a watchdog's way to unblock a device wait on a hung peer's exchange.
+  void abort_halo_comm() const {
+    if (halo_comm_) halo_comm_->abort();
+  }
   // SolverConfig::fused_pack in effect (the plan's windows can take it).
   bool fused_pack() const { return pack_.send != nullptr; }
   // Exchanges of the last run() whose pack was fused into the preceding pass.

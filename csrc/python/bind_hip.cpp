@@ -341,7 +341,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
              const bool ok = c.healthy(&msg);
              return py::make_tuple(ok, msg);
            })
-      .def("abort", &RcclComm::abort)
+      .def("abort", &RcclComm::abort, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("aborted", &RcclComm::aborted)
       .def(
           "wait",
@@ -500,6 +500,9 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def("halo_max_ctas", [](SolverHandle& h) { return h.visit([](auto& s) { return s.halo_max_ctas(); }); },
            "CTA cap of the halo's RCCL communicator (0: RCCL's default)")
       .def("halo_comm_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.halo_comm_note(); }); })
+      .def("abort_halo_comm", [](SolverHandle& h) { h.visit([](auto& s) { s.abort_halo_comm(); }); },
+           py::call_guard<py::gil_scoped_release>(),
+           "abort the halo's own RCCL communicator (halo_max_ctas), e.g. from a watchdog thread")
       .def("fused_pack", [](SolverHandle& h) { return h.visit([](auto& s) { return s.fused_pack(); }); },
            "whether the passes write the send bands into the exchange's send buffer (SolverConfig::fused_pack)")
       .def("last_run_fused_packs",

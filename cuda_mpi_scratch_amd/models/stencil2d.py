@@ -294,6 +294,17 @@ class Stencil2D:
         elif self.device.type == "cuda":
             torch.cuda.synchronize()
 
+    def watchdog(self, timeout_s: float, what: str = "stencil halo exchange (RCCL)"):
+        """A deadline for a blocking wait outside the solver (``torch.cuda.synchronize()``
+        on the solver's work): past it the RCCL communicators the halo uses are
+        aborted and leaving the block raises (parallel/watchdog.py)."""
+        from ..parallel.watchdog import CommWatchdog
+
+        aborts = []
+        if self.solver is not None and self.comm is not None:
+            aborts = [self.solver.abort_halo_comm, self.comm.abort]
+        return CommWatchdog(timeout_s, aborts, what)
+
     # ---------------------------------------------------------------- state
     def current(self) -> torch.Tensor:
         """The tensor holding the current field. The caller may write it, so the

@@ -45,11 +45,35 @@ def test_bench_8gpu_tile_window_through_loopback(gpu):
     assert ex["rccl_ranks"] == 1 and len(ex["rank_devices"]) == 1
     ph = ex["window_phases"]
     assert ph["opening"] == ex["opening"] and ph["exchanges"] == 1
-    assert {"main:pack", "main:rccl", "main:unpack"} <= set(ph["phases_us"])
+    assert {"main:rccl", "main:unpack"} <= set(ph["phases_us"])
+    # Fused pack: the warm-up's last pass packed the field's bands, so the window's
+    # priming exchange (and the replica's) starts at RCCL.
+    assert ex["fused_pack"] is True and ex["timed_fused_packs"] == 1
+    assert "main:pack" not in ph["phases_us"]
+    assert "pack fused" in ex["halo"]
     assert ph["gpu_span_us"] > 0 and ph["wall_us"] > 0
     assert isinstance(ex["env"], dict) and ex["experiments_build"] is False
     # 16384 x 8192 x 20 cell-updates: one pass (~0.25 ms) + one loopback exchange.
     assert d["value"] > 5000, d
+
+
+@pytest.mark.parametrize("extra", [["--window-sync", "torch"], ["--no-fused-pack"]])
+def test_bench_window_options_through_loopback(gpu, extra):
+    """--window-sync torch (the window ends at torch.cuda.synchronize() alone,
+    under the timer-thread watchdog) and --no-fused-pack (the pack launch before
+    every exchange) run and say so in the record."""
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--global", "16384x8192", "--loopback",
+                        "--rehearse-peers", "--steps", "20", "--warmup", "5", "--no-extras", "--clock-warmup-ms", "20",
+                        *extra], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    ex = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["extras"]
+    assert ex["timed_exchanges"] == 1
+    if extra[0] == "--window-sync":
+        assert ex["window_sync"] == "torch" and ex["timed_fused_packs"] == 1
+    else:
+        assert ex["fused_pack"] is False and ex["timed_fused_packs"] == 0
+        assert "main:pack" in ex["window_phases"]["phases_us"]
 
 
 def test_bench_pingpong_and_dot_record_keys_through_loopback(gpu):
