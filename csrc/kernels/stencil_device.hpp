@@ -1412,6 +1412,7 @@ template <typename T>
 __device__ __forceinline__ void pack_rect(const T* __restrict__ core, index_t pitch, T* __restrict__ send,
                                           const PackSegs& pk, index_t x0, index_t x1, index_t y0, index_t y1) {
   constexpr int N = 16 / sizeof(T);
+  constexpr int K = 8;  // vectors in flight per lane: one memory round trip per K, not per vector
   using V = T __attribute__((ext_vector_type(N)));
 #pragma unroll 1
   for (int k = 0; k < pk.n; ++k) {  // workgroup-uniform
@@ -1422,11 +1423,21 @@ __device__ __forceinline__ void pack_rect(const T* __restrict__ core, index_t pi
     const int vw = int((bx - ax) / N), total = vw * int(by - ay);
     const T* __restrict__ src = core + ay * pitch + ax;
     T* __restrict__ dst = send + sg.off + (ay - sg.y0) * sg.w + (ax - sg.x0);
-#pragma unroll 4
-    for (int t = int(threadIdx.x); t < total; t += int(blockDim.x)) {
-      const int ry = t / vw, rx = t - ry * vw;
-      *reinterpret_cast<V*>(dst + index_t(ry) * sg.w + rx * N) =
-          *reinterpret_cast<const V*>(src + index_t(ry) * pitch + rx * N);
+    const int step = int(blockDim.x);
+#pragma unroll 1
+    for (int t0 = int(threadIdx.x); t0 < total; t0 += K * step) {
+      V v[K];
+      index_t o[K];
+#pragma unroll
+      for (int j = 0; j < K; ++j) {
+        const int t = t0 + j * step;
+        const int ry = t / vw, rx = t - ry * vw;
+        o[j] = index_t(ry) * sg.w + rx * N;
+        if (t < total) v[j] = *reinterpret_cast<const V*>(src + index_t(ry) * pitch + rx * N);
+      }
+#pragma unroll
+      for (int j = 0; j < K; ++j)
+        if (t0 + j * step < total) *reinterpret_cast<V*>(dst + o[j]) = v[j];
     }
   }
 }

@@ -271,6 +271,32 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("dtype") = "f32", py::arg("stream") = 0, py::arg("variant") = "auto", py::arg("sum_form") = true,
       "S Jacobi steps over [x0, x1) x [y0, y1); sum_form: allow the sum form when c_center == c_neighbor");
   m.def(
+      "stencil5_tb_packed",
+      [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, double c0, double c1, std::uintptr_t send,
+         const std::vector<std::tuple<index_t, index_t, index_t, index_t, index_t>>& windows, const std::string& dt,
+         std::uintptr_t s) {
+        kernels::PackSegs segs;
+        MXS_CHECK(windows.size() <= size_t(kernels::kMaxPackSegs), "at most " << kernels::kMaxPackSegs << " windows");
+        for (const auto& w : windows)
+          segs.seg[segs.n++] = kernels::PackSeg{std::get<0>(w), std::get<1>(w), std::get<2>(w), std::get<3>(w),
+                                                std::get<4>(w)};
+        kernels::Stencil5Coeffs c{c0, c1, true};
+        if (parse_dtype(dt) == DType::F32) {
+          kernels::PackTarget<float> pk{ptr<float>(send), segs, false};
+          kernels::stencil5_tb<float>(ptr<float>(in), ptr<float>(out), g, steps, 0, g.width, 0, g.height, c, false,
+                                      strm(s), kernels::StencilVariant::Auto, &pk);
+          return pk.applied;
+        }
+        kernels::PackTarget<double> pk{ptr<double>(send), segs, false};
+        kernels::stencil5_tb<double>(ptr<double>(in), ptr<double>(out), g, steps, 0, g.width, 0, g.height, c, false,
+                                     strm(s), kernels::StencilVariant::Auto, &pk);
+        return pk.applied;
+      },
+      py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("steps"), py::arg("c_center"), py::arg("c_neighbor"),
+      py::arg("send"), py::arg("windows"), py::arg("dtype") = "f32", py::arg("stream") = 0,
+      "the whole-core S-step pass with the fused halo pack into `send` (windows: send_windows(plan)); returns "
+      "whether the pass took it (a pipeline form)");
+  m.def(
       "stencil5_rect",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
          double c0, double c1, const std::string& dt, std::uintptr_t s) {

@@ -449,3 +449,29 @@ def test_fused_pack_after_field_change_and_prepare(gpu):
     a.synchronize()
     b.synchronize()
     assert torch.equal(a.core_view(), b.core_view())
+
+
+@pytest.mark.parametrize("w,h,dtype,S", [(16384, 8192, "f32", 20), (4000, 1536, "f32", 24), (4096, 2048, "f64", 16)])
+def test_pack_epilogue_writes_exactly_the_send_windows(gpu, w, h, dtype, S):
+    """The pipeline pass with the fused pack: its core output is bitwise the plain
+    pass's, and the send buffer holds, window by window, exactly the output's
+    cells (the plan's packed layout), every element written."""
+    st = _loopback(w, h, dtype, seed=93, time_block=S)
+    st.run(S)
+    st.synchronize()
+    H, C = hip(), core()
+    g = st.geom
+    plan = C.make_halo_plan(st.decomp.topo, 0, g, True, True)
+    wins = C.send_windows(plan)
+    assert len(wins) == 8
+    a = st.current()
+    out1, out2 = torch.zeros_like(a), torch.zeros_like(a)
+    send = torch.full((plan.send_elems,), float("nan"), dtype=a.dtype, device=a.device)
+    H.stencil5_tb(a.data_ptr(), out1.data_ptr(), g, S, 0, w, 0, h, 0.2, 0.2, False, dtype=dtype)
+    assert H.stencil5_tb_packed(a.data_ptr(), out2.data_ptr(), g, S, 0.2, 0.2, send.data_ptr(), wins, dtype=dtype)
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2)
+    core2 = out2.view(g.total_height(), g.pitch)[g.halo_y:g.halo_y + h, g.x_origin + g.halo_x:g.x_origin + g.halo_x + w]
+    assert not torch.isnan(send).any()
+    for x0, y0, ww, hh, off in wins:
+        assert torch.equal(send[off:off + ww * hh].view(hh, ww), core2[y0:y0 + hh, x0:x0 + ww]), (x0, y0, ww, hh)
