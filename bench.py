@@ -107,7 +107,7 @@ def _sync():
         torch.cuda.synchronize()
 
 
-def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync: str = "solver",
+def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync: str = "torch",
               comm_timeout: float = 300.0) -> float:
     """K steps bracketed by barrier + device synchronisation on both sides; the
     max over ranks. Each rank's clock stops when its own device work is done,
@@ -351,10 +351,12 @@ def main(argv=None) -> int:
     p.add_argument("--opening-graph", action="store_true",
                    help="N > 1: replay the interior-first opening's main-stream chain (pack, RCCL, unpack, outer "
                         "chunks) from a hipGraph captured in prepare()")
-    p.add_argument("--window-sync", default="solver", choices=["solver", "torch"],
-                   help="how the timed window ends: solver = solver.synchronize() (stream polls under the RCCL "
-                        "watchdog) then torch.cuda.synchronize(); torch = torch.cuda.synchronize() alone under a "
-                        "timer-thread watchdog that aborts the communicators past --comm-timeout")
+    p.add_argument("--window-sync", default="torch", choices=["solver", "torch"],
+                   help="how the timed window ends: torch (default) = torch.cuda.synchronize() alone, under a "
+                        "timer-thread watchdog that aborts the halo's RCCL communicators past --comm-timeout "
+                        "(the solver's own checks follow outside the window); solver = solver.synchronize() "
+                        "(stream polls under the RCCL watchdog) then torch.cuda.synchronize(), ~8-10 us more per "
+                        "window (profiles/r04_sync)")
     p.add_argument("--no-fused-pack", action="store_true",
                    help="N > 1: pack the halo with its own launch before each exchange instead of in the pass")
     p.add_argument("--direct-halo", default="off", choices=["off", "validate"],

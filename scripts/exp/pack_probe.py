@@ -76,10 +76,12 @@ def main() -> int:
     spans = {k: [] for k in sts}
     for _ in range(reps):
         for k, x in sts.items():
-            spans[k].append(x.profile_window(20)["gpu_span_us"])
+            spans[k].append(x.profile_window(20))
     for (opening, fp), v in spans.items():
-        print(json.dumps({"opening": opening, "fused_pack": fp, "gpu_span_us_median": med(v),
-                          "min": round(min(v), 1), "max": round(max(v), 1)}), flush=True)
+        v = sorted(v, key=lambda p: p["gpu_span_us"])
+        print(json.dumps({"opening": opening, "fused_pack": fp, "gpu_span_us": [round(p["gpu_span_us"]) for p in v],
+                          "median_phases": v[len(v) // 2]["phases_us"], "slowest_phases": v[-1]["phases_us"]}),
+              flush=True)
     return 0
 
 

@@ -57,11 +57,12 @@ def test_bench_8gpu_tile_window_through_loopback(gpu):
     assert d["value"] > 5000, d
 
 
-@pytest.mark.parametrize("extra", [["--window-sync", "torch"], ["--no-fused-pack"]])
+@pytest.mark.parametrize("extra", [["--window-sync", "solver"], ["--no-fused-pack"]])
 def test_bench_window_options_through_loopback(gpu, extra):
-    """--window-sync torch (the window ends at torch.cuda.synchronize() alone,
-    under the timer-thread watchdog) and --no-fused-pack (the pack launch before
-    every exchange) run and say so in the record."""
+    """--window-sync solver (the window ends at solver.synchronize()'s polled
+    wait, then torch.cuda.synchronize(); the default is torch.cuda.synchronize()
+    alone under the timer-thread watchdog) and --no-fused-pack (the pack launch
+    before every exchange) run and say so in the record."""
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--global", "16384x8192", "--loopback",
                         "--rehearse-peers", "--steps", "20", "--warmup", "5", "--no-extras", "--clock-warmup-ms", "20",
@@ -70,7 +71,7 @@ def test_bench_window_options_through_loopback(gpu, extra):
     ex = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["extras"]
     assert ex["timed_exchanges"] == 1
     if extra[0] == "--window-sync":
-        assert ex["window_sync"] == "torch" and ex["timed_fused_packs"] == 1
+        assert ex["window_sync"] == "solver" and ex["timed_fused_packs"] == 1
     else:
         assert ex["fused_pack"] is False and ex["timed_fused_packs"] == 0
         assert "main:pack" in ex["window_phases"]["phases_us"]
