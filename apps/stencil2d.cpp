@@ -26,7 +26,8 @@
 // serial and interior-first openings, agrees the worst-rank medians over all ranks and keeps the faster),
 // --no-direct-halo (IPC backend: pack -> put -> unpack instead of the device-initiated push),
 // --halo-max-ctas N (RCCL: the halo exchange on a communicator split off with at most N workgroups per kernel),
-// --no-fused-pack (pack the halo with its own launch before each exchange instead of in the preceding pass),
+// --fused-pack (the pipeline passes write their send bands into the send buffer: no pack launch before the
+// exchange after them; off by default, measured slower),
 // --opening-graph (the interior-first opening's pack/RCCL/unpack/outer chain replayed from a hipGraph),
 // --direct-halo on|off|validate (validate: prepare() compares the push with the backend's exchange bitwise on
 // every rank, times both, and uses it only if equal everywhere and faster),
@@ -144,7 +145,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
             "--opening must be auto, serial or interior-first, got " << opening);
   cfg.opening = opening == "serial" ? Opening::Serial : opening == "interior-first" ? Opening::InteriorFirst : Opening::Auto;
   cfg.halo_max_ctas = int(cli.get_int("halo-max-ctas", 0));  // RCCL: the halo on a CTA-capped communicator
-  cfg.fused_pack = !cli.flag("no-fused-pack");  // the pipeline passes write the send bands (exchange = wire + unpack)
+  cfg.fused_pack = cli.flag("fused-pack");  // the pipeline passes write the send bands (exchange = wire + unpack)
   cfg.opening_graph = cli.flag("opening-graph");
   cfg.loopback_self = loopback;
   cfg.coeffs = {c_center, c_neighbor, sum_form};

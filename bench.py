@@ -357,8 +357,10 @@ def main(argv=None) -> int:
                         "(the solver's own checks follow outside the window); solver = solver.synchronize() "
                         "(stream polls under the RCCL watchdog) then torch.cuda.synchronize(), ~8-10 us more per "
                         "window (profiles/r04_sync)")
-    p.add_argument("--no-fused-pack", action="store_true",
-                   help="N > 1: pack the halo with its own launch before each exchange instead of in the pass")
+    p.add_argument("--fused-pack", action="store_true",
+                   help="N > 1: the pipeline passes write their send bands into the exchange's send buffer, so "
+                        "the exchange after them has no pack launch (default off: measured slower on the 8-GPU-tile "
+                        "window, profiles/r04_fp)")
     p.add_argument("--direct-halo", default="off", choices=["off", "validate"],
                    help="N > 1: validate: prepare() compares the device-initiated push of the edge bands into the "
                         "neighbours' tiles (HIP IPC over xGMI) bitwise with the RCCL exchange on every rank and times "
@@ -418,7 +420,7 @@ def main(argv=None) -> int:
                         sum_form=not args.no_sum_form, opening=args.opening, rehearse_peers=args.rehearse_peers,
                         direct_halo=("validate" if args.direct_halo == "validate" else None),
                         halo_max_ctas=args.halo_max_ctas, opening_graph=args.opening_graph,
-                        fused_pack=not args.no_fused_pack,
+                        fused_pack=args.fused_pack,
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3, args.window_sync,

@@ -178,7 +178,11 @@ struct SolverConfig {
   // buffer, so the next exchange is RCCL + unpack (no pack launch). Applies
   // where the plan has remote peers and the pass takes a pipeline form (fp32
   // S > 16, fp64 S 9..16 on whole vectors); other passes keep the pack launch.
-  bool fused_pack = true;
+  // Off by default: measured on the 8-GPU-tile window, the pack launch is what
+  // keeps the GPU busy while the host enqueues the RCCL group, and its fused
+  // form costs the pass 6-7 us (profiles/r04_fp: serial 0.324 vs 0.314 ms,
+  // interior-first 0.308 vs 0.298 with / without).
+  bool fused_pack = false;
   // RCCL backend: run the halo exchange on a communicator split off `comm`
   // with at most this many workgroups per RCCL kernel (0 = RCCL's default).
   int halo_max_ctas = 0;

@@ -481,7 +481,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
            py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = "off",
            py::arg("graph_max_superstep_us") = 150.0, py::arg("opening") = "auto", py::arg("rehearse_peers") = false,
-           py::arg("min_gain") = 0.03, py::arg("halo_max_ctas") = 0, py::arg("opening_graph") = false, py::arg("fused_pack") = true,
+           py::arg("min_gain") = 0.03, py::arg("halo_max_ctas") = 0, py::arg("opening_graph") = false, py::arg("fused_pack") = false,
            py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")

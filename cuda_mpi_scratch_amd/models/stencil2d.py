@@ -97,8 +97,9 @@ class StencilConfig:
     # unpack, outer chunks) from a hipGraph captured in prepare().
     opening_graph: bool = False
     # Fused halo pack: the pipeline passes also write their send bands into the
-    # exchange's send buffer, so the next exchange is RCCL + unpack.
-    fused_pack: bool = True
+    # exchange's send buffer, so the next exchange is RCCL + unpack. Off by
+    # default (measured slower: the pack launch hides the host's RCCL enqueue).
+    fused_pack: bool = False
     # Super-steps estimated longer than this run from eager launches, not a
     # hipGraph (long passes: eager measured faster). 0 = always graphs.
     graph_max_superstep_us: float = 150.0

@@ -16,8 +16,8 @@
 #                          peers' schedule against the fused-periodic tile (no exchange). MODES (default
 #                          "auto fused"; --serial = "auto serial fused"): auto, serial, ifirst (forced
 #                          interior-first), graph (interior-first, its main-stream chain as a hipGraph),
-#                          fused; suffixes: -nofp adds --no-fused-pack, -ssync --window-sync solver (in that
-#                          order, e.g. ifirst-nofp-ssync) -> OUT/window_TILE.jsonl + medians
+#                          fused; suffixes: -fp adds --fused-pack, -ssync --window-sync solver (in that
+#                          order, e.g. ifirst-fp-ssync) -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
 #   final                  tests + smoke + the driver's bench command + its kernel-trace profile
 set -uo pipefail
@@ -91,7 +91,7 @@ task_window() {
       local args=(--global "$tile" --steps 20 --warmup 5 --no-extras)
       local base=$mode
       case $base in *-ssync) args+=(--window-sync solver); base=${base%-ssync} ;; esac
-      case $base in *-nofp) args+=(--no-fused-pack); base=${base%-nofp} ;; esac
+      case $base in *-fp) args+=(--fused-pack); base=${base%-fp} ;; esac
       case $base in
         auto) args+=(--loopback --rehearse-peers) ;;
         serial) args+=(--loopback --rehearse-peers --opening serial) ;;

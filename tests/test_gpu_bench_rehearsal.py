@@ -45,24 +45,21 @@ def test_bench_8gpu_tile_window_through_loopback(gpu):
     assert ex["rccl_ranks"] == 1 and len(ex["rank_devices"]) == 1
     ph = ex["window_phases"]
     assert ph["opening"] == ex["opening"] and ph["exchanges"] == 1
-    assert {"main:rccl", "main:unpack"} <= set(ph["phases_us"])
-    # Fused pack: the warm-up's last pass packed the field's bands, so the window's
-    # priming exchange (and the replica's) starts at RCCL.
-    assert ex["fused_pack"] is True and ex["timed_fused_packs"] == 1
-    assert "main:pack" not in ph["phases_us"]
-    assert "pack fused" in ex["halo"]
+    assert {"main:pack", "main:rccl", "main:unpack"} <= set(ph["phases_us"])
+    assert ex["fused_pack"] is False and ex["timed_fused_packs"] == 0  # default: the pack launch
     assert ph["gpu_span_us"] > 0 and ph["wall_us"] > 0
     assert isinstance(ex["env"], dict) and ex["experiments_build"] is False
     # 16384 x 8192 x 20 cell-updates: one pass (~0.25 ms) + one loopback exchange.
     assert d["value"] > 5000, d
 
 
-@pytest.mark.parametrize("extra", [["--window-sync", "solver"], ["--no-fused-pack"]])
+@pytest.mark.parametrize("extra", [["--window-sync", "solver"], ["--fused-pack"]])
 def test_bench_window_options_through_loopback(gpu, extra):
     """--window-sync solver (the window ends at solver.synchronize()'s polled
     wait, then torch.cuda.synchronize(); the default is torch.cuda.synchronize()
-    alone under the timer-thread watchdog) and --no-fused-pack (the pack launch
-    before every exchange) run and say so in the record."""
+    alone under the timer-thread watchdog) and --fused-pack (the passes write
+    their send bands: the window's priming exchange has no pack launch) run and
+    say so in the record."""
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--global", "16384x8192", "--loopback",
                         "--rehearse-peers", "--steps", "20", "--warmup", "5", "--no-extras", "--clock-warmup-ms", "20",
@@ -71,10 +68,11 @@ def test_bench_window_options_through_loopback(gpu, extra):
     ex = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["extras"]
     assert ex["timed_exchanges"] == 1
     if extra[0] == "--window-sync":
-        assert ex["window_sync"] == "solver" and ex["timed_fused_packs"] == 1
+        assert ex["window_sync"] == "solver" and ex["timed_fused_packs"] == 0
     else:
-        assert ex["fused_pack"] is False and ex["timed_fused_packs"] == 0
-        assert "main:pack" in ex["window_phases"]["phases_us"]
+        assert ex["fused_pack"] is True and ex["timed_fused_packs"] == 1
+        assert "main:pack" not in ex["window_phases"]["phases_us"]
+        assert "pack fused" in ex["halo"]
 
 
 def test_bench_pingpong_and_dot_record_keys_through_loopback(gpu):
