@@ -8,6 +8,8 @@
 // Python launcher. Bootstrap is therefore a plain byte string.
 #pragma once
 
+#include <atomic>
+
 #include <rccl/rccl.h>
 
 #include <memory>
@@ -53,8 +55,8 @@ class RcclComm {
   RcclComm(const RcclComm&) = delete;
   RcclComm& operator=(const RcclComm&) = delete;
 
-  ncclComm_t get() const { return comm_; }
-  bool aborted() const { return comm_ == nullptr; }
+  ncclComm_t get() const { return comm_.load(std::memory_order_acquire); }
+  bool aborted() const { return get() == nullptr; }
   int rank() const { return rank_; }
   int size() const { return nranks_; }
 
@@ -109,12 +111,16 @@ class RcclComm {
 
  private:
   ncclComm_t live() const {
-    MXS_CHECK(comm_ != nullptr, "RCCL communicator aborted (an earlier wait timed out or failed)");
-    return comm_;
+    ncclComm_t c = get();
+    MXS_CHECK(c != nullptr, "RCCL communicator aborted (an earlier wait timed out or failed)");
+    return c;
   }
   RcclComm() = default;
   // Mutable: a watchdog timeout inside a const wait() aborts and clears it.
-  mutable ncclComm_t comm_ = nullptr;
+  // Atomic: abort() may come from a watchdog thread while this thread is
+  // blocked in a device wait (parallel/watchdog.py); exactly one caller takes
+  // the handle and aborts it.
+  mutable std::atomic<ncclComm_t> comm_{nullptr};
   int rank_ = 0;
   int nranks_ = 1;
   int max_ctas_ = 0;  // 0: RCCL's default

@@ -19,17 +19,20 @@ RcclComm::RcclComm(const std::string& unique_id, int nranks, int rank) : rank_(r
   MXS_CHECK(rank >= 0 && rank < nranks, "RcclComm: bad rank " << rank << " of " << nranks);
   ncclUniqueId id;
   std::memcpy(&id, unique_id.data(), sizeof(id));
-  MXS_RCCL_CHECK(ncclCommInitRank(&comm_, nranks, id, rank));
+  ncclComm_t c = nullptr;
+  MXS_RCCL_CHECK(ncclCommInitRank(&c, nranks, id, rank));
+  comm_.store(c, std::memory_order_release);
 }
 
 RcclComm::~RcclComm() {
-  if (comm_) (void)ncclCommDestroy(comm_);
+  if (ncclComm_t c = comm_.exchange(nullptr)) (void)ncclCommDestroy(c);
 }
 
 bool RcclComm::healthy(std::string* msg) const {
-  if (!comm_) return false;
+  ncclComm_t c = get();
+  if (!c) return false;
   ncclResult_t async = ncclSuccess;
-  if (ncclCommGetAsyncError(comm_, &async) != ncclSuccess || async != ncclSuccess) {
+  if (ncclCommGetAsyncError(c, &async) != ncclSuccess || async != ncclSuccess) {
     if (msg) *msg = ncclGetErrorString(async);
     return false;
   }
@@ -77,8 +80,10 @@ std::unique_ptr<RcclComm> RcclComm::split_with_max_ctas(int max_ctas) const {
   c->rank_ = rank_;
   c->nranks_ = nranks_;
   c->max_ctas_ = max_ctas;
-  MXS_RCCL_CHECK(ncclCommSplit(live(), 0, rank_, &c->comm_, &cfg));
-  MXS_CHECK(c->comm_ != nullptr, "ncclCommSplit returned no communicator");
+  ncclComm_t sc = nullptr;
+  MXS_RCCL_CHECK(ncclCommSplit(live(), 0, rank_, &sc, &cfg));
+  MXS_CHECK(sc != nullptr, "ncclCommSplit returned no communicator");
+  c->comm_.store(sc, std::memory_order_release);
   return c;
 }
 
@@ -95,8 +100,7 @@ int RcclComm::device() const {
 }
 
 void RcclComm::abort() const {
-  if (comm_) (void)ncclCommAbort(comm_);
-  comm_ = nullptr;
+  if (ncclComm_t c = comm_.exchange(nullptr)) (void)ncclCommAbort(c);
 }
 
 }  // namespace mxs
