@@ -989,6 +989,21 @@ bool StencilSolver<T>::halo_last(int S) const {
 // the two launches write disjoint cells of nxt. The inner launch is submitted
 // first, so it holds its CUs before RCCL's kernels look for free ones; with
 // streams that share a hardware queue everything simply runs in order.
+namespace {
+// Copy workgroups of the interior-first opening's pack / unpack: 0 = one-wave
+// workgroups sized from the segments (they fit beside the inner launch's
+// workgroups). MXS_HALO_LAST_COPY_WGS (experiments build): 4-wave workgroups,
+// that many per segment; 4 per segment made the exchange so slow that the
+// 8-GPU-tile opening took 0.415 ms instead of 0.264.
+int halo_last_copy_wgs() {
+  static const int copy_wgs = [] {
+    const char* e = experiment_env("MXS_HALO_LAST_COPY_WGS");
+    return e ? std::atoi(e) : 0;
+  }();
+  return copy_wgs;
+}
+}  // namespace
+
 template <typename T>
 void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks* marks) {
   MXS_TRACE_RANGE("stencil.superstep_halo_last");
@@ -1028,14 +1043,7 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
     packed_ = fuse ? nxt : cur;
     return;
   }
-  // One-wave copy workgroups sized from the segments (they fit beside the inner
-  // launch's workgroups). MXS_HALO_LAST_COPY_WGS (experiments build): 4-wave
-  // workgroups, that many per segment; 4 per segment made the exchange so slow
-  // that the 8-GPU-tile opening took 0.415 ms instead of 0.264.
-  static const int copy_wgs = [] {
-    const char* e = experiment_env("MXS_HALO_LAST_COPY_WGS");
-    return e ? std::atoi(e) : 0;
-  }();
+  const int copy_wgs = halo_last_copy_wgs();
   ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
   ex_->set_copy_grid(copy_wgs);
   if (marks) {
@@ -1082,10 +1090,7 @@ bool StencilSolver<T>::capture_chain(HaloLastPass* hl) {
     }
     bool ok = true;
     try {
-      static const int copy_wgs = [] {
-        const char* e = experiment_env("MXS_HALO_LAST_COPY_WGS");
-        return e ? std::atoi(e) : 0;
-      }();
+      const int copy_wgs = halo_last_copy_wgs();
       // With the fused pack the chain starts at the transfer (the launch site
       // sees to the send buffer), else with the pack launch.
       packed_ = fuse ? cur : nullptr;
