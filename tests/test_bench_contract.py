@@ -85,6 +85,15 @@ def test_bench_eight_ranks_cpu_walks_the_8gpu_path():
     # Self-description keys of an N > 1 record (GPU-only ones are absent on CPU).
     assert ex["timed_super_steps"] == [[1, 3]] and ex["halo"].startswith("torch-p2p")
     assert "pingpong_ipc" in ex and isinstance(ex["env"], dict)
+    # The window ends at torch.cuda.synchronize() alone (under the timer-thread watchdog on GPU).
+    assert ex["window_sync"] == "torch"
+
+
+def test_bench_window_sync_solver_cpu():
+    r = run_ranks("bench", 2, {"argv": ["--gpus", "2", "--global", "128x96", "--steps", "4", "--warmup", "1",
+                                        "--no-extras", "--window-sync", "solver"]})
+    assert r[0]["rc"] == 0 and r[1]["rc"] == 0
+    assert _check(r[0]["line"], 2, 4, 1)["extras"]["window_sync"] == "solver"
 
 
 def test_isolated_ipc_pingpong_failure_is_recorded_not_fatal():
