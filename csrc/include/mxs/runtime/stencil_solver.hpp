@@ -167,10 +167,12 @@ struct SolverConfig {
   // Auto: interior-first must beat serial by at least this fraction (and by
   // more than the measured spread) to be chosen.
   double min_gain = 0.03;
-  // Interior-first opening: replay its main-stream chain (pack -> RCCL ->
-  // unpack -> outer chunks) from a hipGraph captured in prepare(), so the host
-  // issues one launch after the inner chunks instead of the RCCL group calls
-  // and three launches (the outer chunks can start as soon as the unpack ends).
+  // The opening from hipGraphs captured in prepare(): the interior-first
+  // opening's main-stream chain (pack -> RCCL -> unpack -> outer chunks), and
+  // the serial opening's priming exchange (pack -> RCCL -> unpack). The host
+  // issues one launch instead of the RCCL group calls and the copy launches,
+  // so the GPU does not wait for the host's RCCL enqueue (~25 us) between the
+  // pack and the transfer.
   bool opening_graph = false;
   // Fused halo pack: the whole-core pipeline passes of the post-exchange
   // schedules (the bare pass, the interior-first opening's outer chunks, the
@@ -311,6 +313,7 @@ class StencilSolver {
     if (!cfg_.opening_graph) return "off";
     for (const auto& hl : halo_lasts_)
       if (hl && hl->chain_tried) return hl->chain_ok ? "captured" : "capture failed";
+    if (prime_graph_.tried) return prime_graph_.ok ? "captured" : "capture failed";
     return "not used yet";
   }
   const std::string& halo_comm_note() const { return halo_comm_note_; }
@@ -395,6 +398,14 @@ class StencilSolver {
     bool outer_packs = false;
   };
   bool capture_chain(HaloLastPass* hl);
+  // The serial priming exchange of cur_ (SolverConfig::opening_graph: from a
+  // graph per buffer orientation, captured on first use).
+  void prime_exchange();
+  struct PrimeGraph {
+    GraphExec g[2];
+    bool tried = false, ok = false;
+  };
+  PrimeGraph prime_graph_;
   HaloLastPass* halo_last_pass(int S, bool build);  // nullptr: not in use / no form for S
   std::unique_ptr<HaloLastPass> build_halo_last(int S, int outer_wgs);  // nullptr: no form for S
   void enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks* marks = nullptr);

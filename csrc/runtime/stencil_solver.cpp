@@ -414,7 +414,7 @@ void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
   // exchanges first and leaves it stale.
   if (post_exchange() && !ghost_fresh_) {
     if (first && last_opening_.empty()) last_opening_ = "serial";
-    exchange(cur_, main_.get());
+    prime_exchange();
     ++last_exchanges_;
   }
   if (first && last_opening_.empty()) last_opening_ = post_exchange() ? "fresh" : "overlap";
@@ -684,7 +684,7 @@ void StencilSolver<T>::choose_opening(int S) {
   std::vector<std::vector<double>> t_cand(kCands), ratio(kCands);
   for (int rep = 0; rep < kReps; ++rep) {
     const double serial = timed(false, [&] {
-      exchange(cur_, main_.get());
+      prime_exchange();
       enqueue_bare_pass(cur_, nxt_, S);
     });
     if (rep > 0) t_serial.push_back(serial);
@@ -693,7 +693,7 @@ void StencilSolver<T>::choose_opening(int S) {
         if (c < cands.size()) {
           enqueue_halo_last(cur_, nxt_, cands[c]);
         } else {
-          exchange(cur_, main_.get());
+          prime_exchange();
           enqueue_bare_pass(cur_, nxt_, S);
         }
       });
@@ -847,7 +847,7 @@ void StencilSolver<T>::validate_direct(int S) {
           if (halo_last_on_) {
             enqueue_opening(S, false);
           } else {
-            exchange(cur_, m);
+            prime_exchange();
             core_pass(cur_, nxt_, S, m);
           }
         });
@@ -1126,12 +1126,73 @@ bool StencilSolver<T>::capture_chain(HaloLastPass* hl) {
 }
 
 template <typename T>
+void StencilSolver<T>::prime_exchange() {
+  hipStream_t m = main_.get();
+  if (!cfg_.opening_graph || !post_exchange()) {
+    exchange(cur_, m);
+    return;
+  }
+  // Captured with the pack launch, or without it when the passes fuse the
+  // pack (the launch site then sees to the send buffer, as for the chain).
+  const bool fuse = pack_.send != nullptr;
+  if (!prime_graph_.tried) {
+    MXS_TRACE_RANGE("stencil.graph_capture_prime");
+    prime_graph_.tried = true;
+    T* const saved = packed_;
+    const int fused_before = last_fused_packs_;
+    bool all = true;
+    for (int k = 0; k < 2 && all; ++k) {
+      T* tile = k == 0 ? buf_a_ : buf_b_;
+      hipGraph_t g = nullptr;
+      if (hipStreamBeginCapture(m, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+        (void)hipGetLastError();
+        all = false;
+        break;
+      }
+      bool ok = true;
+      try {
+        packed_ = fuse ? tile : nullptr;
+        ex_->set_copy_block(0);
+        exchange(tile, m);
+      } catch (const std::exception&) {
+        ok = false;
+      }
+      const hipError_t end = hipStreamEndCapture(m, &g);
+      if (!ok || end != hipSuccess || g == nullptr) {
+        (void)hipGetLastError();
+        if (g) (void)hipGraphDestroy(g);
+        all = false;
+        break;
+      }
+      if (!prime_graph_.g[k].adopt(g)) {  // adopt() releases g when instantiation fails
+        all = false;
+        break;
+      }
+      prime_graph_.g[k].upload(m);
+    }
+    packed_ = saved;
+    last_fused_packs_ = fused_before;
+    prime_graph_.ok = all;
+  }
+  if (!prime_graph_.ok) {
+    exchange(cur_, m);
+    return;
+  }
+  if (fuse) {
+    if (packed_ == cur_) ++last_fused_packs_;
+    ensure_packed(cur_, m);
+  }
+  prime_graph_.g[cur_ == buf_a_ ? 0 : 1].launch(m);
+  packed_ = cur_;
+}
+
+template <typename T>
 void StencilSolver<T>::enqueue_opening(int S, bool advance) {
   if (HaloLastPass* hl = halo_last_pass(S, true)) {
     enqueue_halo_last(cur_, nxt_, hl);
   } else {  // no chunk-list form on this tile: the same one exchange, then the pass
     join_side();
-    exchange(cur_, main_.get());
+    prime_exchange();
     enqueue_bare_pass(cur_, nxt_, S);
   }
   if (advance) std::swap(cur_, nxt_);
@@ -1163,7 +1224,7 @@ void StencilSolver<T>::prepare(int iters) {
   for (const Group& g : gr) {
     if (g.count <= 0) continue;
     if (post_exchange() && !ghost_fresh_) {
-      exchange(cur_, main_.get());
+      prime_exchange();  // (captures the serial opening's graph, opening_graph)
       ghost_fresh_ = true;
     }
     (void)graphs_for(g.S, g.count);
@@ -1193,7 +1254,7 @@ void StencilSolver<T>::warm(int iters, int passes) {
   Group gr[2];
   split(iters, gr);
   if (post_exchange() && !ghost_fresh_) {
-    exchange(cur_, main_.get());
+    prime_exchange();
     ghost_fresh_ = true;
   }
   for (int p = 0; p < passes; ++p)

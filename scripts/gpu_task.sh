@@ -16,6 +16,7 @@
 #                          peers' schedule against the fused-periodic tile (no exchange). MODES (default
 #                          "auto fused"; --serial = "auto serial fused"): auto, serial, ifirst (forced
 #                          interior-first), graph (interior-first, its main-stream chain as a hipGraph),
+#                          sgraph (serial, its priming exchange as a hipGraph),
 #                          fused; suffixes: -fp adds --fused-pack, -ssync --window-sync solver (in that
 #                          order, e.g. ifirst-fp-ssync) -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
@@ -97,6 +98,7 @@ task_window() {
         serial) args+=(--loopback --rehearse-peers --opening serial) ;;
         ifirst) args+=(--loopback --rehearse-peers --opening interior-first) ;;
         graph) args+=(--loopback --rehearse-peers --opening interior-first --opening-graph) ;;
+        sgraph) args+=(--loopback --rehearse-peers --opening serial --opening-graph) ;;
         fused) ;;
         *) echo "unknown window mode '$mode'"; exit 2 ;;
       esac

@@ -356,13 +356,15 @@ def test_halo_communicator_with_cta_cap(gpu):
     assert torch.equal(a.core_view(), b.core_view())
 
 
+@pytest.mark.parametrize("opening", ["interior-first", "serial"])
 @pytest.mark.parametrize("runs", [(20, 20, 40, 20), (60,)])
-def test_opening_graph_bitwise_both_orientations(gpu, runs):
+def test_opening_graph_bitwise_both_orientations(gpu, runs, opening):
     """opening_graph: the interior-first opening's main-stream chain (pack, RCCL,
-    unpack, outer chunks) replayed from one of two hipGraphs (a 20-step call
-    flips the buffers, so consecutive calls open from both orientations).
-    Bitwise the serial schedule's field; still one exchange per super-step."""
-    a = _loopback(16384, 8192, seed=82, opening="interior-first", rehearse_peers=True, time_block=20,
+    unpack, outer chunks), or the serial opening's priming exchange, replayed
+    from one of two hipGraphs (a 20-step call flips the buffers, so consecutive
+    calls open from both orientations). Bitwise the serial schedule's field;
+    still one exchange per super-step."""
+    a = _loopback(16384, 8192, seed=82, opening=opening, rehearse_peers=True, time_block=20,
                   opening_graph=True)
     b = _loopback(16384, 8192, seed=82, opening="serial", time_block=20)
     assert a.solver.opening_graph_state() == "not used yet"
@@ -370,7 +372,7 @@ def test_opening_graph_bitwise_both_orientations(gpu, runs):
     assert a.solver.opening_graph_state() == "captured"
     for n in runs:
         a.run(n)
-        assert a.solver.last_run_opening() == "interior-first"
+        assert a.solver.last_run_opening() == opening
         assert a.solver.last_run_exchanges() == n // 20
         b.run(n)
     a.synchronize()
