@@ -472,6 +472,8 @@ def main(argv=None) -> int:
                 extras["timed_exchanges"] = int(st.solver.last_run_exchanges())
                 # Of those, the exchanges whose pack the preceding pass wrote (fused pack).
                 extras["timed_fused_packs"] = int(st.solver.last_run_fused_packs())
+                if st.solver.stream_note():
+                    extras["side_stream"] = st.solver.stream_note()
                 extras["fused_pack"] = bool(st.solver.fused_pack())
                 extras["schedule_choice"] = {k: (round(v, 4) if isinstance(v, float) else v)
                                              for k, v in st.solver.schedule_times().items()}

@@ -205,6 +205,10 @@ void stencil5_chunk_pass(const T* in, T* out, const TileGeom& g, const Stencil5C
 // any element is NaN): the range check of the sum form.
 template <typename T>
 void absmax(const T* x, index_t n, T* out, hipStream_t s);
+// Whether work on stream b runs while a kernel on stream a still runs (the two
+// sit on different hardware queues): one bounded ~0.8 ms sleeping wave on a, a
+// no-op kernel on b (kernels/queue_probe.hip). Synchronises both streams.
+bool streams_concurrent(hipStream_t a, hipStream_t b);
 // Number of 32-bit words that differ between a and b (bytes % 4 == 0) into
 // *out (device pointer, overwritten): the direct halo's bitwise validation.
 void count_diff(const void* a, const void* b, index_t bytes, unsigned* out, hipStream_t s);

@@ -88,6 +88,7 @@ class Stream {
   Stream(const Stream&) = delete;
   Stream& operator=(const Stream&) = delete;
   hipStream_t get() const { return s_; }
+  void swap(Stream& o) noexcept { std::swap(s_, o.s_); }
   void sync() const { MXS_HIP_CHECK(hipStreamSynchronize(s_)); }
   // Poll for up to `spin_s` seconds, then block. A blocking wait sleeps the
   // host thread: on one GPU it noticed the end of a 2 ms pass ~80 us late and

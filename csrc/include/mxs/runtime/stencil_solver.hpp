@@ -317,6 +317,8 @@ class StencilSolver {
     return "not used yet";
   }
   const std::string& halo_comm_note() const { return halo_comm_note_; }
+  // The side stream's hardware-queue check ("" when no two-stream schedule is possible).
+  const std::string& stream_note() const { return stream_note_; }
   // Abort the halo's own communicator (SolverConfig::halo_max_ctas), from any
   // thread: a watchdog's way to unblock a device wait on a hung peer's exchange.
   void abort_halo_comm() const {
@@ -487,6 +489,8 @@ class StencilSolver {
   // (push of the current bands; the next pass waits for theirs).
   void prime();
   Stream main_, side_;
+  std::vector<std::unique_ptr<Stream>> spare_streams_;  // side streams rejected by the queue check
+  std::string stream_note_;
   Event fork_, interior_;
   std::vector<std::unique_ptr<GraphSet>> graphs_;  // at most kMaxGraphSets sizes, oldest evicted
   static constexpr int kMaxGraphSets = 4;

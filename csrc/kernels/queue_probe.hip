@@ -1,0 +1,57 @@
+// Whether two HIP streams execute concurrently. HIP maps streams onto a pool of
+// hardware queues (GPU_MAX_HW_QUEUES, 4 here); two streams on one queue run in
+// submission order. The interior-first opening runs its inner chunks on one
+// stream while the exchange and the outer chunks go to another: on a shared
+// queue they serialise and the 8-GPU-tile opening takes ~0.5 ms instead of
+// ~0.3 (seen in 2 of 14 bench-flow windows, profiles/r04_sg).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+
+#include "mxs/core/error.hpp"
+#include "mxs/kernels/kernels.hpp"
+
+namespace mxs {
+namespace kernels {
+namespace {
+
+// One wave sleeping `rounds` x 127 x 64 cycles (~0.8 ms for 200 rounds): bounded.
+__global__ __launch_bounds__(64) void sleep_kernel(unsigned rounds) {
+  for (unsigned i = 0; i < rounds; ++i) __builtin_amdgcn_s_sleep(127);
+}
+
+__global__ __launch_bounds__(64) void touch_kernel(unsigned* p) {
+  if (threadIdx.x == 0 && p) *p = 1u;
+}
+
+}  // namespace
+
+bool streams_concurrent(hipStream_t a, hipStream_t b) {
+  hipEvent_t done_b = nullptr;
+  MXS_HIP_CHECK(hipEventCreateWithFlags(&done_b, hipEventDisableTiming));
+  sleep_kernel<<<1, 64, 0, a>>>(200u);
+  MXS_HIP_CHECK_LAUNCH();
+  touch_kernel<<<1, 64, 0, b>>>(nullptr);
+  MXS_HIP_CHECK_LAUNCH();
+  MXS_HIP_CHECK(hipEventRecord(done_b, b));
+  bool concurrent = false;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipEventQuery(done_b);
+    if (q == hipSuccess) {
+      const hipError_t qa = hipStreamQuery(a);
+      concurrent = qa == hipErrorNotReady;
+      (void)hipGetLastError();
+      break;
+    }
+    if (q != hipErrorNotReady) MXS_HIP_CHECK(q);
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) break;
+  }
+  MXS_HIP_CHECK(hipStreamSynchronize(a));
+  MXS_HIP_CHECK(hipStreamSynchronize(b));
+  (void)hipEventDestroy(done_b);
+  return concurrent;
+}
+
+}  // namespace kernels
+}  // namespace mxs

@@ -271,6 +271,11 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("dtype") = "f32", py::arg("stream") = 0, py::arg("variant") = "auto", py::arg("sum_form") = true,
       "S Jacobi steps over [x0, x1) x [y0, y1); sum_form: allow the sum form when c_center == c_neighbor");
   m.def(
+      "streams_concurrent",
+      [](std::uintptr_t a, std::uintptr_t b) { return kernels::streams_concurrent(strm(a), strm(b)); },
+      py::arg("a"), py::arg("b"), py::call_guard<py::gil_scoped_release>(),
+      "whether work on stream b runs while a kernel on stream a still runs (different hardware queues)");
+  m.def(
       "stencil5_tb_packed",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, double c0, double c1, std::uintptr_t send,
          const std::vector<std::tuple<index_t, index_t, index_t, index_t, index_t>>& windows, const std::string& dt,
@@ -529,6 +534,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def("abort_halo_comm", [](SolverHandle& h) { h.visit([](auto& s) { s.abort_halo_comm(); }); },
            py::call_guard<py::gil_scoped_release>(),
            "abort the halo's own RCCL communicator (halo_max_ctas), e.g. from a watchdog thread")
+      .def("stream_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.stream_note(); }); },
+           "the side stream's hardware-queue check (two-stream schedules)")
       .def("fused_pack", [](SolverHandle& h) { return h.visit([](auto& s) { return s.fused_pack(); }); },
            "whether the passes write the send bands into the exchange's send buffer (SolverConfig::fused_pack)")
       .def("last_run_fused_packs",
@@ -598,6 +605,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def("main_stream",
            [](SolverHandle& h) {
              return h.visit([](auto& s) { return reinterpret_cast<std::uintptr_t>(s.main_stream()); });
+           })
+      .def("side_stream",
+           [](SolverHandle& h) {
+             return h.visit([](auto& s) { return reinterpret_cast<std::uintptr_t>(s.side_stream()); });
            })
       .def("graph_active", [](SolverHandle& h) { return h.visit([](auto& s) { return s.graph_active(); }); })
       .def("graph_status", [](SolverHandle& h) { return h.visit([](auto& s) { return s.graph_status(); }); })

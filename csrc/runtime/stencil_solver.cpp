@@ -133,6 +133,25 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
     agree_max(v, "construction: opening agreement");
     halo_last_allowed_ = v[0] == 0.0;
   }
+  // The interior-first opening and the thin-strip overlap run work on both
+  // streams at once: they must sit on different hardware queues (HIP shares a
+  // pool of GPU_MAX_HW_QUEUES queues among all streams of the process; on a
+  // shared queue the two launches serialise). Checked once; a colliding side
+  // stream is replaced (the rejected one is kept, so the next takes another queue).
+  if (halo_last_allowed_ || cfg_.overlap) {
+    int tries = 0;
+    bool ok = kernels::streams_concurrent(side_.get(), main_.get());
+    for (; !ok && tries < 4; ++tries) {
+      spare_streams_.push_back(std::make_unique<Stream>(true, 0));
+      side_.swap(*spare_streams_.back());
+      ok = kernels::streams_concurrent(side_.get(), main_.get());
+    }
+    stream_note_ = ok ? (tries ? "side stream replaced " + std::to_string(tries) +
+                                     " time(s): it shared the main stream's hardware queue"
+                               : "side stream on its own hardware queue")
+                      : "side stream shares the main stream's hardware queue (after " + std::to_string(tries) +
+                            " replacements): the two-stream schedules serialise";
+  }
   halo_last_on_ = halo_last_allowed_ && cfg_.opening == Opening::InteriorFirst;
   if (halo_last_on_) {
     opening_choice_ = "interior-first";

@@ -474,3 +474,17 @@ def test_pack_epilogue_writes_exactly_the_send_windows(gpu, w, h, dtype, S):
     assert not torch.isnan(send).any()
     for x0, y0, ww, hh, off in wins:
         assert torch.equal(send[off:off + ww * hh].view(hh, ww), core2[y0:y0 + hh, x0:x0 + ww]), (x0, y0, ww, hh)
+
+
+def test_streams_concurrent_probe_and_solver_side_stream(gpu):
+    """The hardware-queue check behind the two-stream schedules: a stream is
+    never concurrent with itself, two fresh streams normally are, and a solver
+    that may run the interior-first opening has its side stream on a queue of
+    its own (replacing it when it collided)."""
+    H = hip()
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    assert H.streams_concurrent(s1.cuda_stream, s1.cuda_stream) is False
+    a = _loopback(4096, 2048, seed=95, opening="auto", rehearse_peers=True, time_block=24)
+    note = a.solver.stream_note()
+    assert note.startswith("side stream on its own") or note.startswith("side stream replaced"), note
+    assert H.streams_concurrent(a.solver.side_stream(), a.solver.main_stream()) is True
