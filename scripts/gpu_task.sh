@@ -112,7 +112,7 @@ import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1]); e = d["extras"]
 print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["ms_per_step"] * d["steps"], 4),
                   "opening": e.get("opening"), "opening_graph": e.get("opening_graph"),
-                  "fused_packs": e.get("timed_fused_packs"),
+                  "fused_packs": e.get("timed_fused_packs"), "side_stream": e.get("side_stream"),
                   "phases": e.get("window_phases")}))
 PY
     done
