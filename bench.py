@@ -351,12 +351,13 @@ def main(argv=None) -> int:
     p.add_argument("--opening-graph", action="store_true",
                    help="N > 1: replay the interior-first opening's main-stream chain (pack, RCCL, unpack, outer "
                         "chunks) from a hipGraph captured in prepare()")
-    p.add_argument("--window-sync", default="torch", choices=["solver", "torch"],
-                   help="how the timed window ends: torch (default) = torch.cuda.synchronize() alone, under a "
-                        "timer-thread watchdog that aborts the halo's RCCL communicators past --comm-timeout "
-                        "(the solver's own checks follow outside the window); solver = solver.synchronize() "
-                        "(stream polls under the RCCL watchdog) then torch.cuda.synchronize(), ~8-10 us more per "
-                        "window (profiles/r04_sync)")
+    p.add_argument("--window-sync", default="auto", choices=["auto", "solver", "torch"],
+                   help="how the timed window ends: torch = torch.cuda.synchronize() alone, under a timer-thread "
+                        "watchdog that aborts the halo's RCCL communicators past --comm-timeout; solver = "
+                        "solver.synchronize() (polls the solver's streams, RCCL watchdog) then "
+                        "torch.cuda.synchronize(); auto (default): torch for a solver without a communicator (the "
+                        "1-GPU fused tile: 8-20 us less per window), solver otherwise (with two streams in flight "
+                        "the device sync alone returned ~0.2 ms late in 2-4 of 16 windows; profiles/r04_sync)")
     p.add_argument("--fused-pack", action="store_true",
                    help="N > 1: the pipeline passes write their send bands into the exchange's send buffer, so "
                         "the exchange after them has no pack launch (default off: measured slower on the 8-GPU-tile "
@@ -423,8 +424,10 @@ def main(argv=None) -> int:
                         fused_pack=args.fused_pack,
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
-    dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3, args.window_sync,
-                   args.comm_timeout)
+    window_sync = args.window_sync
+    if window_sync == "auto":
+        window_sync = "torch" if st.comm is None else "solver"
+    dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3, window_sync, args.comm_timeout)
     timed_blocks = st.last_run_blocks()  # the super-steps the timed window executed
     value = st.cells_per_step * args.steps / dt / 1e9
     halo = st.halo_mode()  # what the timed run() executed
@@ -442,7 +445,7 @@ def main(argv=None) -> int:
                                    "c_neighbor = 0.2; range-guarded: 5|c| <= 1, max|u| 5^S < FLT_MAX/4)"
                                    if sum_used else "per step: fma(c_n, (n+s)+(w+e), c_c*c)"),
                     "clock_warmup_ms": args.clock_warmup_ms,
-                    "window_sync": args.window_sync,
+                    "window_sync": window_sync,
                     "tile": f"{st.decomp.width}x{st.decomp.height}",
                     "process_grid": f"{rows} rows x {cols} cols of ranks",
                     "env": env}

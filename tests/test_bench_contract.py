@@ -85,7 +85,7 @@ def test_bench_eight_ranks_cpu_walks_the_8gpu_path():
     # Self-description keys of an N > 1 record (GPU-only ones are absent on CPU).
     assert ex["timed_super_steps"] == [[1, 3]] and ex["halo"].startswith("torch-p2p")
     assert "pingpong_ipc" in ex and isinstance(ex["env"], dict)
-    # The window ends at torch.cuda.synchronize() alone (under the timer-thread watchdog on GPU).
+    # No native communicator (gloo, torch halo): the window ends at torch.cuda.synchronize() alone.
     assert ex["window_sync"] == "torch"
 
 

@@ -43,6 +43,8 @@ def test_bench_8gpu_tile_window_through_loopback(gpu):
     assert ex["stencil_kernel"] == ("stream_pipe_sum_chunks" if ex["opening"] == "interior-first"
                                     else "stream_pipe_sum")
     assert ex["rccl_ranks"] == 1 and len(ex["rank_devices"]) == 1
+    # Two streams in flight: the window ends at the solver's polled wait, then the device sync.
+    assert ex["window_sync"] == "solver"
     ph = ex["window_phases"]
     assert ph["opening"] == ex["opening"] and ph["exchanges"] == 1
     assert {"main:pack", "main:rccl", "main:unpack"} <= set(ph["phases_us"])
@@ -53,11 +55,11 @@ def test_bench_8gpu_tile_window_through_loopback(gpu):
     assert d["value"] > 5000, d
 
 
-@pytest.mark.parametrize("extra", [["--window-sync", "solver"], ["--fused-pack"]])
+@pytest.mark.parametrize("extra", [["--window-sync", "torch"], ["--fused-pack"]])
 def test_bench_window_options_through_loopback(gpu, extra):
-    """--window-sync solver (the window ends at solver.synchronize()'s polled
-    wait, then torch.cuda.synchronize(); the default is torch.cuda.synchronize()
-    alone under the timer-thread watchdog) and --fused-pack (the passes write
+    """--window-sync torch (the window ends at torch.cuda.synchronize() alone,
+    under the timer-thread watchdog; with a communicator the default is the
+    solver's polled wait, then torch.cuda.synchronize()) and --fused-pack (the passes write
     their send bands: the window's priming exchange has no pack launch) run and
     say so in the record."""
     env = dict(os.environ, PYTHONUNBUFFERED="1")
@@ -68,7 +70,7 @@ def test_bench_window_options_through_loopback(gpu, extra):
     ex = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["extras"]
     assert ex["timed_exchanges"] == 1
     if extra[0] == "--window-sync":
-        assert ex["window_sync"] == "solver" and ex["timed_fused_packs"] == 0
+        assert ex["window_sync"] == "torch" and ex["timed_fused_packs"] == 0
     else:
         assert ex["fused_pack"] is True and ex["timed_fused_packs"] == 1
         assert "main:pack" not in ex["window_phases"]["phases_us"]
