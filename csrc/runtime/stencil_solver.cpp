@@ -1280,9 +1280,8 @@ void StencilSolver<T>::warm(int iters, int passes) {
     for (const Group& g : gr)
       if (g.count > 0) enqueue_block(cur_, nxt_, g.S);  // cur -> nxt, no swap: state unchanged
   // End on the opening's own shape (cur -> nxt, one exchange on every rank):
-  // the side stream's hardware queue was idle through the passes above, and
-  // the first launch into an idle queue can start late (a 20-step window then
-  // measured ~0.48 ms instead of ~0.30 in 4 of 20 bench runs, profiles/r04_qw).
+  // a short window is that super-step, so its launches (both chunk-list
+  // passes, the copies beside them) and both streams are the last thing warmed.
   if (passes > 0 && halo_last_on_ && post_exchange()) {
     const Group& first = gr[0].count > 0 ? gr[0] : gr[1];
     join_side();
