@@ -126,6 +126,9 @@ def test_bench_torchrun(gpu, n):
     assert ex["timed_exchanges"] == 1 and ex["timed_super_steps"] == [[20, 1]]
     assert ex["rccl_ranks"] == n and len(set(x.split(":")[0] for x in ex["rank_devices"])) == n
     assert ex["window_phases"]["exchanges"] == 1
+    # A communicator is in use: the window ends at the solver's polled wait, then the device sync.
+    assert ex["window_sync"] == "solver" and ex["fused_pack"] is False
+    assert ex["side_stream"].startswith("side stream on its own") or ex["side_stream"].startswith("side stream replaced")
     if n == 8:
         assert ex["tile"] == "16384x8192"
 
