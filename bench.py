@@ -358,9 +358,6 @@ def main(argv=None) -> int:
                         "torch.cuda.synchronize(); auto (default): torch for a solver without a communicator (the "
                         "1-GPU fused tile: 8-20 us less per window), solver otherwise (with two streams in flight "
                         "the device sync alone returned ~0.2 ms late in 2-4 of 16 windows; profiles/r04_sync)")
-    p.add_argument("--steady-interior-first", action="store_true",
-                   help="N > 1 with the interior-first opening: every super-step of the window (not only the "
-                        "first) exchanges its input under its own inner chunks")
     p.add_argument("--fused-pack", action="store_true",
                    help="N > 1: the pipeline passes write their send bands into the exchange's send buffer, so "
                         "the exchange after them has no pack launch (default off: measured slower on the 8-GPU-tile "
@@ -424,7 +421,7 @@ def main(argv=None) -> int:
                         sum_form=not args.no_sum_form, opening=args.opening, rehearse_peers=args.rehearse_peers,
                         direct_halo=("validate" if args.direct_halo == "validate" else None),
                         halo_max_ctas=args.halo_max_ctas, opening_graph=args.opening_graph,
-                        fused_pack=args.fused_pack, steady_interior_first=args.steady_interior_first,
+                        fused_pack=args.fused_pack,
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     window_sync = args.window_sync

@@ -174,10 +174,6 @@ struct SolverConfig {
   // so the GPU does not wait for the host's RCCL enqueue (~25 us) between the
   // pack and the transfer.
   bool opening_graph = false;
-  // With the interior-first opening on: every super-step of a call, not only
-  // the first, exchanges its input under its own inner chunks (eager launches;
-  // one cross-stream wait each way per super-step).
-  bool steady_interior_first = false;
   // Fused halo pack: the whole-core pipeline passes of the post-exchange
   // schedules (the bare pass, the interior-first opening's outer chunks, the
   // steady super-steps) also write their send bands into the exchange's send

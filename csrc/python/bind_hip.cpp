@@ -441,10 +441,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
                        py::object bootstrap, int graph_supersteps, bool sum_form, const std::string& direct_halo,
                        double graph_max_superstep_us, const std::string& opening, bool rehearse_peers,
-                       double min_gain, int halo_max_ctas, bool opening_graph, bool fused_pack,
-                       bool steady_interior_first) {
+                       double min_gain, int halo_max_ctas, bool opening_graph, bool fused_pack) {
              SolverConfig cfg;
-             cfg.steady_interior_first = steady_interior_first;
              cfg.fused_pack = fused_pack;
              cfg.halo_max_ctas = halo_max_ctas;
              cfg.opening_graph = opening_graph;
@@ -489,7 +487,6 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = "off",
            py::arg("graph_max_superstep_us") = 150.0, py::arg("opening") = "auto", py::arg("rehearse_peers") = false,
            py::arg("min_gain") = 0.03, py::arg("halo_max_ctas") = 0, py::arg("opening_graph") = false, py::arg("fused_pack") = false,
-           py::arg("steady_interior_first") = false,
            py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")

@@ -427,29 +427,6 @@ void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
     ghost_fresh_ = false;  // its output's ring: primed by the next super-step / call
     if (--count == 0) return;
   }
-  // Steady interior-first (SolverConfig::steady_interior_first): every later
-  // super-step exchanges its input under its own inner chunks as well. The
-  // exchange count is the serial schedule's (a group not ending on a bare pass
-  // also exchanges its output at the end), so ranks without the chunk-list
-  // form for S (they run the serial schedule) stay matched.
-  if (cfg_.steady_interior_first && halo_last_on_ && post_exchange() && !ghost_fresh_) {
-    if (HaloLastPass* hl = halo_last_pass(S, true)) {
-      const bool tail = !(last_bare && multi_rank_);
-      for (int i = 0; i < count; ++i) {
-        enqueue_halo_last(cur_, nxt_, hl);
-        std::swap(cur_, nxt_);
-      }
-      last_exchanges_ += count;
-      join_side();
-      if (tail) {
-        exchange(cur_, main_.get());
-        ++last_exchanges_;
-      }
-      if (first && last_opening_.empty()) last_opening_ = "interior-first";
-      ghost_fresh_ = tail;
-      return;
-    }
-  }
   join_side();  // an interior-first opening leaves side work pending
   // Post-exchange super-steps: cur's ghost ring must be fresh before the first
   // one; each leaves the next one's fresh. The thin-strip overlap schedule

@@ -100,9 +100,6 @@ class StencilConfig:
     # exchange's send buffer, so the next exchange is RCCL + unpack. Off by
     # default (measured slower: the pack launch hides the host's RCCL enqueue).
     fused_pack: bool = False
-    # With the interior-first opening on: every super-step of a call exchanges
-    # its input under its own inner chunks, not only the first.
-    steady_interior_first: bool = False
     # Super-steps estimated longer than this run from eager launches, not a
     # hipGraph (long passes: eager measured faster). 0 = always graphs.
     graph_max_superstep_us: float = 150.0
@@ -205,8 +202,7 @@ class Stencil2D:
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
                                           self._direct_mode(backend),
                                           cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain,
-                                          cfg.halo_max_ctas, cfg.opening_graph, cfg.fused_pack,
-                                          cfg.steady_interior_first)
+                                          cfg.halo_max_ctas, cfg.opening_graph, cfg.fused_pack)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()

@@ -16,8 +16,7 @@
 #                          peers' schedule against the fused-periodic tile (no exchange). MODES (default
 #                          "auto fused"; --serial = "auto serial fused"): auto, serial, ifirst (forced
 #                          interior-first), graph (interior-first, its main-stream chain as a hipGraph),
-#                          sgraph (serial, its priming exchange as a hipGraph), steady (every super-step
-#                          interior-first),
+#                          sgraph (serial, its priming exchange as a hipGraph),
 #                          fused; suffixes: -fp adds --fused-pack, -ssync --window-sync solver (in that
 #                          order, e.g. ifirst-fp-ssync) -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
@@ -90,7 +89,7 @@ task_window() {
   if [ "${1:-}" = "--serial" ]; then modes="auto serial fused"; elif [ $# -gt 0 ]; then modes="$*"; fi
   for i in $(seq "$reps"); do
     for mode in $modes; do
-      local args=(--global "$tile" --steps "${WINDOW_STEPS:-20}" --warmup 5 --no-extras)
+      local args=(--global "$tile" --steps 20 --warmup 5 --no-extras)
       local base=$mode
       case $base in *-ssync) args+=(--window-sync solver); base=${base%-ssync} ;; esac
       case $base in *-fp) args+=(--fused-pack); base=${base%-fp} ;; esac
@@ -100,7 +99,6 @@ task_window() {
         ifirst) args+=(--loopback --rehearse-peers --opening interior-first) ;;
         graph) args+=(--loopback --rehearse-peers --opening interior-first --opening-graph) ;;
         sgraph) args+=(--loopback --rehearse-peers --opening serial --opening-graph) ;;
-        steady) args+=(--loopback --rehearse-peers --opening interior-first --steady-interior-first) ;;
         fused) ;;
         *) echo "unknown window mode '$mode'"; exit 2 ;;
       esac

@@ -488,22 +488,3 @@ def test_streams_concurrent_probe_and_solver_side_stream(gpu):
     note = a.solver.stream_note()
     assert note.startswith("side stream on its own") or note.startswith("side stream replaced"), note
     assert H.streams_concurrent(a.solver.side_stream(), a.solver.main_stream()) is True
-
-
-@pytest.mark.parametrize("runs", [(60,), (40, 7, 20), (24, 24)])
-def test_steady_interior_first_bitwise_and_exchange_count(gpu, runs):
-    """steady_interior_first: every super-step exchanges its input under its
-    own inner chunks. Bitwise the serial schedule's field, and the same number
-    of exchanges per call (the peers' schedule: one per super-step)."""
-    a = _loopback(16384, 8192, seed=96, opening="interior-first", rehearse_peers=True, time_block=20,
-                  steady_interior_first=True)
-    b = _loopback(16384, 8192, seed=96, opening="serial", rehearse_peers=True, time_block=20)
-    for n in runs:
-        a.run(n)
-        b.run(n)
-        assert a.solver.last_run_exchanges() == b.solver.last_run_exchanges(), n
-        assert a.solver.last_run_opening() == ("interior-first" if a.solver.halo_last(a.last_run_blocks()[0][0])
-                                               else "serial")
-    a.synchronize()
-    b.synchronize()
-    assert torch.equal(a.core_view(), b.core_view())
