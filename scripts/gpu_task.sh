@@ -11,7 +11,7 @@
 #   smoke                  __graft_entry__.smoke()                  -> OUT/smoke.txt
 #   bench [BENCH ARGS]     python bench.py ARGS                      -> OUT/bench.txt (JSON line echoed)
 #   prof NAME [BENCH ARGS] rocprofv3 --kernel-trace --stats of bench.py ARGS -> OUT/prof_NAME/
-#   window TILE REPS [--serial | MODES...]
+#   window TILE REPS [--serial | MODES...]   (WINDOW_STEPS=K: K-step windows, default 20)
 #                          interleaved single-shot bench-flow windows on TILE: RCCL loopback in the
 #                          peers' schedule against the fused-periodic tile (no exchange). MODES (default
 #                          "auto fused"; --serial = "auto serial fused"): auto, serial, ifirst (forced
@@ -89,7 +89,7 @@ task_window() {
   if [ "${1:-}" = "--serial" ]; then modes="auto serial fused"; elif [ $# -gt 0 ]; then modes="$*"; fi
   for i in $(seq "$reps"); do
     for mode in $modes; do
-      local args=(--global "$tile" --steps 20 --warmup 5 --no-extras)
+      local args=(--global "$tile" --steps "${WINDOW_STEPS:-20}" --warmup 5 --no-extras)
       local base=$mode
       case $base in *-ssync) args+=(--window-sync solver); base=${base%-ssync} ;; esac
       case $base in *-fp) args+=(--fused-pack); base=${base%-fp} ;; esac
