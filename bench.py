@@ -358,6 +358,9 @@ def main(argv=None) -> int:
                         "torch.cuda.synchronize(); auto (default): torch for a solver without a communicator (the "
                         "1-GPU fused tile: 8-20 us less per window), solver otherwise (with two streams in flight "
                         "the device sync alone returned ~0.2 ms late in 2-4 of 16 windows; profiles/r04_sync)")
+    p.add_argument("--device-schedule", default="auto", choices=["auto", "spin", "yield"],
+                   help="hipSetDeviceFlags schedule for host waits (spin: a waiting host thread polls instead of "
+                        "yielding; auto: HIP's heuristic, yield on this many-core host)")
     p.add_argument("--fused-pack", action="store_true",
                    help="N > 1: the pipeline passes write their send bands into the exchange's send buffer, so "
                         "the exchange after them has no pack launch (default off: measured slower on the 8-GPU-tile "
@@ -402,10 +405,14 @@ def main(argv=None) -> int:
     n = ctx.world_size
     if n != args.gpus and ctx.is_root:
         print(f"warning: --gpus {args.gpus} but world size {n}", file=sys.stderr)
+    device_schedule = None
     if gpu:
         from cuda_mpi_scratch_amd import hip
 
         hip().set_comm_timeout(args.comm_timeout)  # RCCL / IPC waits fail instead of hanging
+        if args.device_schedule != "auto":
+            err, flags = hip().set_device_schedule(args.device_schedule)
+            device_schedule = {"mode": args.device_schedule, "result": err, "flags": int(flags)}
     # Default process grid: MPI_Dims_create order (rows >= cols; 8 -> 4 rows x 2
     # columns). Each rank's tile is then wider than tall (16384 x 8192 on 8
     # GPUs): the row-streaming kernel runs 7.5% faster on it than on
@@ -446,6 +453,7 @@ def main(argv=None) -> int:
                                    if sum_used else "per step: fma(c_n, (n+s)+(w+e), c_c*c)"),
                     "clock_warmup_ms": args.clock_warmup_ms,
                     "window_sync": window_sync,
+                    **({"device_schedule": device_schedule} if device_schedule else {}),
                     "tile": f"{st.decomp.width}x{st.decomp.height}",
                     "process_grid": f"{rows} rows x {cols} cols of ranks",
                     "env": env}

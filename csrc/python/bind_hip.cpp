@@ -271,6 +271,23 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("dtype") = "f32", py::arg("stream") = 0, py::arg("variant") = "auto", py::arg("sum_form") = true,
       "S Jacobi steps over [x0, x1) x [y0, y1); sum_form: allow the sum form when c_center == c_neighbor");
   m.def(
+      "set_device_schedule",
+      [](const std::string& mode) {
+        unsigned f = hipDeviceScheduleAuto;
+        if (mode == "spin") f = hipDeviceScheduleSpin;
+        else if (mode == "yield") f = hipDeviceScheduleYield;
+        else if (mode == "blocking") f = hipDeviceScheduleBlockingSync;
+        else if (mode != "auto") throw std::invalid_argument("schedule must be spin, yield, blocking or auto");
+        const hipError_t e = hipSetDeviceFlags(f);
+        unsigned now = 0;
+        (void)hipGetDeviceFlags(&now);
+        (void)hipGetLastError();
+        return py::make_tuple(std::string(hipGetErrorName(e)), now);
+      },
+      py::arg("mode"),
+      "hipSetDeviceFlags for the current device: how host waits detect completion (spin = lowest latency); "
+      "returns (hip error name, flags now in effect)");
+  m.def(
       "streams_concurrent",
       [](std::uintptr_t a, std::uintptr_t b) { return kernels::streams_concurrent(strm(a), strm(b)); },
       py::arg("a"), py::arg("b"), py::call_guard<py::gil_scoped_release>(),

@@ -17,8 +17,9 @@
 #                          "auto fused"; --serial = "auto serial fused"): auto, serial, ifirst (forced
 #                          interior-first), graph (interior-first, its main-stream chain as a hipGraph),
 #                          sgraph (serial, its priming exchange as a hipGraph),
-#                          fused; suffixes: -fp adds --fused-pack, -ssync --window-sync solver (in that
-#                          order, e.g. ifirst-fp-ssync) -> OUT/window_TILE.jsonl + medians
+#                          fused; suffixes: -fp adds --fused-pack, -ssync / -tsync --window-sync solver /
+#                          torch, -spin --device-schedule spin (in that order, e.g. ifirst-fp-tsync-spin)
+#                          -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
 #   final                  tests + smoke + the driver's bench command + its kernel-trace profile
 set -uo pipefail
@@ -91,6 +92,8 @@ task_window() {
     for mode in $modes; do
       local args=(--global "$tile" --steps "${WINDOW_STEPS:-20}" --warmup 5 --no-extras)
       local base=$mode
+      case $base in *-spin) args+=(--device-schedule spin); base=${base%-spin} ;; esac
+      case $base in *-tsync) args+=(--window-sync torch); base=${base%-tsync} ;; esac
       case $base in *-ssync) args+=(--window-sync solver); base=${base%-ssync} ;; esac
       case $base in *-fp) args+=(--fused-pack); base=${base%-fp} ;; esac
       case $base in
@@ -113,6 +116,7 @@ d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1]); e = d["
 print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["ms_per_step"] * d["steps"], 4),
                   "opening": e.get("opening"), "opening_graph": e.get("opening_graph"),
                   "fused_packs": e.get("timed_fused_packs"), "side_stream": e.get("side_stream"),
+                  "window_sync": e.get("window_sync"), "device_schedule": e.get("device_schedule"),
                   "phases": e.get("window_phases")}))
 PY
     done
