@@ -698,7 +698,7 @@ void StencilSolver<T>::choose_opening(int S) {
     wait_idle("prepare: opening timing");
     return std::max(double(e1.since(e0)), double(e2.since(e0)));
   };
-  constexpr int kCands = 3, kReps = 13;  // round 0 warms every shape
+  constexpr int kCands = 3, kReps = 21;  // round 0 warms every shape (20 paired rounds: the notch is 1.58 IQR / sqrt(20))
   std::vector<double> t_serial;
   std::vector<std::vector<double>> t_cand(kCands), ratio(kCands);
   for (int rep = 0; rep < kReps; ++rep) {

@@ -36,7 +36,7 @@ def test_bench_8gpu_tile_window_through_loopback(gpu):
     # The record describes what ran: one 20-step pass, one exchange, the opening.
     assert ex["halo"].startswith("20 iterations as 1 x 20-step pass; 1 halo exchange by RCCL")
     sc = ex["schedule_choice"]
-    assert sc["opening"] in ("serial", "interior-first") and sc["samples"] == 12 and sc["reason"]
+    assert sc["opening"] in ("serial", "interior-first") and sc["samples"] == 20 and sc["reason"]
     # The window is the call's opening super-step: interior-first when measured faster.
     assert ex["opening"] == sc["opening"]
     # The interior-first opening runs the chunk-list form of the same pipeline kernel.

@@ -214,7 +214,7 @@ def test_auto_opening_is_recorded_thresholded_and_exact(gpu):
     auto.run(20)
     auto.prepare(20)
     t = auto.solver.schedule_times()
-    assert t["opening"] in ("serial", "interior-first") and t["samples"] == 12
+    assert t["opening"] in ("serial", "interior-first") and t["samples"] == 20
     assert t["serial_ms"] > 0 and t["interior_first_ms"] > 0 and t["ratio"] > 0 and t["ratio_iqr"] >= 0
     wins = t["ratio"] <= 0.97 and t["ratio"] + 1.58 * t["ratio_iqr"] / math.sqrt(12) < 1.0
     assert (t["opening"] == "interior-first") == wins == auto.solver.halo_last(20)
