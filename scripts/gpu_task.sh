@@ -117,6 +117,8 @@ print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["
                   "opening": e.get("opening"), "opening_graph": e.get("opening_graph"),
                   "fused_packs": e.get("timed_fused_packs"), "side_stream": e.get("side_stream"),
                   "window_sync": e.get("window_sync"), "device_schedule": e.get("device_schedule"),
+                  "choice": {k: (e.get("schedule_choice") or {}).get(k) for k in ("opening", "ratio", "ratio_iqr",
+                                                                                   "outer_wgs")},
                   "phases": e.get("window_phases")}))
 PY
     done
