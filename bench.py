@@ -131,15 +131,18 @@ def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync
         with st.watchdog(comm_timeout, "timed window"):
             t0 = time.perf_counter()
             st.run(steps)
+            tr = time.perf_counter()
             _sync()
             t1 = time.perf_counter()
         st.synchronize()
     else:
         t0 = time.perf_counter()
         st.run(steps)
+        tr = time.perf_counter()
         st.synchronize()  # polls under the communication watchdog when a peer can hang
         _sync()
         t1 = time.perf_counter()
+    st.timed_host_us = (tr - t0) * 1e6  # the window's enqueue on this rank (diagnostics)
     ctx.barrier()
     return ctx.allreduce_max(t1 - t0)
 
@@ -483,6 +486,8 @@ def main(argv=None) -> int:
                 extras["timed_exchanges"] = int(st.solver.last_run_exchanges())
                 # Of those, the exchanges whose pack the preceding pass wrote (fused pack).
                 extras["timed_fused_packs"] = int(st.solver.last_run_fused_packs())
+                extras["timed_forks"] = int(st.solver.last_run_forks())
+                extras["timed_run_host_us"] = round(getattr(st, "timed_host_us", 0.0), 1)
                 if st.solver.stream_note():
                     extras["side_stream"] = st.solver.stream_note()
                 extras["fused_pack"] = bool(st.solver.fused_pack())

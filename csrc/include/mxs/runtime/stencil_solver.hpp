@@ -328,6 +328,9 @@ class StencilSolver {
   bool fused_pack() const { return pack_.send != nullptr; }
   // Exchanges of the last run() whose pack was fused into the preceding pass.
   int last_run_fused_packs() const { return last_fused_packs_; }
+  // Interior-first super-steps of the last run() whose inner launch had to wait
+  // for the main stream (a cross-stream event); 0 when main had drained.
+  int last_run_forks() const { return last_forks_; }
   int graph_supersteps() const { return chain_; }
   index_t cells_per_iteration() const { return tile_.width * tile_.height; }
 
@@ -346,6 +349,7 @@ class StencilSolver {
   kernels::PackTarget<T> pack_;  // send == nullptr: the fused pack is off
   T* packed_ = nullptr;
   int last_fused_packs_ = 0;
+  int last_forks_ = 0;
   // Graphs of `chain` consecutive super-steps of size S, one per buffer
   // orientation: g[0] starts from buf_a_, g[1] from buf_b_.
   struct GraphSet {

@@ -555,6 +555,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            "the side stream's hardware-queue check (two-stream schedules)")
       .def("fused_pack", [](SolverHandle& h) { return h.visit([](auto& s) { return s.fused_pack(); }); },
            "whether the passes write the send bands into the exchange's send buffer (SolverConfig::fused_pack)")
+      .def("last_run_forks", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_forks(); }); })
       .def("last_run_fused_packs",
            [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_fused_packs(); }); },
            "exchanges of the last run() whose pack was fused into the preceding pass")

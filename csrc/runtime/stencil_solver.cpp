@@ -547,6 +547,7 @@ void StencilSolver<T>::run(int iters) {
   last_blocks_.clear();
   last_exchanges_ = 0;
   last_fused_packs_ = 0;
+  last_forks_ = 0;
   last_opening_.clear();
   if (iters <= 0) return;
   maybe_stall("run");
@@ -1041,6 +1042,7 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
     (void)hipGetLastError();  // hipErrorNotReady is not an error here
     fork_.record(m);
     fork_.wait_on(side);
+    ++last_forks_;
   }
   if (marks) marks->mark("side:start", side);
   // The inner chunks never take the fused pack: RCCL reads the send buffer

@@ -116,6 +116,7 @@ d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1]); e = d["
 print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["ms_per_step"] * d["steps"], 4),
                   "opening": e.get("opening"), "opening_graph": e.get("opening_graph"),
                   "fused_packs": e.get("timed_fused_packs"), "side_stream": e.get("side_stream"),
+                  "forks": e.get("timed_forks"), "run_host_us": e.get("timed_run_host_us"),
                   "window_sync": e.get("window_sync"), "device_schedule": e.get("device_schedule"),
                   "choice": {k: (e.get("schedule_choice") or {}).get(k) for k in ("opening", "ratio", "ratio_iqr",
                                                                                    "outer_wgs")},
