@@ -364,6 +364,9 @@ def main(argv=None) -> int:
     p.add_argument("--device-schedule", default="auto", choices=["auto", "spin", "yield"],
                    help="hipSetDeviceFlags schedule for host waits (spin: a waiting host thread polls instead of "
                         "yielding; auto: HIP's heuristic, yield on this many-core host)")
+    p.add_argument("--stream-priorities", default="-1,0",
+                   help="HIP priorities of the solver's main (exchange chain) and side streams, 'MAIN,SIDE' "
+                        "(lower = higher priority)")
     p.add_argument("--fused-pack", action="store_true",
                    help="N > 1: the pipeline passes write their send bands into the exchange's send buffer, so "
                         "the exchange after them has no pack launch (default off: measured slower on the 8-GPU-tile "
@@ -432,6 +435,8 @@ def main(argv=None) -> int:
                         direct_halo=("validate" if args.direct_halo == "validate" else None),
                         halo_max_ctas=args.halo_max_ctas, opening_graph=args.opening_graph,
                         fused_pack=args.fused_pack,
+                        main_priority=int(args.stream_priorities.split(",")[0]),
+                        side_priority=int(args.stream_priorities.split(",")[1]),
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     window_sync = args.window_sync

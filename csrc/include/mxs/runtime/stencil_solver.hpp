@@ -199,6 +199,10 @@ struct SolverConfig {
   // periodic super-step (one launch) goes eager past a fifth of this: 8192^2
   // (~130 us passes) 9.79 -> 10.0 T cells/s (profiles/r03_eager). 0 = always graphs.
   double graph_max_superstep_us = 150.0;
+  // HIP stream priorities (lower = higher priority): the main stream carries
+  // the exchange chain, which must not queue behind the side stream's sweep.
+  int main_priority = -1;
+  int side_priority = 0;
 };
 
 template <typename T>

@@ -458,8 +458,11 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
                        py::object bootstrap, int graph_supersteps, bool sum_form, const std::string& direct_halo,
                        double graph_max_superstep_us, const std::string& opening, bool rehearse_peers,
-                       double min_gain, int halo_max_ctas, bool opening_graph, bool fused_pack) {
+                       double min_gain, int halo_max_ctas, bool opening_graph, bool fused_pack,
+                       int main_priority, int side_priority) {
              SolverConfig cfg;
+             cfg.main_priority = main_priority;
+             cfg.side_priority = side_priority;
              cfg.fused_pack = fused_pack;
              cfg.halo_max_ctas = halo_max_ctas;
              cfg.opening_graph = opening_graph;
@@ -504,6 +507,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = "off",
            py::arg("graph_max_superstep_us") = 150.0, py::arg("opening") = "auto", py::arg("rehearse_peers") = false,
            py::arg("min_gain") = 0.03, py::arg("halo_max_ctas") = 0, py::arg("opening_graph") = false, py::arg("fused_pack") = false,
+           py::arg("main_priority") = -1, py::arg("side_priority") = 0,
            py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")

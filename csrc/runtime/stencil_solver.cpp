@@ -34,8 +34,8 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
       cur_(buf_a),
       nxt_(buf_b),
       comm_(comm),
-      main_(true, -1),
-      side_(true, 0) {
+      main_(true, cfg.main_priority),
+      side_(true, cfg.side_priority) {
   // The main stream gets the higher priority (lower number): its short pack /
   // unpack / boundary launches should not queue behind the long interior sweep.
   block_ = cfg_.kind == StencilKind::Jacobi5 ? std::max(1, cfg_.time_block) : 1;
@@ -142,7 +142,7 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
     int tries = 0;
     bool ok = kernels::streams_concurrent(side_.get(), main_.get());
     for (; !ok && tries < 4; ++tries) {
-      spare_streams_.push_back(std::make_unique<Stream>(true, 0));
+      spare_streams_.push_back(std::make_unique<Stream>(true, cfg_.side_priority));
       side_.swap(*spare_streams_.back());
       ok = kernels::streams_concurrent(side_.get(), main_.get());
     }

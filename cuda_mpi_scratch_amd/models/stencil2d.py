@@ -100,6 +100,9 @@ class StencilConfig:
     # exchange's send buffer, so the next exchange is RCCL + unpack. Off by
     # default (measured slower: the pack launch hides the host's RCCL enqueue).
     fused_pack: bool = False
+    # HIP stream priorities of the solver's main (exchange chain) and side streams.
+    main_priority: int = -1
+    side_priority: int = 0
     # Super-steps estimated longer than this run from eager launches, not a
     # hipGraph (long passes: eager measured faster). 0 = always graphs.
     graph_max_superstep_us: float = 150.0
@@ -202,7 +205,8 @@ class Stencil2D:
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
                                           self._direct_mode(backend),
                                           cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain,
-                                          cfg.halo_max_ctas, cfg.opening_graph, cfg.fused_pack)
+                                          cfg.halo_max_ctas, cfg.opening_graph, cfg.fused_pack,
+                                          cfg.main_priority, cfg.side_priority)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
