@@ -93,8 +93,8 @@ task_window() {
       local args=(--global "$tile" --steps "${WINDOW_STEPS:-20}" --warmup 5 --no-extras)
       local base=$mode
       case $base in *-spin) args+=(--device-schedule spin); base=${base%-spin} ;; esac
-      case $base in *-p00) args+=(--stream-priorities 0,0); base=${base%-p00} ;; esac
-      case $base in *-p11) args+=(--stream-priorities -1,-1); base=${base%-p11} ;; esac
+      case $base in *-p00) args+=(--stream-priorities=0,0); base=${base%-p00} ;; esac
+      case $base in *-p11) args+=(--stream-priorities=-1,-1); base=${base%-p11} ;; esac
       case $base in *-tsync) args+=(--window-sync torch); base=${base%-tsync} ;; esac
       case $base in *-ssync) args+=(--window-sync solver); base=${base%-ssync} ;; esac
       case $base in *-fp) args+=(--fused-pack); base=${base%-fp} ;; esac
