@@ -7,7 +7,8 @@ usage: python scripts/exp/opening_probe.py [TILE] [SOLVERS] [REPLICAS]"""
 import json
 import sys
 
-sys.path.insert(0, ".")
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.dirname(
+    __import__("os").path.abspath(__file__)))))
 
 import torch  # noqa: E402
 
@@ -33,14 +34,17 @@ def main() -> int:
         st.run(20)
         st.prepare(20)
         st.warm(20, 0.2)
-    spans = {o: [] for o in sts}
+    reps_ = {o: [] for o in sts}
     for _ in range(reps):
         for o, st in sts.items():
-            p = st.profile_window(20)
-            spans[o].append(p["gpu_span_us"])
-    for o, v in spans.items():
-        v = sorted(v)
-        print(json.dumps({"opening": o, "gpu_span_us_median": v[len(v) // 2], "min": v[0], "max": v[-1]}))
+            reps_[o].append(st.profile_window(20))
+    spans = {o: [p["gpu_span_us"] for p in v] for o, v in reps_.items()}
+    for o, v in reps_.items():
+        v = sorted(v, key=lambda p: p["gpu_span_us"])
+        med = v[len(v) // 2]
+        print(json.dumps({"opening": o, "gpu_span_us_median": med["gpu_span_us"], "min": v[0]["gpu_span_us"],
+                          "max": v[-1]["gpu_span_us"], "median_phases": med["phases_us"],
+                          "outer_wgs": sts[o].solver.schedule_times()["outer_wgs"]}))
     ratio = sorted(a / b for a, b in zip(spans["interior-first"], spans["serial"]))
     print(json.dumps({"paired_ratio_median": round(ratio[len(ratio) // 2], 4), "min": round(ratio[0], 4),
                       "max": round(ratio[-1], 4)}))
