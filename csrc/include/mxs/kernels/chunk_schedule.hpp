@@ -137,6 +137,7 @@ struct HaloLastSchedule {
   std::int64_t hf = 0;
   double inner_cost = 0, outer_cost = 0;  // slowest workgroup (rows + fills) of each set
   double serial_cost = 0;                 // the same pass as one balanced launch
+  std::int64_t moved_rows = 0;            // interior rows the outer launch took over (balance)
 };
 
 namespace detail {
@@ -201,30 +202,92 @@ inline HaloLastSchedule make_halo_last_schedule(std::int64_t groups, std::int64_
   if (inner.empty()) throw std::invalid_argument("make_halo_last_schedule: no interior");
   h.serial_cost = double(detail::runs_cost(all, blocks, fill));
   granule = std::max(1, granule);
+  const double lead = lead_frac * h.serial_cost;
+  // The ghost-ring chunks alone are a small share of a large tile's pass (the
+  // 2-GPU tile 32768 x 16384: 6%; its outer launch ended 445 us before the inner
+  // one, which ran the rest on 7/8 of the CUs and lost to the serial pass,
+  // profiles/r04_op2). So the outer launch also takes interior rows, moved from
+  // the end of the inner set, until the two launches, the outer one started
+  // `lead` late, end together.
+  std::int64_t inner_rows = 0;
+  for (const auto& r : inner) inner_rows += r.r1 - r.r0;
+  auto split = [&](std::int64_t moved, std::vector<detail::Run>* in, std::vector<detail::Run>* out) {
+    *in = inner;
+    *out = outer;
+    while (moved > 0 && !in->empty()) {
+      detail::Run& last = in->back();
+      const std::int64_t take = std::min(moved, last.r1 - last.r0);
+      out->push_back(detail::Run{last.g, last.r1 - take, last.r1});
+      last.r1 -= take;
+      moved -= take;
+      if (last.r1 <= last.r0) in->pop_back();
+    }
+  };
+  // Rows moved for k outer workgroups: the largest amount that keeps the outer
+  // launch's (delayed) end at or before the inner launch's end.
+  auto balance = [&](int k, double* cost) {
+    std::vector<detail::Run> in, out;
+    std::int64_t lo = 0, hi = inner_rows - 1;  // the inner set keeps at least one row
+    auto times = [&](std::int64_t x, double* ci, double* co) {
+      split(x, &in, &out);
+      *ci = double(detail::runs_cost(in, blocks - k, fill));
+      *co = lead + double(detail::runs_cost(out, k, fill));
+    };
+    double ci = 0, co = 0;
+    times(0, &ci, &co);
+    if (co >= ci) {
+      *cost = std::max(ci, co);
+      return std::int64_t(0);
+    }
+    while (lo < hi) {  // largest x with co(x) <= ci(x)
+      const std::int64_t mid = lo + (hi - lo + 1) / 2;
+      times(mid, &ci, &co);
+      (co <= ci ? lo : hi) = co <= ci ? mid : mid - 1;
+    }
+    times(lo, &ci, &co);
+    double best = std::max(ci, co);
+    std::int64_t x = lo;
+    if (lo + 1 < inner_rows) {  // one row past the crossing may be the better side
+      double ci2 = 0, co2 = 0;
+      times(lo + 1, &ci2, &co2);
+      if (std::max(ci2, co2) < best) {
+        best = std::max(ci2, co2);
+        x = lo + 1;
+      }
+    }
+    *cost = best;
+    return x;
+  };
   int m = outer_wgs;
+  std::int64_t moved = 0;
   if (m <= 0) {
-    // The smallest outer set whose (delayed) finish does not trail the inner set,
-    // and no fewer than min_outer: the exchange's kernels run on the CUs the
-    // inner launch leaves free (RCCL's p2p kernel starved on 8-16 free CUs and
-    // finished only with the inner launch, profiles/r03_halolast).
-    const double lead = lead_frac * h.serial_cost;
+    // The outer set with the earliest common end, no fewer than min_outer
+    // workgroups: the exchange's kernels run on the CUs the inner launch leaves
+    // free (RCCL's p2p kernel starved on 8-16 free CUs and finished only with
+    // the inner launch, profiles/r03_halolast).
     double best = 1e300;
     const int k0 = std::max(granule, (std::max(1, min_outer) + granule - 1) / granule * granule);
     for (int k = k0; k < blocks; k += granule) {
-      const double ci = double(detail::runs_cost(inner, blocks - k, fill));
-      const double co = lead + double(detail::runs_cost(outer, k, fill));
-      const double t = std::max(ci, co);
-      if (t < best) {
+      double t = 0;
+      const std::int64_t x = balance(k, &t);
+      if (t < best - 1e-9) {
         best = t;
         m = k;
+        moved = x;
       }
-      if (co <= ci) break;  // more outer workgroups only slow the inner set
     }
   }
   if (m <= 0) m = std::max(granule, min_outer);
   m = std::min(std::max(m, 1), blocks - 1);
-  h.inner = detail::partition_runs(inner, blocks - m, fill, &h.inner_cost);
-  h.outer = detail::partition_runs(outer, m, fill, &h.outer_cost);
+  if (outer_wgs > 0) {
+    double t = 0;
+    moved = balance(m, &t);
+  }
+  std::vector<detail::Run> in, out;
+  split(moved, &in, &out);
+  h.moved_rows = moved;
+  h.inner = detail::partition_runs(in, blocks - m, fill, &h.inner_cost);
+  h.outer = detail::partition_runs(out, m, fill, &h.outer_cost);
   return h;
 }
 

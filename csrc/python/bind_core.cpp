@@ -208,6 +208,7 @@ PYBIND11_MODULE(_mxs_core, m) {
         d["inner_cost"] = h.inner_cost;
         d["outer_cost"] = h.outer_cost;
         d["serial_cost"] = h.serial_cost;
+        d["moved_rows"] = h.moved_rows;
         d["check"] = kernels::check_halo_last_schedule(h, groups, rows, depth, ghost);
         return d;
       },

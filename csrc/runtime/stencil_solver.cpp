@@ -950,12 +950,18 @@ std::unique_ptr<typename StencilSolver<T>::HaloLastPass> StencilSolver<T>::build
     const char* e = experiment_env(k);
     return e ? std::atof(e) : dflt;
   };
+  // The exchange's delay of the outer launch as a share of the pass: on the
+  // one-GPU rehearsal the outer chunks started 44-71 us after the inner ones on
+  // every tile (pack, RCCL, unpack beside the inner launch; profiles/r04_op2),
+  // a fixed cost, so its share falls with the tile's area (est. ~10 T cell-steps/s).
+  const double est_pass_us = double(tile_.width) * double(tile_.height) * S / 10e6;
+  const double lead_frac = std::min(0.35, std::max(0.03, 60.0 / std::max(est_pass_us, 1.0)));
   auto hl = std::make_unique<HaloLastPass>();
   hl->S = S;
   try {
     hl->sched = kernels::make_halo_last_schedule(shape.groups, tile_.height, shape.blocks, shape.fill, S, ghost,
                                                  outer_wgs > 0 ? outer_wgs : int(env_num("MXS_HALO_LAST_WGS", 0)),
-                                                 env_num("MXS_HALO_LAST_LEAD", 0.12),
+                                                 env_num("MXS_HALO_LAST_LEAD", lead_frac),
                                                  std::int64_t(env_num("MXS_HALO_LAST_ROWS", 0)),
                                                  shape.blocks % kXcds == 0 ? kXcds : 1,
                                                  int(env_num("MXS_HALO_LAST_MIN_WGS", 32)));

@@ -83,6 +83,22 @@ def test_halo_last_schedule_8gpu_tile_balance():
     assert d["outer_cost"] + 0.12 * d["serial_cost"] <= 1.04 * d["inner_cost"]
 
 
+@pytest.mark.parametrize("groups,rows,fill,lead", [(36, 16384, 66, 0.056), (18, 16384, 52, 0.11),
+                                                   (18, 8192, 40, 0.22)])
+def test_halo_last_schedule_balances_large_tiles(groups, rows, fill, lead):
+    """The 2-, 4- and 8-GPU tiles with the solver's lead model: the outer launch
+    takes interior rows when the ghost-ring chunks alone would end early (the
+    2-GPU tile's outer set is ~6% of the pass), so both launches end together
+    and the inner set costs at most ~2% more than the one-launch pass."""
+    d = C.halo_last_schedule(groups, rows, 256, fill, 20, _ghost(groups), lead_frac=lead, granule=8, min_outer=32)
+    assert d["check"] == ""
+    lead_cost = lead * d["serial_cost"]
+    assert abs((d["outer_cost"] + lead_cost) - d["inner_cost"]) <= 0.03 * d["inner_cost"], d["moved_rows"]
+    assert d["inner_cost"] <= 1.02 * d["serial_cost"] + lead_cost
+    if groups == 36:
+        assert d["moved_rows"] > 0  # the ghost-ring chunks alone would leave the outer CUs idle
+
+
 def test_halo_last_schedule_xcd_granule():
     """Both launches in multiples of the 8 XCDs (the solver's setting)."""
     d = C.halo_last_schedule(18, 8192, 256, 40, 20, _ghost(18), granule=8)
