@@ -700,6 +700,29 @@ void StencilSolver<T>::choose_opening(int S) {
     return std::max(double(e1.since(e0)), double(e2.since(e0)));
   };
   constexpr int kCands = 3, kReps = 21;  // round 0 warms every shape (20 paired rounds: the notch is 1.58 IQR / sqrt(20))
+  std::vector<double> t_serial;
+  std::vector<std::vector<double>> t_cand(kCands), ratio(kCands);
+  for (int rep = 0; rep < kReps; ++rep) {
+    const double serial = timed(false, [&] {
+      prime_exchange();
+      enqueue_bare_pass(cur_, nxt_, S);
+    });
+    if (rep > 0) t_serial.push_back(serial);
+    for (size_t c = 0; c < size_t(kCands); ++c) {
+      const double ms = timed(c < cands.size(), [&] {
+        if (c < cands.size()) {
+          enqueue_halo_last(cur_, nxt_, cands[c]);
+        } else {
+          prime_exchange();
+          enqueue_bare_pass(cur_, nxt_, S);
+        }
+      });
+      if (rep > 0 && c < cands.size()) {
+        t_cand[c].push_back(ms);
+        ratio[c].push_back(ms / std::max(serial, 1e-9));  // paired with this round's serial sample
+      }
+    }
+  }
   // The decision rests on the paired ratios (candidate / serial of the same
   // round): the clock drifts between rounds by far more than the openings
   // differ (IQR of either series alone 11% of a 0.29 ms opening on one box),
@@ -708,63 +731,13 @@ void StencilSolver<T>::choose_opening(int S) {
   // ratio is at most 1 - min_gain and its notch (median + 1.58 IQR / sqrt(n),
   // the 95% interval of a median) stays below 1.
   constexpr double kMissing = 1e30;
-  std::vector<std::vector<double>> ratio(kCands);
-  std::vector<double> v;
-  auto measure = [&] {
-    std::vector<double> t_serial;
-    std::vector<std::vector<double>> t_cand(kCands);
-    for (auto& r : ratio) r.clear();
-    for (int rep = 0; rep < kReps; ++rep) {
-      const double serial = timed(false, [&] {
-        prime_exchange();
-        enqueue_bare_pass(cur_, nxt_, S);
-      });
-      if (rep > 0) t_serial.push_back(serial);
-      for (size_t c = 0; c < size_t(kCands); ++c) {
-        const double ms = timed(c < cands.size(), [&] {
-          if (c < cands.size()) {
-            enqueue_halo_last(cur_, nxt_, cands[c]);
-          } else {
-            prime_exchange();
-            enqueue_bare_pass(cur_, nxt_, S);
-          }
-        });
-        if (rep > 0 && c < cands.size()) {
-          t_cand[c].push_back(ms);
-          ratio[c].push_back(ms / std::max(serial, 1e-9));  // paired with this round's serial sample
-        }
-      }
-    }
-    v.assign(4 * kCands + 2, kMissing);
-    std::tie(v[0], v[1]) = median_iqr(t_serial);
-    for (size_t c = 0; c < cands.size(); ++c) {
-      v[2 + c] = median_iqr(t_cand[c]).first;
-      std::tie(v[2 + kCands + c], v[2 + 2 * kCands + c]) = median_iqr(ratio[c]);
-    }
-    agree_max(v, "prepare: opening agreement");
-  };
-  measure();
-  // Interior-first slower than serial on the worst rank although both launches
-  // end together by construction: the state seen in some solvers of a process
-  // (ratios 1.03-1.05 while other solvers of the same process measured 0.92,
-  // profiles/r04_bal). Once, on every rank alike (the condition is agreed): a
-  // fresh side stream, and measure again.
-  double first_ratio = 0;
-  {
-    double lo = kMissing;
-    for (size_t c = 0; c < size_t(kCands); ++c) lo = std::min(lo, v[2 + kCands + c]);
-    if (lo < kMissing && lo > 1.0) {
-      first_ratio = lo;
-      join_side();
-      wait_idle("prepare: opening timing");
-      auto fresh = std::make_unique<Stream>(true, cfg_.side_priority);
-      if (kernels::streams_concurrent(fresh->get(), main_.get())) {
-        side_.swap(*fresh);
-        spare_streams_.push_back(std::move(fresh));
-      }
-      measure();
-    }
+  std::vector<double> v(4 * kCands + 2, kMissing);
+  std::tie(v[0], v[1]) = median_iqr(t_serial);
+  for (size_t c = 0; c < cands.size(); ++c) {
+    v[2 + c] = median_iqr(t_cand[c]).first;
+    std::tie(v[2 + kCands + c], v[2 + 2 * kCands + c]) = median_iqr(ratio[c]);
   }
+  agree_max(v, "prepare: opening agreement");
   // The candidate with the lowest notch (median + 1.58 IQR / sqrt(n)): a
   // consistent 0.94 beats a median of 0.93 whose rounds spread to 1.2 (the
   // outer set one XCD step above the model's measured that way, 4 solvers on
@@ -793,7 +766,7 @@ void StencilSolver<T>::choose_opening(int S) {
   }
   halo_last_on_ = win;
   opening_choice_ = win ? "interior-first" : "serial";
-  char buf[480];
+  char buf[320];
   if (r >= kMissing) {
     std::snprintf(buf, sizeof(buf), "no rank-wide interior-first candidate (serial median %.4f ms)", serial);
   } else {
@@ -802,11 +775,6 @@ void StencilSolver<T>::choose_opening(int S) {
                   "IQR %.3f, notch %.3f (switch at <= %.3f with notch < 1); medians %.4f / %.4f ms: %s",
                   n, r, r_iqr, notch, 1.0 - cfg_.min_gain, hlt, serial,
                   win ? "interior-first" : "serial kept");
-    if (first_ratio > 0) {
-      const std::string b(buf);
-      std::snprintf(buf, sizeof(buf), "%s (measured again with a fresh side stream: the first best ratio was %.3f)",
-                    b.c_str(), first_ratio);
-    }
   }
   opening_reason_ = buf;
 }
