@@ -137,6 +137,7 @@ struct HaloLastSchedule {
   std::int64_t hf = 0;
   double inner_cost = 0, outer_cost = 0;  // slowest workgroup (rows + fills) of each set
   double serial_cost = 0;                 // the same pass as one balanced launch
+  std::int64_t band = 0;                  // rows per band of the outer set (>= hf: balance)
   std::int64_t moved_rows = 0;            // interior rows the outer launch took over (balance)
 };
 
@@ -187,17 +188,11 @@ inline HaloLastSchedule make_halo_last_schedule(std::int64_t groups, std::int64_
     throw std::invalid_argument("make_halo_last_schedule: bad shape");
   HaloLastSchedule h;
   h.hf = std::max(depth, band_rows);
-  std::vector<detail::Run> inner, outer, all;
+  std::vector<detail::Run> inner, all;  // inner: the interior at the minimal band depth hf
   for (std::int64_t g = 0; g < groups; ++g) {
     const auto gi = std::int32_t(g);
     all.push_back(detail::Run{gi, 0, rows});
-    if (ghost_group[size_t(g)] || rows <= 2 * h.hf) {
-      outer.push_back(detail::Run{gi, 0, rows});
-    } else {
-      outer.push_back(detail::Run{gi, 0, h.hf});
-      outer.push_back(detail::Run{gi, rows - h.hf, rows});
-      inner.push_back(detail::Run{gi, h.hf, rows - h.hf});
-    }
+    if (!ghost_group[size_t(g)] && rows > 2 * h.hf) inner.push_back(detail::Run{gi, h.hf, rows - h.hf});
   }
   if (inner.empty()) throw std::invalid_argument("make_halo_last_schedule: no interior");
   h.serial_cost = double(detail::runs_cost(all, blocks, fill));
@@ -206,60 +201,64 @@ inline HaloLastSchedule make_halo_last_schedule(std::int64_t groups, std::int64_
   // The ghost-ring chunks alone are a small share of a large tile's pass (the
   // 2-GPU tile 32768 x 16384: 6%; its outer launch ended 445 us before the inner
   // one, which ran the rest on 7/8 of the CUs and lost to the serial pass,
-  // profiles/r04_op2). So the outer launch also takes interior rows, moved from
-  // the end of the inner set, until the two launches, the outer one started
-  // `lead` late, end together.
-  std::int64_t inner_rows = 0;
-  for (const auto& r : inner) inner_rows += r.r1 - r.r0;
-  auto split = [&](std::int64_t moved, std::vector<detail::Run>* in, std::vector<detail::Run>* out) {
-    *in = inner;
-    *out = outer;
-    while (moved > 0 && !in->empty()) {
-      detail::Run& last = in->back();
-      const std::int64_t take = std::min(moved, last.r1 - last.r0);
-      out->push_back(detail::Run{last.g, last.r1 - take, last.r1});
-      last.r1 -= take;
-      moved -= take;
-      if (last.r1 <= last.r0) in->pop_back();
+  // profiles/r04_bal). So the outer launch takes deeper bands: rows [0, b) and
+  // [rows - b, rows) of every non-edge group, b >= hf, until the two launches,
+  // the outer one started `lead` late, end together. Deeper bands rather than
+  // rows from elsewhere: a band chunk is one chunk either way, so its pipeline
+  // fill is spread over more rows, and every inner run stays one run.
+  const std::int64_t max_band = rows / 2 - 1;  // every inner run keeps >= 2 rows
+  auto split = [&](std::int64_t band, std::vector<detail::Run>* in, std::vector<detail::Run>* out) {
+    in->clear();
+    out->clear();
+    for (std::int64_t g = 0; g < groups; ++g) {
+      const auto gi = std::int32_t(g);
+      if (ghost_group[size_t(g)] || rows <= 2 * h.hf) {
+        out->push_back(detail::Run{gi, 0, rows});
+      } else {
+        out->push_back(detail::Run{gi, 0, band});
+        out->push_back(detail::Run{gi, rows - band, rows});
+        in->push_back(detail::Run{gi, band, rows - band});
+      }
     }
   };
-  // Rows moved for k outer workgroups: the largest amount that keeps the outer
-  // launch's (delayed) end at or before the inner launch's end.
+  // Band depth for k outer workgroups: the deepest that keeps the outer
+  // launch's (delayed) end at or before the inner launch's end (or one row more).
   auto balance = [&](int k, double* cost) {
     std::vector<detail::Run> in, out;
-    std::int64_t lo = 0, hi = inner_rows - 1;  // the inner set keeps at least one row
-    auto times = [&](std::int64_t x, double* ci, double* co) {
-      split(x, &in, &out);
+    auto times = [&](std::int64_t bd, double* ci, double* co) {
+      split(bd, &in, &out);
       *ci = double(detail::runs_cost(in, blocks - k, fill));
       *co = lead + double(detail::runs_cost(out, k, fill));
     };
     double ci = 0, co = 0;
-    times(0, &ci, &co);
-    if (co >= ci) {
+    times(h.hf, &ci, &co);
+    if (co >= ci || max_band <= h.hf) {
       *cost = std::max(ci, co);
-      return std::int64_t(0);
+      return h.hf;
     }
-    while (lo < hi) {  // largest x with co(x) <= ci(x)
+    std::int64_t lo = h.hf, hi = max_band;
+    while (lo < hi) {  // deepest band with co <= ci
       const std::int64_t mid = lo + (hi - lo + 1) / 2;
       times(mid, &ci, &co);
-      (co <= ci ? lo : hi) = co <= ci ? mid : mid - 1;
+      if (co <= ci) lo = mid;
+      else hi = mid - 1;
     }
     times(lo, &ci, &co);
     double best = std::max(ci, co);
-    std::int64_t x = lo;
-    if (lo + 1 < inner_rows) {  // one row past the crossing may be the better side
+    std::int64_t bd = lo;
+    if (lo + 1 <= max_band) {
       double ci2 = 0, co2 = 0;
       times(lo + 1, &ci2, &co2);
       if (std::max(ci2, co2) < best) {
         best = std::max(ci2, co2);
-        x = lo + 1;
+        bd = lo + 1;
       }
     }
     *cost = best;
-    return x;
+    return bd;
   };
   int m = outer_wgs;
-  std::int64_t moved = 0;
+  std::int64_t band = h.hf;
   if (m <= 0) {
     // The outer set with the earliest common end, no fewer than min_outer
     // workgroups: the exchange's kernels run on the CUs the inner launch leaves
@@ -269,11 +268,11 @@ inline HaloLastSchedule make_halo_last_schedule(std::int64_t groups, std::int64_
     const int k0 = std::max(granule, (std::max(1, min_outer) + granule - 1) / granule * granule);
     for (int k = k0; k < blocks; k += granule) {
       double t = 0;
-      const std::int64_t x = balance(k, &t);
+      const std::int64_t bd = balance(k, &t);
       if (t < best - 1e-9) {
         best = t;
         m = k;
-        moved = x;
+        band = bd;
       }
     }
   }
@@ -281,11 +280,14 @@ inline HaloLastSchedule make_halo_last_schedule(std::int64_t groups, std::int64_
   m = std::min(std::max(m, 1), blocks - 1);
   if (outer_wgs > 0) {
     double t = 0;
-    moved = balance(m, &t);
+    band = balance(m, &t);
   }
   std::vector<detail::Run> in, out;
-  split(moved, &in, &out);
-  h.moved_rows = moved;
+  split(band, &in, &out);
+  h.band = band;
+  h.moved_rows = 0;
+  for (const auto& r : in) h.moved_rows -= r.r1 - r.r0;
+  for (const auto& r : inner) h.moved_rows += r.r1 - r.r0;
   h.inner = detail::partition_runs(in, blocks - m, fill, &h.inner_cost);
   h.outer = detail::partition_runs(out, m, fill, &h.outer_cost);
   return h;

@@ -209,6 +209,7 @@ PYBIND11_MODULE(_mxs_core, m) {
         d["outer_cost"] = h.outer_cost;
         d["serial_cost"] = h.serial_cost;
         d["moved_rows"] = h.moved_rows;
+        d["band"] = h.band;
         d["check"] = kernels::check_halo_last_schedule(h, groups, rows, depth, ghost);
         return d;
       },
