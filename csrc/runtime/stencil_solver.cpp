@@ -1311,7 +1311,6 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
   split(iters, gr);
   const int S = gr[0].count > 0 ? gr[0].S : gr[1].S;
   const int supersteps = gr[0].count + gr[1].count;
-  const index_t w = tile_.width, h = tile_.height;
   hipStream_t m = main_.get();
   if (direct_on_ || (!fused_ && !post_exchange())) {
     out.opening = direct_on_ ? "direct (not profiled)" : "overlap (not profiled)";
