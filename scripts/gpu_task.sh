@@ -148,6 +148,29 @@ task_final() {
   task_prof driver --steps 20 --warmup 5
 }
 
+task_warmab() {  # REPS: the driver's N = 1 command with clock warm-up 200 ms (default) vs 1000 ms, interleaved
+  local reps=${1:-6}
+  : > "$OUT/warmab.jsonl"
+  for i in $(seq "$reps"); do
+    for w in 200 1000; do
+      timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-extras --clock-warmup-ms "$w" > "$OUT/warm_last.txt" 2>&1 || {
+        echo "bench failed"; tail -20 "$OUT/warm_last.txt"; exit 1; }
+      python - "$OUT/warm_last.txt" "$w" >> "$OUT/warmab.jsonl" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+print(json.dumps({"warm_ms": int(sys.argv[2]), "value": d["value"], "span_us": d["extras"]["window_phases"]["gpu_span_us"]}))
+PY
+    done
+  done
+  python - "$OUT/warmab.jsonl" <<'PY'
+import json, sys
+rs = [json.loads(l) for l in open(sys.argv[1])]
+for w in (200, 1000):
+    v = sorted(r["value"] for r in rs if r["warm_ms"] == w)
+    print(w, "median", v[len(v) // 2], "min", v[0], "max", v[-1])
+PY
+}
+
 case "$TASK" in
   tests) task_tests "$@" ;;
   smoke) task_smoke ;;
@@ -156,5 +179,6 @@ case "$TASK" in
   window) task_window "$@" ;;
   py) task_py "$@" ;;
   final) task_final ;;
+  warmab) task_warmab "$@" ;;
   *) echo "unknown task '$TASK'"; exit 2 ;;
 esac
