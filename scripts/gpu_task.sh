@@ -104,6 +104,7 @@ task_window() {
         ifirst) args+=(--loopback --rehearse-peers --opening interior-first) ;;
         graph) args+=(--loopback --rehearse-peers --opening interior-first --opening-graph) ;;
         sgraph) args+=(--loopback --rehearse-peers --opening serial --opening-graph) ;;
+        agraph) args+=(--loopback --rehearse-peers --opening-graph) ;;
         fused) ;;
         *) echo "unknown window mode '$mode'"; exit 2 ;;
       esac
