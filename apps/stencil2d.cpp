@@ -23,12 +23,9 @@
 // More options: --local WxH | --global WxH, --dims RxC, --stencil-height H, --dtype f32|f64,
 // --iters N, --warmup N, --time-block S (default: measured per tile size and dtype), --no-overlap, --no-graph,
 // --opening auto|serial|interior-first (--halo-last = interior-first; default auto: prepare() times the
-// serial and interior-first openings, agrees the worst-rank medians over all ranks and keeps the faster),
+// serial and interior-first openings, agrees the per-round maxima over all ranks and keeps the faster),
 // --no-direct-halo (IPC backend: pack -> put -> unpack instead of the device-initiated push),
 // --halo-max-ctas N (RCCL: the halo exchange on a communicator split off with at most N workgroups per kernel),
-// --fused-pack (the pipeline passes write their send bands into the send buffer: no pack launch before the
-// exchange after them; off by default, measured slower),
-// --opening-graph (the interior-first opening's pack/RCCL/unpack/outer chain replayed from a hipGraph),
 // --direct-halo on|off|validate (validate: prepare() compares the push with the backend's exchange bitwise on
 // every rank, times both, and uses it only if equal everywhere and faster),
 // --c-center C --c-neighbor C (default 0.2 / 0.2), --no-sum-form (keep the per-step evaluation in the
@@ -145,8 +142,6 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
             "--opening must be auto, serial or interior-first, got " << opening);
   cfg.opening = opening == "serial" ? Opening::Serial : opening == "interior-first" ? Opening::InteriorFirst : Opening::Auto;
   cfg.halo_max_ctas = int(cli.get_int("halo-max-ctas", 0));  // RCCL: the halo on a CTA-capped communicator
-  cfg.fused_pack = cli.flag("fused-pack");  // the pipeline passes write the send bands (exchange = wire + unpack)
-  cfg.opening_graph = cli.flag("opening-graph");
   cfg.loopback_self = loopback;
   cfg.coeffs = {c_center, c_neighbor, sum_form};
   cfg.time_block = time_block;
@@ -269,7 +264,6 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
         js << ", \"interior_first_opening\": " << (solver->halo_last(solver->time_block()) ? "true" : "false");
         if (!solver->opening_choice().empty()) js << ", \"opening_choice\": \"" << solver->opening_choice() << "\"";
         js << ", \"last_opening\": \"" << solver->last_run_opening() << "\"";
-        js << ", \"fused_packs\": " << solver->last_run_fused_packs();
         if (!solver->direct_state().empty()) js << ", \"direct_halo\": \"" << solver->direct_state() << "\"";
       }
       if (want_sum) js << ", \"checksum\": " << app::fmt(checksum);

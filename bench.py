@@ -44,7 +44,7 @@ one of the K steps runs in full inside the window.
 
 Self-description (extras): the executed super-steps and exchanges (``halo``,
 ``timed_super_steps``, ``timed_exchanges``), the opening prepare() chose and
-the worst-rank timings it agreed on (``schedule_choice``), the RCCL
+the per-round maxima over ranks it decided on (``schedule_choice``), the RCCL
 communicator's own rank count and every rank's device (``rccl_ranks``,
 ``rank_devices``), an event-timed phase breakdown of one untimed replica of the
 window (``window_phases``: pack / RCCL / unpack / passes / host overhead), and
@@ -351,9 +351,9 @@ def main(argv=None) -> int:
     p.add_argument("--halo-max-ctas", type=int, default=0,
                    help="N > 1: the halo exchange on an RCCL communicator split off with at most this many "
                         "workgroups per kernel (0 = RCCL's default)")
-    p.add_argument("--opening-graph", action="store_true",
-                   help="N > 1: replay the interior-first opening's main-stream chain (pack, RCCL, unpack, outer "
-                        "chunks) from a hipGraph captured in prepare()")
+    p.add_argument("--wire-delay-us", type=float, default=0.0,
+                   help="with --loopback --rehearse-peers: a single-wave kernel holds the stream this long after "
+                        "every RCCL transfer, standing in for xGMI wire time (one-GPU rehearsal only)")
     p.add_argument("--window-sync", default="auto", choices=["auto", "solver", "torch"],
                    help="how the timed window ends: torch = torch.cuda.synchronize() alone, under a timer-thread "
                         "watchdog that aborts the halo's RCCL communicators past --comm-timeout; solver = "
@@ -361,16 +361,9 @@ def main(argv=None) -> int:
                         "torch.cuda.synchronize(); auto (default): torch for a solver without a communicator (the "
                         "1-GPU fused tile: 8-20 us less per window), solver otherwise (with two streams in flight "
                         "the device sync alone returned ~0.2 ms late in 2-4 of 16 windows; profiles/r04_sync)")
-    p.add_argument("--device-schedule", default="auto", choices=["auto", "spin", "yield"],
-                   help="hipSetDeviceFlags schedule for host waits (spin: a waiting host thread polls instead of "
-                        "yielding; auto: HIP's heuristic, yield on this many-core host)")
     p.add_argument("--stream-priorities", default="-1,0",
                    help="HIP priorities of the solver's main (exchange chain) and side streams, 'MAIN,SIDE' "
                         "(lower = higher priority)")
-    p.add_argument("--fused-pack", action="store_true",
-                   help="N > 1: the pipeline passes write their send bands into the exchange's send buffer, so "
-                        "the exchange after them has no pack launch (default off: measured slower on the 8-GPU-tile "
-                        "window, profiles/r04_fp)")
     p.add_argument("--direct-halo", default="off", choices=["off", "validate"],
                    help="N > 1: validate: prepare() compares the device-initiated push of the edge bands into the "
                         "neighbours' tiles (HIP IPC over xGMI) bitwise with the RCCL exchange on every rank and times "
@@ -407,18 +400,16 @@ def main(argv=None) -> int:
             return 3
     if args.rehearse_peers and not args.loopback:
         p.error("--rehearse-peers needs --loopback")
+    if args.wire_delay_us and not (args.loopback and args.rehearse_peers):
+        p.error("--wire-delay-us is a one-GPU rehearsal option: it needs --loopback --rehearse-peers")
     ctx = dist_init(backend="nccl" if gpu else "gloo", timeout_s=max(60, int(args.comm_timeout) + 60))
     n = ctx.world_size
     if n != args.gpus and ctx.is_root:
         print(f"warning: --gpus {args.gpus} but world size {n}", file=sys.stderr)
-    device_schedule = None
     if gpu:
         from cuda_mpi_scratch_amd import hip
 
         hip().set_comm_timeout(args.comm_timeout)  # RCCL / IPC waits fail instead of hanging
-        if args.device_schedule != "auto":
-            err, flags = hip().set_device_schedule(args.device_schedule)
-            device_schedule = {"mode": args.device_schedule, "result": err, "flags": int(flags)}
     # Default process grid: MPI_Dims_create order (rows >= cols; 8 -> 4 rows x 2
     # columns). Each rank's tile is then wider than tall (16384 x 8192 on 8
     # GPUs): the row-streaming kernel runs 7.5% faster on it than on
@@ -433,8 +424,7 @@ def main(argv=None) -> int:
                         variant=args.variant, time_block=args.time_block, loopback=args.loopback,
                         sum_form=not args.no_sum_form, opening=args.opening, rehearse_peers=args.rehearse_peers,
                         direct_halo=("validate" if args.direct_halo == "validate" else None),
-                        halo_max_ctas=args.halo_max_ctas, opening_graph=args.opening_graph,
-                        fused_pack=args.fused_pack,
+                        halo_max_ctas=args.halo_max_ctas, wire_delay_us=args.wire_delay_us,
                         main_priority=int(args.stream_priorities.split(",")[0]),
                         side_priority=int(args.stream_priorities.split(",")[1]),
                         fuse_periodic=not args.no_fuse_periodic)
@@ -461,7 +451,6 @@ def main(argv=None) -> int:
                                    if sum_used else "per step: fma(c_n, (n+s)+(w+e), c_c*c)"),
                     "clock_warmup_ms": args.clock_warmup_ms,
                     "window_sync": window_sync,
-                    **({"device_schedule": device_schedule} if device_schedule else {}),
                     "tile": f"{st.decomp.width}x{st.decomp.height}",
                     "process_grid": f"{rows} rows x {cols} cols of ranks",
                     "env": env}
@@ -477,8 +466,10 @@ def main(argv=None) -> int:
         extras["pipe_balanced_shares"] = bool(H.pipe_balanced())
         if st.solver is not None:
             extras["opening"] = st.solver.last_run_opening()
-            if args.opening_graph:
-                extras["opening_graph"] = st.solver.opening_graph_state()
+            # How the ranks agreed on the time block, the opening and the sum-form range.
+            extras["agreement"] = st.solver.agreement_path()
+            if args.wire_delay_us:
+                extras["rehearsed_wire_delay_us"] = args.wire_delay_us
             if args.halo_max_ctas:
                 extras["halo_max_ctas"] = int(st.solver.halo_max_ctas())
                 if st.solver.halo_comm_note():
@@ -489,13 +480,10 @@ def main(argv=None) -> int:
                 # Halo exchanges inside the timed window: one per super-step (with
                 # peers the call primes and ends on a bare pass).
                 extras["timed_exchanges"] = int(st.solver.last_run_exchanges())
-                # Of those, the exchanges whose pack the preceding pass wrote (fused pack).
-                extras["timed_fused_packs"] = int(st.solver.last_run_fused_packs())
                 extras["timed_forks"] = int(st.solver.last_run_forks())
                 extras["timed_run_host_us"] = round(getattr(st, "timed_host_us", 0.0), 1)
                 if st.solver.stream_note():
                     extras["side_stream"] = st.solver.stream_note()
-                extras["fused_pack"] = bool(st.solver.fused_pack())
                 extras["schedule_choice"] = {k: (round(v, 4) if isinstance(v, float) else v)
                                              for k, v in st.solver.schedule_times().items()}
         # Who ran: the RCCL communicator's own view (not the launcher's) and every rank's device.

@@ -71,14 +71,6 @@ class HaloExchanger {
   void pack(T* tile, hipStream_t stream);
   void transfer(hipStream_t stream);
   void unpack(T* tile, hipStream_t stream);
-  // An exchange whose send buffer already holds the tile's bands (a pipeline
-  // pass with the fused pack wrote them): transfer + unpack.
-  void exchange_packed(T* tile, hipStream_t stream);
-  // The plan's send windows in core coordinates of tile `g`, for the fused
-  // pack (kernels::PackSegs); false when the plan cannot take it: no remote
-  // peers, self copies (they stay in the pack launch), more than
-  // kernels::kMaxPackSegs windows.
-  bool pack_windows(const TileGeom& g, kernels::PackSegs* out) const;
 
   const HaloPlan& plan() const { return plan_; }
   HaloBackend backend() const { return backend_; }
@@ -93,6 +85,11 @@ class HaloExchanger {
   void set_copy_block(int threads) { copy_block_ = threads; }
   // Workgroups per copy segment (0 = sized from the segments, or MXS_HALO_GRID).
   void set_copy_grid(int wgs) { copy_grid_ = wgs; }
+  // Rehearsal of wire time on one GPU (RCCL loopback): every transfer() is
+  // followed by a one-workgroup kernel that holds the stream for `us`
+  // microseconds, so the exchange takes as long as an xGMI transfer would.
+  void set_wire_delay_us(double us) { wire_delay_us_ = us; }
+  double wire_delay_us() const { return wire_delay_us_; }
 
  private:
   HaloPlan plan_;
@@ -103,6 +100,7 @@ class HaloExchanger {
   std::unique_ptr<IpcHaloTransport<T>> ipc_;
   int copy_block_ = 0;
   int copy_grid_ = 0;
+  double wire_delay_us_ = 0;
 };
 
 }  // namespace mxs

@@ -122,26 +122,4 @@ inline HaloPlan make_halo_plan(const CartTopology& topo, int rank, const TileGeo
   return plan;
 }
 
-// The send windows of a plan in core coordinates of its tile, with each one's
-// element offset in the packed send buffer (row-major, `w` elements per row):
-// what a pass that writes its send bands straight into the buffer (the fused
-// pack) needs. Empty when the plan has self copies (they stay in the pack
-// launch) or no remote peer.
-struct SendWindow {
-  index_t x0 = 0, y0 = 0, w = 0, h = 0, off = 0;
-};
-inline std::vector<SendWindow> send_windows(const HaloPlan& plan) {
-  std::vector<SendWindow> out;
-  if (plan.sends.empty() || !plan.self_copies.empty()) return out;
-  const Array2D core = plan.tile.core();
-  for (const auto& m : plan.sends)
-    for (const auto& seg : m.segments) {
-      if (seg.region.empty()) continue;
-      if (seg.region.row_stride != plan.tile.pitch) return {};
-      out.push_back(SendWindow{seg.region.x_offset - core.x_offset, seg.region.y_offset - core.y_offset,
-                               seg.region.width, seg.region.height, seg.offset});
-    }
-  return out;
-}
-
 }  // namespace mxs

@@ -130,44 +130,9 @@ template <typename T>
 constexpr bool stencil5_deep_supported(int steps, index_t x0, index_t x1) {
   return steps <= kMaxTimeBlock || (steps <= kMaxTimeBlockDeep && sizeof(T) == 4 && x0 % 4 == 0 && x1 % 4 == 0);
 }
-// Fused halo pack: a pipeline pass over a ghost-ring tile also copies the
-// cells it stores inside the send windows of the halo plan into the packed send
-// buffer (each workgroup, after its last chunk, re-reads the cells it stored
-// from L2), so the next exchange of its output is transfer + unpack only.
-// Windows in core coordinates; x0, w and off multiples of 16 / sizeof(T).
-constexpr int kMaxPackSegs = 8;
-struct PackSeg {
-  index_t x0 = 0, y0 = 0, w = 0, h = 0;
-  index_t off = 0;  // element offset of the window's first cell in the send buffer (row-major, w per row)
-};
-struct PackSegs {
-  int n = 0;
-  PackSeg seg[kMaxPackSegs];
-};
-template <typename T>
-struct PackTarget {
-  T* send = nullptr;
-  PackSegs segs;
-  bool applied = false;  // set by the launcher when the pass took it (a pipeline form, no wrap)
-};
-// Whether the windows can take the fused pack on tile g (whole 16-byte vectors, inside the core).
-template <typename T>
-inline bool pack_segs_ok(const TileGeom& g, const PackSegs& p) {
-  constexpr index_t N = 16 / index_t(sizeof(T));
-  if (p.n <= 0 || p.n > kMaxPackSegs) return false;
-  for (int k = 0; k < p.n; ++k) {
-    const PackSeg& q = p.seg[k];
-    if (q.x0 % N || q.w % N || q.off % N || q.w <= 0 || q.h <= 0 || q.x0 < 0 || q.y0 < 0 || q.x0 + q.w > g.width ||
-        q.y0 + q.h > g.height)
-      return false;
-  }
-  return g.pitch % N == 0 && g.core_offset() % N == 0;
-}
-
 template <typename T>
 void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0, index_t y1,
-                 Stencil5Coeffs c, bool wrap, hipStream_t s, StencilVariant v = StencilVariant::Auto,
-                 PackTarget<T>* pack = nullptr);
+                 Stencil5Coeffs c, bool wrap, hipStream_t s, StencilVariant v = StencilVariant::Auto);
 
 // ------------------------------------- chunk-list pass (interior-first super-step)
 // The S-step pass over chunks of the core of a ghost-ring tile (no wrap) on the
@@ -196,10 +161,9 @@ struct ChunkPassShape {
 template <typename T>
 bool chunk_pass_shape(const TileGeom& g, int steps, const Stencil5Coeffs& c, ChunkPassShape* out);
 // table: shape.blocks x entries chunks in device memory (ChunkSchedule::table).
-// pack: the fused halo pack of the cells this launch stores (sets pack->applied).
 template <typename T>
 void stencil5_chunk_pass(const T* in, T* out, const TileGeom& g, const Stencil5Coeffs& c, const ChunkPassShape& shape,
-                         const PassChunk* table, int entries, hipStream_t s, PackTarget<T>* pack = nullptr);
+                         const PassChunk* table, int entries, hipStream_t s);
 
 // max |x[i]| over n elements into *out (device pointer, overwritten; NaN if
 // any element is NaN): the range check of the sum form.
@@ -209,6 +173,10 @@ void absmax(const T* x, index_t n, T* out, hipStream_t s);
 // sit on different hardware queues): one bounded ~0.8 ms sleeping wave on a, a
 // no-op kernel on b (kernels/queue_probe.hip). Synchronises both streams.
 bool streams_concurrent(hipStream_t a, hipStream_t b);
+// One single-wave kernel that holds stream s for `us` microseconds (capped at
+// 10 ms) of the GPU's constant-rate wall clock (kernels/queue_probe.hip): the
+// wire time an RCCL-loopback rehearsal adds after each transfer.
+void spin_delay(double us, hipStream_t s);
 // Number of 32-bit words that differ between a and b (bytes % 4 == 0) into
 // *out (device pointer, overwritten): the direct halo's bitwise validation.
 void count_diff(const void* a, const void* b, index_t bytes, unsigned* out, hipStream_t s);

@@ -72,11 +72,14 @@
 //     super-step but the bare last one; the interior-first opening IS the
 //     priming exchange, so a rank without a chunk-list form for its tile
 //     (uneven decomposition) runs prime + pass instead and stays in step;
-//   * prepare()'s schedule decision is taken from timings agreed over ranks
-//     (element-wise max through an RCCL all-reduce, or the host allgather):
-//     every rank adopts the same opening; interior-first only when its
-//     worst-rank median beats the serial one by min_gain and by more than the
-//     worst-rank spread (interquartile range) of either;
+//   * prepare()'s schedule decision is taken from timings agreed over ranks:
+//     each round times every opening from a device barrier on every rank, the
+//     ranks agree on the round's maximum of each (the window is the max over
+//     ranks), and the decision rests on the paired ratios of those maxima
+//     (runtime/decision.hpp); every rank adopts the same opening. Agreements
+//     go through the host allgather whenever the caller passed one (the path
+//     the one-GPU multi-rank tests run), else through an RCCL all-reduce;
+//     agreement_path() names the one in use;
 //   * the sum form's range guard takes max|u| over all ranks (at the first
 //     check and in every collective call: prepare, warm, profile_window).
 // Every host wait with collectives in flight goes through wait_idle(), which
@@ -164,27 +167,9 @@ struct SolverConfig {
   // always prime + pass (Serial), always interior-first where the tile has the
   // form (InteriorFirst).
   Opening opening = Opening::Auto;
-  // Auto: interior-first must beat serial by at least this fraction (and by
-  // more than the measured spread) to be chosen.
-  double min_gain = 0.03;
-  // The opening from hipGraphs captured in prepare(): the interior-first
-  // opening's main-stream chain (pack -> RCCL -> unpack -> outer chunks), and
-  // the serial opening's priming exchange (pack -> RCCL -> unpack). The host
-  // issues one launch instead of the RCCL group calls and the copy launches,
-  // so the GPU does not wait for the host's RCCL enqueue (~25 us) between the
-  // pack and the transfer.
-  bool opening_graph = false;
-  // Fused halo pack: the whole-core pipeline passes of the post-exchange
-  // schedules (the bare pass, the interior-first opening's outer chunks, the
-  // steady super-steps) also write their send bands into the exchange's send
-  // buffer, so the next exchange is RCCL + unpack (no pack launch). Applies
-  // where the plan has remote peers and the pass takes a pipeline form (fp32
-  // S > 16, fp64 S 9..16 on whole vectors); other passes keep the pack launch.
-  // Off by default: measured on the 8-GPU-tile window, the pack launch is what
-  // keeps the GPU busy while the host enqueues the RCCL group, and its fused
-  // form costs the pass 6-7 us (profiles/r04_fp: serial 0.324 vs 0.314 ms,
-  // interior-first 0.308 vs 0.298 with / without).
-  bool fused_pack = false;
+  // Auto: the upper end of the median paired ratio's 95% notch must be below
+  // 1 - min_gain (0: the notch alone guards against noise; decision.hpp).
+  double min_gain = 0.0;
   // RCCL backend: run the halo exchange on a communicator split off `comm`
   // with at most this many workgroups per RCCL kernel (0 = RCCL's default).
   int halo_max_ctas = 0;
@@ -192,6 +177,10 @@ struct SolverConfig {
   // primes, its last pass is bare, the opening is chosen as with peers), so
   // one GPU rehearses the window shape an N-GPU run executes.
   bool rehearse_peers = false;
+  // One-GPU rehearsal only (loopback_self, one rank): every RCCL transfer is
+  // followed by a single-wave kernel holding the main stream this long (us),
+  // standing in for the xGMI wire time the loopback does not have.
+  double wire_delay_us = 0;
   // Super-steps estimated longer than this (us, at ~9 T cell-steps/s) are
   // launched eagerly instead of from a hipGraph: on the 8-GPU tile (0.24 ms
   // passes) a 20-step RCCL-loopback window took 0.276 ms eager vs 0.285 from
@@ -242,7 +231,6 @@ class StencilSolver {
   void field_changed() {
     ghost_fresh_ = false;
     range_checked_ = false;
-    packed_ = nullptr;
   }
   // Fault injection (like the apps' --fault-inject): the host
   // sleeps `seconds` on entering `phase` ("prepare", "warm", "run",
@@ -270,6 +258,10 @@ class StencilSolver {
   // Fault injection for the validation: this rank corrupts one received ghost
   // cell of the direct push before the comparison (tests of the fallback).
   void inject_direct_mismatch(bool on) { inject_mismatch_ = on; }
+  // Fault injection for the validation: this rank's first direct pass does not
+  // wait for the neighbours' pushes and runs before they land (the visibility
+  // race the check must catch).
+  void inject_direct_skip_wait(bool on) { inject_skip_wait_ = on; }
   bool overlapped() const { return cfg_.overlap; }
   // Whether the solver follows the peers' schedule (remote peers, or a
   // loopback rehearsal of them).
@@ -278,7 +270,7 @@ class StencilSolver {
   // this rank (the opening is on and the tile has the chunk-list form).
   bool halo_last(int S) const;
   // prepare()'s decision ("" before it decided, "serial" or "interior-first")
-  // and the agreed (worst-rank) medians / spreads it was taken from.
+  // and the statistics of the per-round maxima over ranks it was taken from.
   const std::string& opening_choice() const { return opening_choice_; }
   const std::string& opening_reason() const { return opening_reason_; }
   double opening_serial_ms() const { return opening_ms_[0]; }
@@ -287,8 +279,19 @@ class StencilSolver {
   double opening_ratio() const { return opening_ratio_; }
   double opening_ratio_iqr() const { return opening_spread_[1]; }
   int opening_samples() const { return opening_samples_; }
-  // This rank's paired ratios of every candidate (outer workgroups, ratios per round).
+  // Paired ratios of the per-round maxima over ranks, per candidate (outer
+  // workgroups, ratio per round), and this rank's own per-round ratios.
   const std::vector<std::pair<int, std::vector<double>>>& opening_ratio_samples() const { return opening_ratio_samples_; }
+  const std::vector<std::pair<int, std::vector<double>>>& opening_local_ratio_samples() const {
+    return opening_local_ratio_samples_;
+  }
+  // How collective agreements travel: "host allgather", "rccl all-reduce" or
+  // "none (one rank)"; the device barrier before timed samples uses RCCL when
+  // a communicator exists.
+  std::string agreement_path() const {
+    if (world_ <= 1) return "none (one rank)";
+    return cfg_.bootstrap ? "host allgather" : "rccl all-reduce";
+  }
   // Workgroups of the outer (ghost-ring) launch of the interior-first opening
   // at depth S (0: none built).
   int halo_last_outer_wgs(int S) const {
@@ -312,14 +315,6 @@ class StencilSolver {
   // The halo communicator's CTA cap (0: RCCL's default) and why it is not the
   // requested one ("" when it is).
   int halo_max_ctas() const { return halo_comm_ ? halo_comm_->max_ctas() : 0; }
-  // SolverConfig::opening_graph: "off", "not used yet", "captured" or "capture failed".
-  std::string opening_graph_state() const {
-    if (!cfg_.opening_graph) return "off";
-    for (const auto& hl : halo_lasts_)
-      if (hl && hl->chain_tried) return hl->chain_ok ? "captured" : "capture failed";
-    if (prime_graph_.tried) return prime_graph_.ok ? "captured" : "capture failed";
-    return "not used yet";
-  }
   const std::string& halo_comm_note() const { return halo_comm_note_; }
   // The side stream's hardware-queue check ("" when no two-stream schedule is possible).
   const std::string& stream_note() const { return stream_note_; }
@@ -328,10 +323,7 @@ class StencilSolver {
   void abort_halo_comm() const {
     if (halo_comm_) halo_comm_->abort();
   }
-  // SolverConfig::fused_pack in effect (the plan's windows can take it).
-  bool fused_pack() const { return pack_.send != nullptr; }
-  // Exchanges of the last run() whose pack was fused into the preceding pass.
-  int last_run_fused_packs() const { return last_fused_packs_; }
+  double wire_delay_us() const { return ex_ ? ex_->wire_delay_us() : 0.0; }
   // Interior-first super-steps of the last run() whose inner launch had to wait
   // for the main stream (a cross-stream event); 0 when main had drained.
   int last_run_forks() const { return last_forks_; }
@@ -342,17 +334,7 @@ class StencilSolver {
   void enqueue_block(T* cur, T* nxt, int S);  // S <= block_ iterations, one exchange
   // `steps` iterations over core rows [r0, r1) x cols [c0, c1).
   void update(const T* in, T* out, int steps, index_t c0, index_t c1, index_t r0, index_t r1, hipStream_t s);
-  // Fused halo pack state. packed_: the buffer whose send bands the exchange's
-  // send buffer holds (nullptr: none / unknown). Every pass notes what it wrote
-  // (note_written); exchange() skips the pack launch when the send buffer
-  // already holds the tile's bands.
-  void core_pass(T* cur, T* nxt, int S, hipStream_t s, bool pack = true);  // whole core, fused pack if available
-  void note_written(T* out, bool packed) { packed_ = packed ? out : (packed_ == out ? nullptr : packed_); }
-  void exchange(T* tile, hipStream_t s);
-  void ensure_packed(T* tile, hipStream_t s);  // the send buffer holds tile's bands afterwards
-  kernels::PackTarget<T> pack_;  // send == nullptr: the fused pack is off
-  T* packed_ = nullptr;
-  int last_fused_packs_ = 0;
+  void core_pass(const T* cur, T* nxt, int S, hipStream_t s) { update(cur, nxt, S, 0, tile_.width, 0, tile_.height, s); }
   int last_forks_ = 0;
   // Graphs of `chain` consecutive super-steps of size S, one per buffer
   // orientation: g[0] starts from buf_a_, g[1] from buf_b_.
@@ -361,8 +343,6 @@ class StencilSolver {
     int chain = 1;
     bool ok = false;
     GraphExec g[2];
-    T* packed_after[2] = {nullptr, nullptr};  // packed_ after a replay of g[k]
-    int fused_packs = 0;                      // exchanges per replay whose pack was fused
   };
   // Graphs for super-step size S, captured on first use with a chain of at
   // most `count` super-steps (nullptr: graphs off or capture failed).
@@ -398,24 +378,9 @@ class StencilSolver {
     kernels::ChunkPassShape inner_shape, outer_shape;  // blocks = workgroups of each launch
     kernels::HaloLastSchedule sched;
     DeviceBuffer<kernels::PassChunk> inner_table, outer_table;
-    // SolverConfig::opening_graph: the main stream's part (pack -> RCCL ->
-    // unpack -> outer chunks) captured once per buffer orientation.
-    GraphExec chain[2];
-    bool chain_tried = false, chain_ok = false;
-    // The outer chunks take the fused pack: the inner chunks store no cell of
-    // a send window (checked on the host), so no launch writes the send buffer
-    // while RCCL reads it and the outer launch alone writes every send band.
-    bool outer_packs = false;
   };
-  bool capture_chain(HaloLastPass* hl);
-  // The serial priming exchange of cur_ (SolverConfig::opening_graph: from a
-  // graph per buffer orientation, captured on first use).
-  void prime_exchange();
-  struct PrimeGraph {
-    GraphExec g[2];
-    bool tried = false, ok = false;
-  };
-  PrimeGraph prime_graph_;
+  // The serial priming exchange of cur_ (pack -> wire -> unpack on main).
+  void prime_exchange() { ex_->exchange(cur_, main_.get()); }
   HaloLastPass* halo_last_pass(int S, bool build);  // nullptr: not in use / no form for S
   std::unique_ptr<HaloLastPass> build_halo_last(int S, int outer_wgs);  // nullptr: no form for S
   void enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks* marks = nullptr);
@@ -435,21 +400,22 @@ class StencilSolver {
   // over ranks at the first check and whenever `collective`.
   void ensure_range(bool collective);
   void begin_run(bool collective);           // range check + prime
-  double opening_ms_[2] = {0, 0};            // agreed medians: prime + pass, interior-first (ms)
-  double opening_spread_[2] = {0, 0};        // agreed IQRs: serial (ms), paired ratio
-  double opening_ratio_ = 0;                 // agreed median paired ratio interior-first / serial
+  double opening_ms_[2] = {0, 0};            // medians of the per-round maxima: prime + pass, interior-first (ms)
+  double opening_spread_[2] = {0, 0};        // IQRs: serial maxima (ms), paired ratio of maxima
+  double opening_ratio_ = 0;                 // median paired ratio of the maxima, interior-first / serial
   int opening_samples_ = 0;
-  std::vector<std::pair<int, std::vector<double>>> opening_ratio_samples_;
+  std::vector<std::pair<int, std::vector<double>>> opening_ratio_samples_, opening_local_ratio_samples_;
   std::string opening_choice_;               // "" before prepare() decided, "serial" or "interior-first"
   std::string opening_reason_;
   void choose_opening(int S);                // Opening::Auto: time both, agree, keep the faster
   bool side_pending_ = false;                // side-stream work not yet joined to main
   void join_side();                          // main stream waits for the side stream's work
-  // Collective agreement: element-wise max over ranks (RCCL all-reduce, or
-  // the host allgather). No-op on one rank.
+  // Collective agreement: element-wise max over ranks (the host allgather when
+  // the caller passed one, else an RCCL all-reduce). No-op on one rank.
   void agree_max(std::vector<double>& v, const char* phase);
-  // RCCL ranks only: every rank reaches this point before any returns (a
-  // one-element all-reduce, waited under the watchdog).
+  // Every rank reaches this point before any returns: a one-element RCCL
+  // all-reduce waited under the watchdog (tight release skew, so timed samples
+  // start together), or the agreement path without a communicator.
   void device_barrier(const char* phase);
   // Both streams drained, polled under the communication watchdog when
   // collectives may be in flight; failures name `phase`.
@@ -489,7 +455,8 @@ class StencilSolver {
   std::string direct_state_;
   double direct_ms_[2] = {0, 0};              // agreed medians: backend opening, direct opening
   bool inject_mismatch_ = false;
-  DeviceBuffer<T> ref_;                       // validation snapshot
+  bool inject_skip_wait_ = false;
+  DeviceBuffer<T> ref_;                       // validation snapshots: the field before, the backend's result
   DeviceBuffer<unsigned> diff_;
   void validate_direct(int S);                // DirectHalo::Validate, collective (prepare)
   void poison_ghost(T* tile);                 // sentinel into every received ghost cell

@@ -4,6 +4,7 @@
 // stream while the exchange and the outer chunks go to another: on a shared
 // queue they serialise and the 8-GPU-tile opening takes ~0.5 ms instead of
 // ~0.3 (seen in 2 of 14 bench-flow windows, profiles/r04_sg).
+// Also: spin_delay, the one-GPU rehearsal's stand-in for xGMI wire time.
 #include <hip/hip_runtime.h>
 
 #include <chrono>
@@ -24,7 +25,26 @@ __global__ __launch_bounds__(64) void touch_kernel(unsigned* p) {
   if (threadIdx.x == 0 && p) *p = 1u;
 }
 
+// One wave holding its queue for `ticks` of the constant-rate wall clock
+// (wall_clock64(), hipDeviceAttributeWallClockRate): bounded by the host's cap.
+__global__ __launch_bounds__(64) void spin_delay_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
 }  // namespace
+
+void spin_delay(double us, hipStream_t s) {
+  static const double ticks_per_us = [] {
+    int dev = 0, khz = 0;
+    MXS_HIP_CHECK(hipGetDevice(&dev));
+    MXS_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    return khz > 0 ? double(khz) / 1e3 : 100.0;
+  }();
+  const double capped = us < 0 ? 0 : (us > 10000.0 ? 10000.0 : us);  // at most 10 ms
+  spin_delay_kernel<<<1, 64, 0, s>>>((unsigned long long)(capped * ticks_per_us));
+  MXS_HIP_CHECK_LAUNCH();
+}
 
 bool streams_concurrent(hipStream_t a, hipStream_t b) {
   hipEvent_t done_b = nullptr;

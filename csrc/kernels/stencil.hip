@@ -239,7 +239,7 @@ void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
 // LDS tile (32 x 128 for column strips, 128 x 16 for row strips).
 template <typename T, int S, bool WRAP, bool SUM>
 void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
-               T sc, StencilVariant v, hipStream_t s, PackTarget<T>* pk) {
+               T sc, StencilVariant v, hipStream_t s) {
   constexpr int TW = sizeof(T) == 4 ? 128 : 64;
   constexpr int NW = sizeof(T) == 4 ? 32 : 16;
   constexpr int NH = (sizeof(T) == 8 && S > 8) ? 64 : 128;  // keeps the fp64 thin tile under 64 KB of LDS
@@ -253,7 +253,7 @@ void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, i
   }
   if constexpr (sizeof(T) == 8 && S >= kPipeMinF64) {
     if (wide_pipe_ok<T, S, WRAP>(g, x0, x1, y0, y1))
-      return launch_pipe<T, S, WRAP, SUM>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s, pk);
+      return launch_pipe<T, S, WRAP, SUM>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
   }
   launch_stream<T, S, WRAP, SUM && sizeof(T) == 4>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
 }
@@ -262,22 +262,22 @@ void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, i
 // bodies then take sc = c^S); S = 1 always keeps the per-step form.
 template <typename T, bool WRAP, int S = 1>
 void dispatch_tb(int steps, bool sum, const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0,
-                 index_t y1, T c0, T c1, StencilVariant v, hipStream_t s, PackTarget<T>* pk) {
+                 index_t y1, T c0, T c1, StencilVariant v, hipStream_t s) {
   const T sc = T(std::pow(double(c1), double(S)));
   if constexpr (S <= kMaxTimeBlock) {
     if (steps == S) {
       if constexpr (S > 1) {
-        if (sum) return launch_tb<T, S, WRAP, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s, pk);
+        if (sum) return launch_tb<T, S, WRAP, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s);
       }
-      return launch_tb<T, S, WRAP, false>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s, pk);
+      return launch_tb<T, S, WRAP, false>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s);
     }
-    return dispatch_tb<T, WRAP, S + 1>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s, pk);
+    return dispatch_tb<T, WRAP, S + 1>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   } else if constexpr (S <= kMaxTimeBlockDeep && sizeof(T) == 4) {
     if (steps == S) {
-      if (sum) return launch_pipe<T, S, WRAP, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s, pk);
-      return launch_pipe<T, S, WRAP, false>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s, pk);
+      if (sum) return launch_pipe<T, S, WRAP, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+      return launch_pipe<T, S, WRAP, false>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
     }
-    return dispatch_tb<T, WRAP, S + 1>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s, pk);
+    return dispatch_tb<T, WRAP, S + 1>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   } else {
     MXS_CHECK(false, "stencil5_tb: steps must be in [1, " << (sizeof(T) == 4 ? kMaxTimeBlockDeep : kMaxTimeBlock)
                                                           << "], got " << steps);
@@ -287,8 +287,7 @@ void dispatch_tb(int steps, bool sum, const T* in, T* out, const TileGeom& g, in
 
 template <typename T>
 void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0, index_t y1,
-                 Stencil5Coeffs c, bool wrap, hipStream_t s, StencilVariant v, PackTarget<T>* pack) {
-  if (pack) pack->applied = false;
+                 Stencil5Coeffs c, bool wrap, hipStream_t s, StencilVariant v) {
   if (x1 <= x0 || y1 <= y0) return;
   constexpr int N = Vec16<T>::N;
   MXS_CHECK(x0 >= 0 && y0 >= 0 && x1 <= g.width && y1 <= g.height, "stencil5_tb: rect out of the core");
@@ -309,11 +308,8 @@ void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, 
   }
   const T c0 = T(c.center), c1 = T(c.neighbor);
   const bool sum = uses_sum_form(c) && v != StencilVariant::LdsTile;
-  // The fused pack needs the pipeline's ghost-ring forms (which take it) and
-  // whole-vector windows; the rectangle's columns are whole vectors already.
-  PackTarget<T>* pk = pack && !wrap && pack->send && x1 % N == 0 && pack_segs_ok<T>(g, pack->segs) ? pack : nullptr;
-  if (wrap) dispatch_tb<T, true>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s, nullptr);
-  else dispatch_tb<T, false>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s, pk);
+  if (wrap) dispatch_tb<T, true>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+  else dispatch_tb<T, false>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   MXS_HIP_CHECK_LAUNCH();
 }
 
@@ -403,7 +399,7 @@ void note_pipe_lag1(bool lag1) { g_last_lag1.store(lag1, std::memory_order_relax
                                  Stencil5Coeffs, hipStream_t);                                                 \
   template void stencil5_periodic<T>(const T*, T*, const TileGeom&, Stencil5Coeffs, hipStream_t);              \
   template void stencil5_tb<T>(const T*, T*, const TileGeom&, int, index_t, index_t, index_t, index_t,          \
-                               Stencil5Coeffs, bool, hipStream_t, StencilVariant, PackTarget<T>*);             \
+                               Stencil5Coeffs, bool, hipStream_t, StencilVariant);                             \
   template bool stencil5_periodic_supported<T>(const TileGeom&);                                               \
   template void stencil_box<T>(const T*, T*, const TileGeom&, index_t, index_t, index_t, index_t,               \
                                const BoxWeights&, hipStream_t);

@@ -1400,54 +1400,11 @@ struct PipeShares {
   }
 };
 
-// Fused halo pack (kernels.hpp: PackSegs), run by the whole workgroup after
-// its last chunk: the cells of the core rectangle [x0, x1) x [y0, y1) that this
-// workgroup stored and that lie in a send window are copied from the tile into
-// the packed send buffer, 16 bytes per lane. The caller's __syncthreads() makes
-// the stage-1 waves' stores visible to every wave of the workgroup (one CU, one
-// L1; each wave first waits for its own stores to be acknowledged). Window
-// columns and the rectangle's columns are whole 16-byte vectors
-// (host-checked), so a vector is inside a window or outside it.
-template <typename T>
-__device__ __forceinline__ void pack_rect(const T* __restrict__ core, index_t pitch, T* __restrict__ send,
-                                          const PackSegs& pk, index_t x0, index_t x1, index_t y0, index_t y1) {
-  constexpr int N = 16 / sizeof(T);
-  constexpr int K = 8;  // vectors in flight per lane: one memory round trip per K, not per vector
-  using V = T __attribute__((ext_vector_type(N)));
-#pragma unroll 1
-  for (int k = 0; k < pk.n; ++k) {  // workgroup-uniform
-    const PackSeg sg = pk.seg[k];
-    const index_t ax = x0 > sg.x0 ? x0 : sg.x0, bx = x1 < sg.x0 + sg.w ? x1 : sg.x0 + sg.w;
-    const index_t ay = y0 > sg.y0 ? y0 : sg.y0, by = y1 < sg.y0 + sg.h ? y1 : sg.y0 + sg.h;
-    if (ax >= bx || ay >= by) continue;
-    const int vw = int((bx - ax) / N), total = vw * int(by - ay);
-    const T* __restrict__ src = core + ay * pitch + ax;
-    T* __restrict__ dst = send + sg.off + (ay - sg.y0) * sg.w + (ax - sg.x0);
-    const int step = int(blockDim.x);
-#pragma unroll 1
-    for (int t0 = int(threadIdx.x); t0 < total; t0 += K * step) {
-      V v[K];
-      index_t o[K];
-#pragma unroll
-      for (int j = 0; j < K; ++j) {
-        const int t = t0 + j * step;
-        const int ry = t / vw, rx = t - ry * vw;
-        o[j] = index_t(ry) * sg.w + rx * N;
-        if (t < total) v[j] = *reinterpret_cast<const V*>(src + index_t(ry) * pitch + rx * N);
-      }
-#pragma unroll
-      for (int j = 0; j < K; ++j)
-        if (t0 + j * step < total) *reinterpret_cast<V*>(dst + o[j]) = v[j];
-    }
-  }
-}
-
 template <int S0, int S1, int PF, bool WRAP, int PRIO = 0, typename T = float, bool SUM = false,
           int G = kWavesPerBlock, bool XM = false, bool JOINT = false, int LAG1 = 0, int XB = 0>
 __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
-    index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, const PipeShares shares, T c0, T c1,
-    T* __restrict__ send = nullptr, const PackSegs pack = PackSegs{}) {
+    index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, const PipeShares shares, T c0, T c1) {
   using P = PipeShape<S0, S1, PF>;
   using B = typename FastBody<T, SUM, XB>::type;
   constexpr int OW = StripShape<T, P::S, true>::OW;
@@ -1476,7 +1433,6 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
     a = slot * shares.share;
     b = a + shares.share < total ? a + shares.share : total;
   }
-  const index_t a0 = a;
 #pragma unroll 1
   while (a < b) {  // workgroup-uniform: all 8 waves take every chunk (barriers inside)
     const index_t grp = a / rows, r0 = a - grp * rows;
@@ -1490,21 +1446,6 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
                                       ring + strip * P::RING * kWaveSize, stage);
     }
     a += r1 - r0;
-  }
-  if constexpr (!WRAP) {
-    if (pack.n > 0) {  // fused halo pack of the cells this workgroup stored (kernel-uniform)
-      __builtin_amdgcn_s_waitcnt(0);  // this wave's tile stores acknowledged (vmcnt counts stores on gfx9)
-      __syncthreads();
-      constexpr index_t GW = JOINT ? index_t(OWG) : index_t(G) * OW;  // output columns per group
-#pragma unroll 1
-      for (index_t c = a0; c < b;) {
-        const index_t grp = c / rows, r0 = c - grp * rows;
-        const index_t r1 = rows < r0 + (b - c) ? rows : r0 + (b - c);
-        const index_t cx0 = x_begin + grp * GW, cx1 = cx0 + GW < x_end ? cx0 + GW : x_end;
-        pack_rect<T>(out + core_off, pitch, send, pack, cx0, cx1, y_begin + r0, y_begin + r1);
-        c += r1 - r0;
-      }
-    }
   }
 }
 
@@ -1520,8 +1461,7 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
 template <int S0, int S1, int PF, typename T, bool SUM, int LAG1>
 __global__ __launch_bounds__(2 * kWavesPerBlock * kWaveSize) void stencil5_pipe_chunks_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
-    index_t x_begin, index_t x_end, index_t y_begin, const PassChunk* __restrict__ table, int entries, T c0, T c1,
-    T* __restrict__ send, const PackSegs pack) {
+    index_t x_begin, index_t x_end, index_t y_begin, const PassChunk* __restrict__ table, int entries, T c0, T c1) {
   constexpr int G = kWavesPerBlock;
   using P = PipeShape<S0, S1, PF>;
   using B = typename FastBody<T, SUM>::type;
@@ -1536,17 +1476,6 @@ __global__ __launch_bounds__(2 * kWavesPerBlock * kWaveSize) void stencil5_pipe_
     if (c.r1 <= c.r0) break;  // lists are packed from slot 0
     pipe_chunk<B, S0, S1, PF, false, true, G, LAG1>(in, out, pitch, core_off, W, H, x_begin + index_t(c.group) * OWG,
                                                    x_end, y_begin + c.r0, y_begin + c.r1, c0, c1, ring, stage, strip);
-  }
-  if (pack.n > 0) {  // fused halo pack (see stencil5_stream_pipe_kernel)
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-#pragma unroll 1
-    for (int e = 0; e < entries; ++e) {
-      const PassChunk c = mine[e];
-      if (c.r1 <= c.r0) break;
-      const index_t cx0 = x_begin + index_t(c.group) * OWG, cx1 = cx0 + OWG < x_end ? cx0 + OWG : x_end;
-      pack_rect<T>(out + core_off, pitch, send, pack, cx0, cx1, y_begin + c.r0, y_begin + c.r1);
-    }
   }
 }
 

@@ -133,7 +133,7 @@ bool pipe_balanced();
 
 template <typename T, int S, bool WRAP, bool SUM, int JS0, int LAG1 = 0>
 void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0,
-                      T c1, T sc, hipStream_t s, PackTarget<T>* pk) {
+                      T c1, T sc, hipStream_t s) {
   const index_t share = pipe_share<T, S, WRAP, SUM, JS0>(x0, x1, y0, y1);
   const int blocks = pipe_blocks<T, S, WRAP, SUM, JS0>();
   PipeShares shares = PipeShares::equal(share);
@@ -149,41 +149,33 @@ void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_
   }
   MXS_CHECK(chunk * g.pitch * index_t(sizeof(T)) <= kMaxChunkBytes,
             "stencil5_tb: a pipeline chunk must stay within kMaxChunkBytes (buffer-descriptor stores)");
-  // The fused pack: ghost-ring passes only (stencil5_tb checked the windows).
-  T* send = nullptr;
-  PackSegs segs;
-  if (pk && !WRAP) {
-    send = pk->send;
-    segs = pk->segs;
-    pk->applied = true;
-  }
   pipe_kernel<T, S, WRAP, SUM, JS0, LAG1>()<<<blocks, 2 * kBlock, 0, s>>>(
-      in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, shares, SUM ? sc : c0, c1, send, segs);
+      in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, shares, SUM ? sc : c0, c1);
   note_dispatch(SUM ? "stream_pipe_sum" : "stream_pipe");
   note_pipe_lag1(LAG1 != 0);
 }
 
 template <typename T, int S, bool WRAP, bool SUM>
 void launch_pipe_impl(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
-                 T sc, hipStream_t s, PackTarget<T>* pk) {
+                 T sc, hipStream_t s) {
   if constexpr (pipe_joint_ok<T, S>()) {
     if (pipe_joint()) {
       if constexpr (sizeof(T) == 4 && S == 20) {
         if (pipe_lag1() && pipe_share<T, S, WRAP, SUM, 12>(x0, x1, y0, y1) <= kLag1MaxChunk) {
           if (x1 - x0 < kJointWide)
-            return launch_pipe_form<T, S, WRAP, SUM, 8, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s, pk);
-          return launch_pipe_form<T, S, WRAP, SUM, 12, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s, pk);
+            return launch_pipe_form<T, S, WRAP, SUM, 8, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+          return launch_pipe_form<T, S, WRAP, SUM, 12, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
         }
       } else if constexpr (sizeof(T) == 4 && S == 24) {
-        if (pipe_lag1()) return launch_pipe_form<T, S, WRAP, SUM, 12, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s, pk);
+        if (pipe_lag1()) return launch_pipe_form<T, S, WRAP, SUM, 12, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
       } else if constexpr (sizeof(T) == 8 && S == 16) {
         if (pipe_lag1() && pipe_share<T, S, WRAP, SUM, 8>(x0, x1, y0, y1) <= kLag1MaxChunkF64)
-          return launch_pipe_form<T, S, WRAP, SUM, 8, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s, pk);
+          return launch_pipe_form<T, S, WRAP, SUM, 8, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
       }
-      return launch_pipe_form<T, S, WRAP, SUM, joint_s0<T, S>()>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s, pk);
+      return launch_pipe_form<T, S, WRAP, SUM, joint_s0<T, S>()>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
     }
   }
-  launch_pipe_form<T, S, WRAP, SUM, 0>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s, pk);
+  launch_pipe_form<T, S, WRAP, SUM, 0>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
 }
 
 // Whether the fp64 wide-lane pipeline can take [x0, x1) x [y0, y1) at depth S:
@@ -204,7 +196,7 @@ bool wide_pipe_ok_impl(const TileGeom& g, index_t x0, index_t x1, index_t y0, in
 // Explicitly instantiated in the pipeline TUs.
 template <typename T, int S, bool WRAP, bool SUM>
 void launch_pipe(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
-                 T sc, hipStream_t s, PackTarget<T>* pk = nullptr);
+                 T sc, hipStream_t s);
 template <typename T, int S, bool WRAP>
 bool wide_pipe_ok(const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1);
 

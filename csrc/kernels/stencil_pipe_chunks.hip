@@ -72,34 +72,27 @@ bool shape_for(const TileGeom& g, ChunkPassShape* out) {
 
 template <typename T, int S, bool SUM, int JS0, int LAG1>
 void launch_chunks(const T* in, T* out, const TileGeom& g, T c0, T c1, const ChunkPassShape& sh,
-                   const PassChunk* table, int entries, hipStream_t s, PackTarget<T>* pk) {
-  T* send = nullptr;
-  PackSegs segs;
-  if (pk) {
-    send = pk->send;
-    segs = pk->segs;
-    pk->applied = true;
-  }
+                   const PassChunk* table, int entries, hipStream_t s) {
   chunks_kernel<T, S, SUM, JS0, LAG1>()<<<sh.blocks, 2 * kBlock, 0, s>>>(
-      in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, table, entries, c0, c1, send, segs);
+      in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, table, entries, c0, c1);
   note_dispatch(SUM ? "stream_pipe_sum_chunks" : "stream_pipe_chunks");
   note_pipe_lag1(LAG1 != 0);
 }
 
 template <typename T, int S, bool SUM>
 void launch_for(const T* in, T* out, const TileGeom& g, T c0, T c1, const ChunkPassShape& sh, const PassChunk* table,
-                int entries, hipStream_t s, PackTarget<T>* pk) {
+                int entries, hipStream_t s) {
   const bool lag = sh.lag1 != 0;
   if constexpr (sizeof(T) == 4 && S == 20) {
-    if (sh.js0 == 8 && lag) return launch_chunks<T, S, SUM, 8, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s, pk);
-    if (sh.js0 == 12 && lag) return launch_chunks<T, S, SUM, 12, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s, pk);
-    if (sh.js0 == 12) return launch_chunks<T, S, SUM, 12, 0>(in, out, g, c0, c1, sh, table, entries, s, pk);
+    if (sh.js0 == 8 && lag) return launch_chunks<T, S, SUM, 8, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s);
+    if (sh.js0 == 12 && lag) return launch_chunks<T, S, SUM, 12, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s);
+    if (sh.js0 == 12) return launch_chunks<T, S, SUM, 12, 0>(in, out, g, c0, c1, sh, table, entries, s);
   } else if constexpr (sizeof(T) == 4 && S == 24) {
-    if (sh.js0 == 12 && lag) return launch_chunks<T, S, SUM, 12, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s, pk);
-    if (sh.js0 == 12) return launch_chunks<T, S, SUM, 12, 0>(in, out, g, c0, c1, sh, table, entries, s, pk);
+    if (sh.js0 == 12 && lag) return launch_chunks<T, S, SUM, 12, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s);
+    if (sh.js0 == 12) return launch_chunks<T, S, SUM, 12, 0>(in, out, g, c0, c1, sh, table, entries, s);
   } else if constexpr (sizeof(T) == 8 && S == 16) {
-    if (sh.js0 == 8 && lag) return launch_chunks<T, S, SUM, 8, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s, pk);
-    if (sh.js0 == 8) return launch_chunks<T, S, SUM, 8, 0>(in, out, g, c0, c1, sh, table, entries, s, pk);
+    if (sh.js0 == 8 && lag) return launch_chunks<T, S, SUM, 8, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s);
+    if (sh.js0 == 8) return launch_chunks<T, S, SUM, 8, 0>(in, out, g, c0, c1, sh, table, entries, s);
   }
   MXS_CHECK(false, "stencil5_chunk_pass: no kernel for S = " << S << ", js0 = " << sh.js0 << ", lag1 = " << sh.lag1);
 }
@@ -131,10 +124,8 @@ bool chunk_pass_shape(const TileGeom& g, int steps, const Stencil5Coeffs& c, Chu
 
 template <typename T>
 void stencil5_chunk_pass(const T* in, T* out, const TileGeom& g, const Stencil5Coeffs& c, const ChunkPassShape& sh,
-                         const PassChunk* table, int entries, hipStream_t s, PackTarget<T>* pack) {
+                         const PassChunk* table, int entries, hipStream_t s) {
   using namespace detail;
-  if (pack) pack->applied = false;
-  PackTarget<T>* pk = pack && pack->send && pack_segs_ok<T>(g, pack->segs) ? pack : nullptr;
   MXS_CHECK(table != nullptr && entries > 0 && sh.blocks > 0, "stencil5_chunk_pass: no schedule");
   MXS_CHECK(sh.sum == uses_sum_form(c), "stencil5_chunk_pass: shape built for the other evaluation form");
   const T c0 = T(c.center), c1 = T(c.neighbor);
@@ -142,18 +133,18 @@ void stencil5_chunk_pass(const T* in, T* out, const TileGeom& g, const Stencil5C
   const T k0 = sh.sum ? sc : c0;
   if constexpr (sizeof(T) == 4) {
     if (sh.steps == 20) {
-      if (sh.sum) launch_for<T, 20, true>(in, out, g, k0, c1, sh, table, entries, s, pk);
-      else launch_for<T, 20, false>(in, out, g, k0, c1, sh, table, entries, s, pk);
+      if (sh.sum) launch_for<T, 20, true>(in, out, g, k0, c1, sh, table, entries, s);
+      else launch_for<T, 20, false>(in, out, g, k0, c1, sh, table, entries, s);
     } else if (sh.steps == 24) {
-      if (sh.sum) launch_for<T, 24, true>(in, out, g, k0, c1, sh, table, entries, s, pk);
-      else launch_for<T, 24, false>(in, out, g, k0, c1, sh, table, entries, s, pk);
+      if (sh.sum) launch_for<T, 24, true>(in, out, g, k0, c1, sh, table, entries, s);
+      else launch_for<T, 24, false>(in, out, g, k0, c1, sh, table, entries, s);
     } else {
       MXS_CHECK(false, "stencil5_chunk_pass: fp32 depth " << sh.steps);
     }
   } else {
     MXS_CHECK(sh.steps == 16, "stencil5_chunk_pass: fp64 depth " << sh.steps);
-    if (sh.sum) launch_for<T, 16, true>(in, out, g, k0, c1, sh, table, entries, s, pk);
-    else launch_for<T, 16, false>(in, out, g, k0, c1, sh, table, entries, s, pk);
+    if (sh.sum) launch_for<T, 16, true>(in, out, g, k0, c1, sh, table, entries, s);
+    else launch_for<T, 16, false>(in, out, g, k0, c1, sh, table, entries, s);
   }
   MXS_HIP_CHECK_LAUNCH();
 }
@@ -161,11 +152,9 @@ void stencil5_chunk_pass(const T* in, T* out, const TileGeom& g, const Stencil5C
 template bool chunk_pass_shape<float>(const TileGeom&, int, const Stencil5Coeffs&, ChunkPassShape*);
 template bool chunk_pass_shape<double>(const TileGeom&, int, const Stencil5Coeffs&, ChunkPassShape*);
 template void stencil5_chunk_pass<float>(const float*, float*, const TileGeom&, const Stencil5Coeffs&,
-                                         const ChunkPassShape&, const PassChunk*, int, hipStream_t,
-                                         PackTarget<float>*);
+                                         const ChunkPassShape&, const PassChunk*, int, hipStream_t);
 template void stencil5_chunk_pass<double>(const double*, double*, const TileGeom&, const Stencil5Coeffs&,
-                                          const ChunkPassShape&, const PassChunk*, int, hipStream_t,
-                                          PackTarget<double>*);
+                                          const ChunkPassShape&, const PassChunk*, int, hipStream_t);
 
 }  // namespace kernels
 }  // namespace mxs

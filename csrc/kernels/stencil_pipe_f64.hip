@@ -8,8 +8,8 @@ namespace detail {
 
 template <typename T, int S, bool WRAP, bool SUM>
 void launch_pipe(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
-                 T sc, hipStream_t s, PackTarget<T>* pk) {
-  launch_pipe_impl<T, S, WRAP, SUM>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s, pk);
+                 T sc, hipStream_t s) {
+  launch_pipe_impl<T, S, WRAP, SUM>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
 }
 
 template <typename T, int S, bool WRAP>
@@ -19,8 +19,7 @@ bool wide_pipe_ok(const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t
 
 #define MXS_INST_LAUNCH(S, WRAP, SUM)                                                                \
   template void launch_pipe<double, S, WRAP, SUM>(const double*, double*, const TileGeom&, index_t, index_t, index_t, \
-                                               index_t, double, double, double, hipStream_t, \
-                                               PackTarget<double>*);
+                                               index_t, double, double, double, hipStream_t);
 #define MXS_INST_PIPE(S)                                                                                 \
   MXS_INST_LAUNCH(S, true, false)                                                                        \
   MXS_INST_LAUNCH(S, true, true)                                                                         \

@@ -6,6 +6,7 @@
 
 #include <sstream>
 
+#include "mxs/core/error.hpp"
 #include "mxs/grid/layout.hpp"
 #include "mxs/grid/regions.hpp"
 #include "mxs/halo/plan.hpp"
@@ -156,17 +157,6 @@ PYBIND11_MODULE(_mxs_core, m) {
   m.def("make_halo_plan", &make_halo_plan, py::arg("topo"), py::arg("rank"), py::arg("tile"),
         py::arg("corners") = true, py::arg("loopback_self") = false);
   m.def(
-      "send_windows",
-      [](const HaloPlan& p) {
-        py::list out;
-        for (const auto& w : send_windows(p)) out.append(py::make_tuple(w.x0, w.y0, w.w, w.h, w.off));
-        return out;
-      },
-      py::arg("plan"),
-      "the plan's send windows (x0, y0, w, h, offset) in core coordinates, for the fused pack; [] when the plan "
-      "has self copies or no remote peer");
-
-  m.def(
       "paired_decision",
       [](std::vector<double> ratios, double min_gain) {
         const int n = int(ratios.size());
@@ -178,8 +168,44 @@ PYBIND11_MODULE(_mxs_core, m) {
         d["win"] = paired_win(med, iqr, n, min_gain);
         return d;
       },
-      py::arg("ratios"), py::arg("min_gain") = 0.03,
+      py::arg("ratios"), py::arg("min_gain") = 0.0,
       "the solver's opening / direct-halo rule on per-round ratios candidate / baseline (runtime/decision.hpp)");
+  m.def(
+      "opening_decision",
+      [](const std::vector<std::vector<double>>& serial, const std::vector<std::vector<std::vector<double>>>& cands,
+         double min_gain) {
+        // serial[rank][round], cands[rank][candidate][round]: what every rank timed.
+        // The solver agrees the element-wise max (one vector per rank), then decides.
+        MXS_CHECK(!serial.empty() && serial.size() == cands.size(), "one serial and one candidate set per rank");
+        const size_t nr = serial[0].size(), nc = cands[0].size();
+        std::vector<std::vector<double>> flat(serial.size());
+        for (size_t r = 0; r < serial.size(); ++r) {
+          MXS_CHECK(serial[r].size() == nr && cands[r].size() == nc, "ranks must time the same rounds and slots");
+          flat[r] = serial[r];
+          for (const auto& c : cands[r]) {
+            MXS_CHECK(c.size() == nr, "ranks must time the same rounds");
+            flat[r].insert(flat[r].end(), c.begin(), c.end());
+          }
+        }
+        const std::vector<double> v = elementwise_max(flat);
+        std::vector<std::vector<double>> cm(nc);
+        for (size_t c = 0; c < nc; ++c) cm[c].assign(v.begin() + (1 + c) * nr, v.begin() + (2 + c) * nr);
+        const RoundDecision d = decide_on_maxima(std::vector<double>(v.begin(), v.begin() + nr), cm, min_gain);
+        py::dict out;
+        out["best"] = d.best;
+        out["win"] = d.win;
+        out["ratio"] = d.ratio;
+        out["ratio_iqr"] = d.ratio_iqr;
+        out["notch"] = d.notch;
+        out["serial_ms"] = d.baseline_ms;
+        out["candidate_ms"] = d.candidate_ms;
+        out["ratios"] = d.ratios;
+        return out;
+      },
+      py::arg("serial"), py::arg("candidates"), py::arg("min_gain") = 0.0,
+      "StencilSolver::choose_opening's collective rule: per-round maxima over ranks, paired ratios of the maxima, "
+      "the lowest notch among candidates (runtime/decision.hpp); missing slots: kMissingSample");
+  m.attr("MISSING_SAMPLE") = kMissingSample;
   m.def("balanced_starts", &kernels::balanced_starts, py::arg("groups"), py::arg("rows"), py::arg("blocks"),
         py::arg("fill"), "fill-aware linear starts of the pipeline workgroups' shares (blocks + 1 entries)");
   // Interior-first (halo-last) schedule of the multi-GPU opening super-step.

@@ -271,53 +271,13 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("dtype") = "f32", py::arg("stream") = 0, py::arg("variant") = "auto", py::arg("sum_form") = true,
       "S Jacobi steps over [x0, x1) x [y0, y1); sum_form: allow the sum form when c_center == c_neighbor");
   m.def(
-      "set_device_schedule",
-      [](const std::string& mode) {
-        unsigned f = hipDeviceScheduleAuto;
-        if (mode == "spin") f = hipDeviceScheduleSpin;
-        else if (mode == "yield") f = hipDeviceScheduleYield;
-        else if (mode == "blocking") f = hipDeviceScheduleBlockingSync;
-        else if (mode != "auto") throw std::invalid_argument("schedule must be spin, yield, blocking or auto");
-        const hipError_t e = hipSetDeviceFlags(f);
-        unsigned now = 0;
-        (void)hipGetDeviceFlags(&now);
-        (void)hipGetLastError();
-        return py::make_tuple(std::string(hipGetErrorName(e)), now);
-      },
-      py::arg("mode"),
-      "hipSetDeviceFlags for the current device: how host waits detect completion (spin = lowest latency); "
-      "returns (hip error name, flags now in effect)");
-  m.def(
       "streams_concurrent",
       [](std::uintptr_t a, std::uintptr_t b) { return kernels::streams_concurrent(strm(a), strm(b)); },
       py::arg("a"), py::arg("b"), py::call_guard<py::gil_scoped_release>(),
       "whether work on stream b runs while a kernel on stream a still runs (different hardware queues)");
   m.def(
-      "stencil5_tb_packed",
-      [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, double c0, double c1, std::uintptr_t send,
-         const std::vector<std::tuple<index_t, index_t, index_t, index_t, index_t>>& windows, const std::string& dt,
-         std::uintptr_t s) {
-        kernels::PackSegs segs;
-        MXS_CHECK(windows.size() <= size_t(kernels::kMaxPackSegs), "at most " << kernels::kMaxPackSegs << " windows");
-        for (const auto& w : windows)
-          segs.seg[segs.n++] = kernels::PackSeg{std::get<0>(w), std::get<1>(w), std::get<2>(w), std::get<3>(w),
-                                                std::get<4>(w)};
-        kernels::Stencil5Coeffs c{c0, c1, true};
-        if (parse_dtype(dt) == DType::F32) {
-          kernels::PackTarget<float> pk{ptr<float>(send), segs, false};
-          kernels::stencil5_tb<float>(ptr<float>(in), ptr<float>(out), g, steps, 0, g.width, 0, g.height, c, false,
-                                      strm(s), kernels::StencilVariant::Auto, &pk);
-          return pk.applied;
-        }
-        kernels::PackTarget<double> pk{ptr<double>(send), segs, false};
-        kernels::stencil5_tb<double>(ptr<double>(in), ptr<double>(out), g, steps, 0, g.width, 0, g.height, c, false,
-                                     strm(s), kernels::StencilVariant::Auto, &pk);
-        return pk.applied;
-      },
-      py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("steps"), py::arg("c_center"), py::arg("c_neighbor"),
-      py::arg("send"), py::arg("windows"), py::arg("dtype") = "f32", py::arg("stream") = 0,
-      "the whole-core S-step pass with the fused halo pack into `send` (windows: send_windows(plan)); returns "
-      "whether the pass took it (a pipeline form)");
+      "spin_delay", [](double us, std::uintptr_t s) { kernels::spin_delay(us, strm(s)); }, py::arg("us"),
+      py::arg("stream") = 0, "a single-wave kernel holding `stream` for `us` microseconds (wire-time rehearsal)");
   m.def(
       "stencil5_rect",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1,
@@ -458,14 +418,13 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        const std::vector<float>& box_w, const std::string& variant, bool fuse_periodic, int time_block,
                        py::object bootstrap, int graph_supersteps, bool sum_form, const std::string& direct_halo,
                        double graph_max_superstep_us, const std::string& opening, bool rehearse_peers,
-                       double min_gain, int halo_max_ctas, bool opening_graph, bool fused_pack,
-                       int main_priority, int side_priority) {
+                       double min_gain, int halo_max_ctas, int main_priority, int side_priority,
+                       double wire_delay_us) {
              SolverConfig cfg;
              cfg.main_priority = main_priority;
              cfg.side_priority = side_priority;
-             cfg.fused_pack = fused_pack;
              cfg.halo_max_ctas = halo_max_ctas;
-             cfg.opening_graph = opening_graph;
+             cfg.wire_delay_us = wire_delay_us;
              if (opening == "auto") cfg.opening = Opening::Auto;
              else if (opening == "serial") cfg.opening = Opening::Serial;
              else if (opening == "interior-first") cfg.opening = Opening::InteriorFirst;
@@ -506,8 +465,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("fuse_periodic") = true, py::arg("time_block") = 1, py::arg("bootstrap") = py::none(),
            py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = "off",
            py::arg("graph_max_superstep_us") = 150.0, py::arg("opening") = "auto", py::arg("rehearse_peers") = false,
-           py::arg("min_gain") = 0.03, py::arg("halo_max_ctas") = 0, py::arg("opening_graph") = false, py::arg("fused_pack") = false,
-           py::arg("main_priority") = -1, py::arg("side_priority") = 0,
+           py::arg("min_gain") = 0.0, py::arg("halo_max_ctas") = 0, py::arg("main_priority") = -1,
+           py::arg("side_priority") = 0, py::arg("wire_delay_us") = 0.0,
            py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")
@@ -529,15 +488,19 @@ PYBIND11_MODULE(_mxs_hip, m) {
                d["ratio_iqr"] = s.opening_ratio_iqr();
                d["samples"] = s.opening_samples();
                d["outer_wgs"] = s.halo_last_outer_wgs(s.time_block());
-               // This rank's paired ratios per candidate outer set (diagnostics).
-               py::list rs;
+               // Paired ratios of the per-round maxima over ranks per candidate
+               // outer set, and this rank's own ratios (diagnostics).
+               py::list rs, ls;
                for (const auto& c : s.opening_ratio_samples()) rs.append(py::make_tuple(c.first, c.second));
+               for (const auto& c : s.opening_local_ratio_samples()) ls.append(py::make_tuple(c.first, c.second));
                d["candidate_ratios"] = rs;
+               d["local_candidate_ratios"] = ls;
+               d["agreement"] = s.agreement_path();
                return d;
              });
            },
-           "prepare()'s opening decision: the worst-rank median paired ratio interior-first / serial and its "
-           "IQR it was taken from, and the medians (ms; 0 = not measured)")
+           "prepare()'s opening decision: the median paired ratio of the per-round maxima over ranks, "
+           "interior-first / serial, its IQR, and the medians of the maxima (ms; 0 = not measured)")
       .def("direct_state", [](SolverHandle& h) { return h.visit([](auto& s) { return s.direct_state(); }); },
            "direct halo: '' (not configured), on, pending validation, validated: ..., rejected: ...")
       .def("direct_times",
@@ -549,6 +512,14 @@ PYBIND11_MODULE(_mxs_hip, m) {
           "inject_direct_mismatch",
           [](SolverHandle& h, bool on) { h.visit([on](auto& s) { s.inject_direct_mismatch(on); }); },
           py::arg("on") = true, "fault injection: corrupt one received cell of the direct push before validation")
+      .def(
+          "inject_direct_skip_wait",
+          [](SolverHandle& h, bool on) { h.visit([on](auto& s) { s.inject_direct_skip_wait(on); }); },
+          py::arg("on") = true, "fault injection: the validation's direct schedule skips its first wait on this rank")
+      .def("agreement_path", [](SolverHandle& h) { return h.visit([](auto& s) { return s.agreement_path(); }); },
+           "how collective agreements travel: host allgather, rccl all-reduce or none (one rank)")
+      .def("wire_delay_us", [](SolverHandle& h) { return h.visit([](auto& s) { return s.wire_delay_us(); }); },
+           "rehearsal wire time added after each RCCL transfer (us)")
       .def("halo_max_ctas", [](SolverHandle& h) { return h.visit([](auto& s) { return s.halo_max_ctas(); }); },
            "CTA cap of the halo's RCCL communicator (0: RCCL's default)")
       .def("halo_comm_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.halo_comm_note(); }); })
@@ -557,14 +528,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            "abort the halo's own RCCL communicator (halo_max_ctas), e.g. from a watchdog thread")
       .def("stream_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.stream_note(); }); },
            "the side stream's hardware-queue check (two-stream schedules)")
-      .def("fused_pack", [](SolverHandle& h) { return h.visit([](auto& s) { return s.fused_pack(); }); },
-           "whether the passes write the send bands into the exchange's send buffer (SolverConfig::fused_pack)")
       .def("last_run_forks", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_forks(); }); })
-      .def("last_run_fused_packs",
-           [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_fused_packs(); }); },
-           "exchanges of the last run() whose pack was fused into the preceding pass")
-      .def("opening_graph_state",
-           [](SolverHandle& h) { return h.visit([](auto& s) { return s.opening_graph_state(); }); })
       .def("last_run_opening", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_opening(); }); },
            "opening of the last run(): interior-first, serial, fresh, fused, direct, overlap or ''")
       .def(

@@ -113,6 +113,7 @@ void HaloExchanger<T>::transfer(hipStream_t stream) {
   for (const auto& m : plan_.recvs) comm_->recv<T>(recv_.get() + m.offset, size_t(m.count), m.peer, stream);
   for (const auto& m : plan_.sends) comm_->send<T>(send_.get() + m.offset, size_t(m.count), m.peer, stream);
   comm_->group_end();
+  if (wire_delay_us_ > 0) kernels::spin_delay(wire_delay_us_, stream);
 }
 
 template <typename T>
@@ -129,24 +130,6 @@ void HaloExchanger<T>::exchange(T* tile, hipStream_t stream) {
   pack(tile, stream);
   transfer(stream);
   unpack(tile, stream);
-}
-
-template <typename T>
-void HaloExchanger<T>::exchange_packed(T* tile, hipStream_t stream) {
-  MXS_TRACE_RANGE("halo.exchange_packed");
-  transfer(stream);
-  unpack(tile, stream);
-}
-
-template <typename T>
-bool HaloExchanger<T>::pack_windows(const TileGeom& g, kernels::PackSegs* out) const {
-  if (!(g == plan_.tile)) return false;
-  const std::vector<SendWindow> ws = send_windows(plan_);
-  if (ws.empty() || ws.size() > size_t(kernels::kMaxPackSegs)) return false;
-  kernels::PackSegs p;
-  for (const auto& w : ws) p.seg[p.n++] = kernels::PackSeg{w.x0, w.y0, w.w, w.h, w.off};
-  *out = p;
-  return true;
 }
 
 template class HaloExchanger<float>;

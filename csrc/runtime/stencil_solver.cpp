@@ -87,6 +87,11 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
     }
   }
   ex_ = std::make_unique<HaloExchanger<T>>(plan, cfg_.backend, comm_, &boot);
+  if (cfg_.wire_delay_us > 0) {
+    MXS_CHECK(world_ == 1 && cfg_.loopback_self && cfg_.backend == HaloBackend::Rccl,
+              "wire_delay_us is a one-GPU rehearsal option (one rank, RCCL loopback)");
+    ex_->set_wire_delay_us(cfg_.wire_delay_us);
+  }
   const bool all_self_nbrs = plan.sends.empty();
   if (cfg_.kind == StencilKind::Jacobi5 && !all_self_nbrs) {
     if (cfg_.direct == DirectHalo::On && cfg_.backend == HaloBackend::Ipc) {
@@ -114,15 +119,6 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   constexpr int N = 16 / int(sizeof(T));
   fused_ = cfg_.fuse_periodic_self && all_self && cfg_.kind == StencilKind::Jacobi5 && tile_.width % N == 0 &&
            kernels::stencil5_periodic_supported<T>(tile_);
-  // Fused halo pack: the plan's send windows as core rectangles (a per-rank
-  // property: it changes which launches run, not the collectives).
-  if (cfg_.fused_pack && cfg_.kind == StencilKind::Jacobi5 && !fused_) {
-    kernels::PackSegs segs;
-    if (ex_->pack_windows(tile_, &segs) && kernels::pack_segs_ok<T>(tile_, segs)) {
-      pack_.send = ex_->send_buffer();
-      pack_.segs = segs;
-    }
-  }
   // Interior-first opening: RCCL with a wire transfer, the tuned kernel forms,
   // every edge a neighbour's (time blocking), the thin-strip overlap off.
   halo_last_allowed_ = cfg_.opening != Opening::Serial && cfg_.backend == HaloBackend::Rccl && !plan.sends.empty() &&
@@ -188,6 +184,10 @@ StencilSolver<T>::~StencilSolver() {
   }
   (void)hipStreamSynchronize(main_.get());
   (void)hipStreamSynchronize(side_.get());
+  // Executables holding captured RCCL operations go before the halo's own
+  // communicator (halo_comm_, declared earlier, is destroyed after them otherwise).
+  graphs_.clear();
+  halo_lasts_.clear();
 }
 
 template <typename T>
@@ -203,37 +203,6 @@ void StencilSolver<T>::update(const T* in, T* out, int steps, index_t c0, index_
   } else {
     kernels::stencil5_rect<T>(in, out, tile_, c0, c1, r0, r1, cfg_.coeffs, s);
   }
-}
-
-template <typename T>
-void StencilSolver<T>::core_pass(T* cur, T* nxt, int S, hipStream_t s, bool pack) {
-  if (pack && pack_.send && cfg_.kind == StencilKind::Jacobi5 && S > 1) {
-    kernels::PackTarget<T> pk = pack_;
-    kernels::stencil5_tb<T>(cur, nxt, tile_, S, 0, tile_.width, 0, tile_.height, cfg_.coeffs, false, s, cfg_.variant,
-                            &pk);
-    note_written(nxt, pk.applied);
-    return;
-  }
-  update(cur, nxt, S, 0, tile_.width, 0, tile_.height, s);
-  note_written(nxt, false);
-}
-
-template <typename T>
-void StencilSolver<T>::exchange(T* tile, hipStream_t s) {
-  if (pack_.send && packed_ == tile) {
-    ex_->exchange_packed(tile, s);
-    ++last_fused_packs_;
-    return;
-  }
-  ex_->exchange(tile, s);
-  packed_ = tile;  // the pack launch wrote tile's bands
-}
-
-template <typename T>
-void StencilSolver<T>::ensure_packed(T* tile, hipStream_t s) {
-  if (!pack_.send || packed_ == tile) return;
-  ex_->pack(tile, s);
-  packed_ = tile;
 }
 
 // Stream roles: the MAIN stream (the capture origin, high priority) carries the
@@ -253,7 +222,6 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
   if (direct_on_) {  // the neighbours pushed cur's ghost ring after their previous pass
     direct_->wait(m);
     update(cur, nxt, S, 0, w, 0, h, m);
-    note_written(nxt, false);
     direct_->push(nxt, m);
     return;
   }
@@ -262,14 +230,12 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
     // sees to it), then the exchange of its output. The pass is on the GPU
     // before the host has enqueued the RCCL group (~25 us of host time that
     // a pre-exchange super-step leaves the GPU idle for).
-    core_pass(cur, nxt, S, m);  // writes nxt's send bands too when the pack is fused
+    core_pass(cur, nxt, S, m);
     ex_->set_copy_block(0);  // alone on the GPU: the default (256-thread) copies
-    exchange(nxt, m);
+    ex_->exchange(nxt, m);
     return;
   }
-  // The thin-strip overlap exchanges before the pass and splits the pass into
-  // launches that do not pack: explicit packs.
-  note_written(nxt, false);
+  // The thin-strip overlap: the exchange of cur under the interior.
   const index_t d = std::max(radius_, S);  // dependency depth of the super-step
   constexpr index_t N = 16 / index_t(sizeof(T));
   // Temporally blocked Jacobi: the kernels take any vector-aligned column range,
@@ -283,7 +249,6 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
     update(cur, nxt, S, dl, dr, d, h - d, side);
     interior_.record(side);
     ex_->exchange(cur, m);
-    packed_ = cur;
     update(cur, nxt, S, 0, w, 0, d, m);
     update(cur, nxt, S, 0, w, h - d, h, m);
     update(cur, nxt, S, 0, dl, d, h - d, m);
@@ -296,7 +261,6 @@ void StencilSolver<T>::enqueue_block(T* cur, T* nxt, int S) {
   update(cur, nxt, S, 0, w, d, h - d, side);  // interior (its edge columns are redone below)
   interior_.record(side);
   ex_->exchange(cur, m);
-  packed_ = cur;
   interior_.wait_on(m);
   update(cur, nxt, S, 0, w, 0, d, m);
   update(cur, nxt, S, 0, w, h - d, h, m);
@@ -335,13 +299,6 @@ bool StencilSolver<T>::capture(GraphSet& gs) {
       return false;
     }
     bool ok = true;
-    // The captured launches must not depend on what the send buffer holds when
-    // a replay starts: capture from "unknown" (a super-step packs before it
-    // exchanges unless its own pass fused the pack) and record the state a
-    // replay leaves.
-    T* const saved = packed_;
-    const int fused_before = last_fused_packs_;
-    packed_ = nullptr;
     try {
       for (int c = 0; c < gs.chain; ++c) {  // chain consecutive super-steps per graph
         enqueue_block(a, b, gs.S);
@@ -351,10 +308,6 @@ bool StencilSolver<T>::capture(GraphSet& gs) {
       graph_status_ = std::string("capture failed: ") + e.what();
       ok = false;
     }
-    gs.packed_after[k] = packed_;
-    gs.fused_packs = last_fused_packs_ - fused_before;
-    packed_ = saved;
-    last_fused_packs_ = fused_before;
     const hipError_t end = hipStreamEndCapture(main_.get(), &g);
     if (!ok || end != hipSuccess || g == nullptr) {
       (void)hipGetLastError();
@@ -451,8 +404,6 @@ void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
       MXS_TRACE_RANGE("stencil.graph_launch");
       const int k = cur_ == buf_a_ ? 0 : 1;
       gs->g[k].launch(main_.get());
-      packed_ = gs->packed_after[k];
-      last_fused_packs_ += gs->fused_packs;
       if (gs->chain % 2) std::swap(cur_, nxt_);  // an odd chain ends on the other buffer
     }
   }
@@ -474,9 +425,7 @@ template <typename T>
 void StencilSolver<T>::enqueue_bare_pass(T* cur, T* nxt, int S) {
   MXS_TRACE_RANGE("stencil.superstep_bare");
   if (direct_on_) direct_->wait(main_.get());  // the neighbours' pushes of cur's ring
-  // With the fused pack the bare pass leaves its send bands packed: the next
-  // call's priming exchange is RCCL + unpack.
-  core_pass(cur, nxt, S, main_.get(), !direct_on_);
+  core_pass(cur, nxt, S, main_.get());
 }
 
 // Direct halo: every pass pushes its output bands, so the current tile's ghost
@@ -507,18 +456,22 @@ void StencilSolver<T>::ensure_range(bool collective) {
   // same evaluation form (the result must not depend on the decomposition):
   // at the first check and in every collective call (prepare, warm,
   // profile_window). A run() after one rank alone changed its field
-  // (field_changed() is per rank) re-measures locally: that rank may leave the
-  // sum form on its own (numerically safe, only the rounding differs) until
-  // the next collective call agrees again.
+  // (field_changed() is per rank) re-measures locally, and may only switch
+  // the sum form OFF on that rank (numerically safe, only the rounding
+  // differs): its own maximum does not bound what the neighbours' exchanges
+  // write into its ghost ring, so switching back on waits for the next
+  // collective agreement.
   double md = local_absmax_;
+  bool agreed = world_ <= 1;
   if (world_ > 1 && (collective || !range_agreed_)) {
     std::vector<double> v{md};
     agree_max(v, "sum-form range agreement");
     md = v[0];
     range_agreed_ = true;
+    agreed = true;
   }
   const double bound = double(std::numeric_limits<T>::max()) / 4.0 / std::pow(5.0, double(block_));
-  const bool ok = std::isfinite(md) && md < bound;
+  const bool ok = std::isfinite(md) && md < bound && (agreed || cfg_.coeffs.sum_form);
   if (ok == cfg_.coeffs.sum_form) return;
   cfg_.coeffs.sum_form = ok;
   sum_note_ = ok ? "" : "sum form off: max|u| * 5^S would overflow the element type (per-step form)";
@@ -546,7 +499,6 @@ void StencilSolver<T>::run(int iters) {
   MXS_TRACE_RANGE("stencil.run");
   last_blocks_.clear();
   last_exchanges_ = 0;
-  last_fused_packs_ = 0;
   last_forks_ = 0;
   last_opening_.clear();
   if (iters <= 0) return;
@@ -595,53 +547,61 @@ void StencilSolver<T>::wait_idle(const char* phase) {
 template <typename T>
 void StencilSolver<T>::agree_max(std::vector<double>& v, const char* phase) {
   if (world_ <= 1 || v.empty()) return;
-  if (comm_) {
-    if (agree_buf_.size() < index_t(v.size())) agree_buf_.reset(index_t(v.size()));
-    const size_t bytes = v.size() * sizeof(double);
-    MXS_HIP_CHECK(hipMemcpyAsync(agree_buf_.get(), v.data(), bytes, hipMemcpyHostToDevice, main_.get()));
-    comm_->allreduce_max<double>(agree_buf_.get(), agree_buf_.get(), v.size(), main_.get());
-    MXS_HIP_CHECK(hipMemcpyAsync(v.data(), agree_buf_.get(), bytes, hipMemcpyDeviceToHost, main_.get()));
-    wait_idle(phase);
+  if (cfg_.bootstrap) {  // the host allgather: the path the one-GPU multi-rank tests run too
+    std::string blob(v.size() * sizeof(double), '\0');
+    std::memcpy(blob.data(), v.data(), blob.size());
+    std::vector<std::string> parts;
+    try {
+      parts = cfg_.bootstrap(blob);
+    } catch (const std::exception& e) {
+      raise_error(std::string(phase) + ": host agreement failed: " + e.what());
+    }
+    MXS_CHECK(int(parts.size()) == world_, phase << ": host agreement returned " << parts.size() << " of "
+                                                 << world_ << " ranks");
+    for (const auto& p : parts) {
+      MXS_CHECK(p.size() == blob.size(), phase << ": ranks disagree on the agreement's length");
+      for (size_t i = 0; i < v.size(); ++i) {
+        double x;
+        std::memcpy(&x, p.data() + i * sizeof(double), sizeof(double));
+        v[i] = std::max(v[i], x);
+      }
+    }
     return;
   }
-  MXS_CHECK(static_cast<bool>(cfg_.bootstrap),
-            phase << ": " << world_ << " ranks but neither an RCCL communicator nor a host allgather to agree on");
-  std::string blob(v.size() * sizeof(double), '\0');
-  std::memcpy(blob.data(), v.data(), blob.size());
-  std::vector<std::string> parts;
-  try {
-    parts = cfg_.bootstrap(blob);
-  } catch (const std::exception& e) {
-    raise_error(std::string(phase) + ": host agreement failed: " + e.what());
-  }
-  for (const auto& p : parts) {
-    MXS_CHECK(p.size() == blob.size(), phase << ": ranks disagree on the agreement's length");
-    for (size_t i = 0; i < v.size(); ++i) {
-      double x;
-      std::memcpy(&x, p.data() + i * sizeof(double), sizeof(double));
-      v[i] = std::max(v[i], x);
-    }
-  }
+  MXS_CHECK(comm_ != nullptr,
+            phase << ": " << world_ << " ranks but neither a host allgather nor an RCCL communicator to agree on");
+  if (agree_buf_.size() < index_t(v.size())) agree_buf_.reset(index_t(v.size()));
+  const size_t bytes = v.size() * sizeof(double);
+  MXS_HIP_CHECK(hipMemcpyAsync(agree_buf_.get(), v.data(), bytes, hipMemcpyHostToDevice, main_.get()));
+  comm_->allreduce_max<double>(agree_buf_.get(), agree_buf_.get(), v.size(), main_.get());
+  MXS_HIP_CHECK(hipMemcpyAsync(v.data(), agree_buf_.get(), bytes, hipMemcpyDeviceToHost, main_.get()));
+  wait_idle(phase);
 }
 
 template <typename T>
 void StencilSolver<T>::device_barrier(const char* phase) {
   if (world_ <= 1) return;
+  if (comm_) {  // a device all-reduce releases every rank within microseconds of each other
+    if (agree_buf_.size() < 1) agree_buf_.reset(1);
+    comm_->allreduce_max<double>(agree_buf_.get(), agree_buf_.get(), 1, main_.get());
+    wait_idle(phase);
+    return;
+  }
   std::vector<double> v{0.0};
   agree_max(v, phase);
 }
 
 // Opening::Auto, once (the first prepare() with a form at its depth): the
 // call's opening super-step timed from drained streams after a device barrier,
-// as a timed window sees it (host clock to both streams drained again; an
-// event recorded on main before the opening would itself force the fork the
-// opening skips): prime + pass against up to three interior-first outer sets
-// (the modelled one and one XCD step either side: where the outer workgroups
-// land decides the opening; on one box 32 / 40 / 48 measured 0.296 / 0.259 /
-// 0.431 ms against 0.269 serial, profiles/r03_halolast). Every rank times the
-// same 4 openings in the same order (a candidate it lacks is replaced by the
-// serial one: the same exchanges everywhere), then the medians and spreads are
-// agreed (worst rank) and every rank adopts the same decision.
+// as a timed window sees it: prime + pass against up to three interior-first
+// outer sets (the modelled one and one XCD step either side: where the outer
+// workgroups land decides the opening; on one box 32 / 40 / 48 measured
+// 0.296 / 0.259 / 0.431 ms against 0.269 serial, profiles/r03_halolast). Every
+// rank times the same 4 openings in the same order, one fixed slot per outer
+// set (model - 8, model, model + 8; a candidate a rank lacks is timed as the
+// serial opening, so every rank issues the same exchanges, and its slot is
+// marked missing). The ranks agree on the per-round maxima and decide on their
+// paired ratios (decision.hpp): every rank adopts the same decision.
 template <typename T>
 void StencilSolver<T>::choose_opening(int S) {
   if (!halo_last_allowed_ || cfg_.opening != Opening::Auto || !opening_choice_.empty()) return;
@@ -655,21 +615,18 @@ void StencilSolver<T>::choose_opening(int S) {
     opening_reason_ = "no rank has an interior-first form at depth " + std::to_string(S);
     return;
   }
-  std::vector<std::unique_ptr<HaloLastPass>> alt;
+  constexpr int kCands = 3;  // slots: model outer set, model - 8, model + 8 workgroups (one XCD step)
+  std::unique_ptr<HaloLastPass> alt[kCands];
+  HaloLastPass* cands[kCands] = {hl, nullptr, nullptr};
   if (hl && !experiment_env("MXS_HALO_LAST_WGS")) {
     const int m = hl->sched.outer.blocks;
-    for (int d : {-kXcds, kXcds}) {
-      const int k = m + d;
-      if (k >= 32 && k < hl->inner_shape.blocks + m) {
-        if (auto h = build_halo_last(S, k)) alt.push_back(std::move(h));
-      }
+    for (int c = 1; c < kCands; ++c) {
+      const int k = m + (c == 1 ? -kXcds : kXcds);
+      if (k >= 32 && k < hl->inner_shape.blocks + m && (alt[c] = build_halo_last(S, k))) cands[c] = alt[c].get();
     }
   }
-  std::vector<HaloLastPass*> cands;
-  if (hl) cands.push_back(hl);
-  for (auto& h : alt) cands.push_back(h.get());
   if (!ghost_fresh_) {
-    exchange(cur_, main_.get());
+    prime_exchange();
     ghost_fresh_ = true;
   }
   // GPU time of one opening, from drained streams after a device barrier and
@@ -677,11 +634,8 @@ void StencilSolver<T>::choose_opening(int S) {
   // sample runs at the clocks a window after warm() sees. The start event goes
   // on the stream that receives the opening's first launch (the side stream
   // for interior-first: an event on main would itself force the fork the
-  // opening skips), the end event on main after the join. Host-clock samples
-  // of the same openings spread by 15-18% (IQR) on one box; the GPU span
-  // still contains every gap the host leaves (RCCL's enqueue) after the first launch.
-  // The end is the later of an event on each stream, with no join between
-  // them: a window ends when both streams have drained (synchronize()), and a
+  // opening skips). The end is the later of an event on each stream, with no
+  // join between them: a window ends when both streams have drained, and a
   // cross-stream join (~15 us) would be charged to the interior-first opening
   // alone (it measured 1.0x serial that way, 0.92x as the window runs it).
   Event e0(true), e1(true), e2(true);
@@ -689,7 +643,6 @@ void StencilSolver<T>::choose_opening(int S) {
     join_side();
     enqueue_block(cur_, nxt_, S);
     join_side();
-    ensure_packed(cur_, main_.get());  // as a window finds it: the last pass packed the field's bands
     wait_idle("prepare: opening timing");
     device_barrier("prepare: opening timing");
     e0.record(starts_on_side ? side_.get() : main_.get());
@@ -699,82 +652,67 @@ void StencilSolver<T>::choose_opening(int S) {
     wait_idle("prepare: opening timing");
     return std::max(double(e1.since(e0)), double(e2.since(e0)));
   };
-  constexpr int kCands = 3, kReps = 21;  // round 0 warms every shape (20 paired rounds: the notch is 1.58 IQR / sqrt(20))
-  std::vector<double> t_serial;
-  std::vector<std::vector<double>> t_cand(kCands), ratio(kCands);
+  constexpr int kReps = 21;  // round 0 warms every shape (20 paired rounds: the notch is 1.58 IQR / sqrt(20))
+  constexpr int nr = kReps - 1;
+  // Per round: serial, then the three slots. v = [serial x nr, slot 0 x nr, slot 1 x nr, slot 2 x nr].
+  std::vector<double> v(size_t((1 + kCands) * nr), kMissingSample);
   for (int rep = 0; rep < kReps; ++rep) {
     const double serial = timed(false, [&] {
       prime_exchange();
       enqueue_bare_pass(cur_, nxt_, S);
     });
-    if (rep > 0) t_serial.push_back(serial);
-    for (size_t c = 0; c < size_t(kCands); ++c) {
-      const double ms = timed(c < cands.size(), [&] {
-        if (c < cands.size()) {
+    if (rep > 0) v[size_t(rep - 1)] = serial;
+    for (int c = 0; c < kCands; ++c) {
+      const double ms = timed(cands[c] != nullptr, [&] {
+        if (cands[c]) {
           enqueue_halo_last(cur_, nxt_, cands[c]);
         } else {
           prime_exchange();
           enqueue_bare_pass(cur_, nxt_, S);
         }
       });
-      if (rep > 0 && c < cands.size()) {
-        t_cand[c].push_back(ms);
-        ratio[c].push_back(ms / std::max(serial, 1e-9));  // paired with this round's serial sample
-      }
+      if (rep > 0 && cands[c]) v[size_t((1 + c) * nr + rep - 1)] = ms;
     }
   }
-  // The decision rests on the paired ratios (candidate / serial of the same
-  // round): the clock drifts between rounds by far more than the openings
-  // differ (IQR of either series alone 11% of a 0.29 ms opening on one box),
-  // and a round's two samples see the same clock. Agreed over ranks: the worst
-  // median ratio and the widest spread. Interior-first wins when the median
-  // ratio is at most 1 - min_gain and its notch (median + 1.58 IQR / sqrt(n),
-  // the 95% interval of a median) stays below 1.
-  constexpr double kMissing = 1e30;
-  std::vector<double> v(4 * kCands + 2, kMissing);
-  std::tie(v[0], v[1]) = median_iqr(t_serial);
-  for (size_t c = 0; c < cands.size(); ++c) {
-    v[2 + c] = median_iqr(t_cand[c]).first;
-    std::tie(v[2 + kCands + c], v[2 + 2 * kCands + c]) = median_iqr(ratio[c]);
+  // This rank's own paired ratios (diagnostics), then the agreed maxima.
+  opening_local_ratio_samples_.clear();
+  for (int c = 0; c < kCands; ++c) {
+    if (!cands[c]) continue;
+    std::vector<double> r(nr);
+    for (int i = 0; i < nr; ++i) r[size_t(i)] = v[size_t((1 + c) * nr + i)] / std::max(v[size_t(i)], 1e-12);
+    opening_local_ratio_samples_.emplace_back(cands[c]->sched.outer.blocks, std::move(r));
   }
   agree_max(v, "prepare: opening agreement");
-  // The candidate with the lowest notch (median + 1.58 IQR / sqrt(n)): a
-  // consistent 0.94 beats a median of 0.93 whose rounds spread to 1.2 (the
-  // outer set one XCD step above the model's measured that way, 4 solvers on
-  // one box, profiles/r04_fp/opening_probe.txt).
-  const int nr = kReps - 1;
-  size_t best = 0;
-  for (size_t c = 1; c < size_t(kCands); ++c)
-    if (median_notch(v[2 + kCands + c], v[2 + 2 * kCands + c], nr) <
-        median_notch(v[2 + kCands + best], v[2 + 2 * kCands + best], nr))
-      best = c;
-  const double serial = v[0], hlt = v[2 + best], r = v[2 + kCands + best], r_iqr = v[2 + 2 * kCands + best];
-  const int n = nr;
-  const double notch = median_notch(r, r_iqr, n);
-  const bool win = r < kMissing && paired_win(r, r_iqr, n, cfg_.min_gain);
-  opening_ms_[0] = serial;
-  opening_ms_[1] = hlt < kMissing ? hlt : 0.0;
-  opening_spread_[0] = v[1];
-  opening_spread_[1] = r < kMissing ? r_iqr : 0.0;
-  opening_ratio_ = r < kMissing ? r : 0.0;
-  opening_samples_ = n;
+  std::vector<double> base(v.begin(), v.begin() + nr);
+  std::vector<std::vector<double>> cand(kCands);
+  for (int c = 0; c < kCands; ++c) cand[size_t(c)].assign(v.begin() + (1 + c) * nr, v.begin() + (2 + c) * nr);
+  const RoundDecision d = decide_on_maxima(base, cand, cfg_.min_gain);
+  opening_ms_[0] = d.baseline_ms;
+  opening_ms_[1] = d.best >= 0 ? d.candidate_ms : 0.0;
+  opening_spread_[0] = d.baseline_iqr;
+  opening_spread_[1] = d.best >= 0 ? d.ratio_iqr : 0.0;
+  opening_ratio_ = d.best >= 0 ? d.ratio : 0.0;
+  opening_samples_ = nr;
   opening_ratio_samples_.clear();
-  for (size_t c = 0; c < cands.size(); ++c) opening_ratio_samples_.emplace_back(cands[c]->sched.outer.blocks, ratio[c]);
-  if (win && best > 0 && best - 1 < alt.size()) {  // keep the measured best outer set for S
+  for (int c = 0; c < kCands; ++c)
+    if (!d.ratios[size_t(c)].empty() && cands[c])
+      opening_ratio_samples_.emplace_back(cands[c]->sched.outer.blocks, d.ratios[size_t(c)]);
+  if (d.win && d.best > 0 && alt[d.best]) {  // keep the measured best outer set for S
     for (auto& h : halo_lasts_)
-      if (h->S == S) h = std::move(alt[best - 1]);
+      if (h->S == S) h = std::move(alt[d.best]);
   }
-  halo_last_on_ = win;
-  opening_choice_ = win ? "interior-first" : "serial";
-  char buf[320];
-  if (r >= kMissing) {
-    std::snprintf(buf, sizeof(buf), "no rank-wide interior-first candidate (serial median %.4f ms)", serial);
+  halo_last_on_ = d.win;
+  opening_choice_ = d.win ? "interior-first" : "serial";
+  char buf[360];
+  if (d.best < 0) {
+    std::snprintf(buf, sizeof(buf), "no rank-wide interior-first candidate (serial median %.4f ms)", d.baseline_ms);
   } else {
     std::snprintf(buf, sizeof(buf),
-                  "worst-rank paired ratio interior-first / serial over %d rounds (GPU event spans): median %.3f, "
-                  "IQR %.3f, notch %.3f (switch at <= %.3f with notch < 1); medians %.4f / %.4f ms: %s",
-                  n, r, r_iqr, notch, 1.0 - cfg_.min_gain, hlt, serial,
-                  win ? "interior-first" : "serial kept");
+                  "paired ratio of the per-round maxima over %d rank(s), interior-first / serial, %d rounds (GPU "
+                  "event spans): median %.3f, IQR %.3f, notch %.3f (switch at notch < %.3f); medians %.4f / %.4f "
+                  "ms: %s",
+                  world_, nr, d.ratio, d.ratio_iqr, d.notch, 1.0 - cfg_.min_gain, d.candidate_ms, d.baseline_ms,
+                  d.win ? "interior-first" : "serial kept");
   }
   opening_reason_ = buf;
 }
@@ -790,55 +728,85 @@ void StencilSolver<T>::poison_ghost(T* tile) {
   for (const auto& c : plan.self_copies) kernels::fill_region<T>(tile, c.dst, sentinel, main_.get());
 }
 
-// DirectHalo::Validate, once, inside prepare() (collective). (1) Bitwise: the
-// received ghost cells of the current tile after one exchange through the
-// backend (RCCL, or the IPC transport for ranks sharing a GPU) and after one
-// direct push, both from sentinel-filled rings, must be identical on every
-// rank (agreed). (2) Timing: the direct opening (push, wait, pass) against the
-// backend's opening (the chosen one), sampled like choose_opening and agreed.
-// Direct is switched on only if (1) holds everywhere and (2) wins by min_gain
-// beyond the spread. The current field is unchanged (its ring is re-exchanged).
+// DirectHalo::Validate, once, inside prepare() (collective). (1) Bitwise, over
+// kSteps super-steps from the current (random) field: the backend's schedule
+// (exchange, pass, ..., a final exchange) against the direct one started from
+// a sentinel-filled ring (push, then wait, pass, push per super-step, a final
+// wait), on the same buffers the backend's unpacks just wrote; the whole tiles,
+// ghost rings included, must be identical on every rank (agreed). A missing or
+// too-early wait shows up as sentinel values or stale bands in a later
+// super-step. (2) Timing: the direct opening (push, wait, pass) against the
+// backend's opening (the chosen one), per-round maxima over ranks, paired
+// ratios (decision.hpp). Direct is switched on only if (1) holds everywhere and
+// (2) wins. The current field is unchanged (restored, its ring re-exchanged).
 template <typename T>
 void StencilSolver<T>::validate_direct(int S) {
   if (!direct_ || cfg_.direct != DirectHalo::Validate || direct_state_ != "pending validation") return;
   MXS_TRACE_RANGE("stencil.validate_direct");
   hipStream_t m = main_.get();
   join_side();
-  if (!ref_.get()) ref_.reset(tile_.alloc_elems());
+  constexpr int kSteps = 3;
+  const index_t elems = tile_.alloc_elems();
+  const size_t bytes = size_t(elems) * sizeof(T);
+  if (!ref_.get()) ref_.reset(2 * elems);
   if (!diff_.get()) diff_.reset(1);
-  const size_t bytes = size_t(tile_.alloc_elems()) * sizeof(T);
+  T* const before = ref_.get();
+  T* const want = ref_.get() + elems;
+  const index_t w = tile_.width, h = tile_.height;
+  MXS_HIP_CHECK(hipMemcpyAsync(before, cur_, bytes, hipMemcpyDeviceToDevice, m));
+  T* a = cur_;
+  T* b = nxt_;
+  for (int k = 0; k < kSteps; ++k) {  // the backend's schedule
+    ex_->exchange(a, m);
+    update(a, b, S, 0, w, 0, h, m);
+    std::swap(a, b);
+  }
+  ex_->exchange(a, m);
+  MXS_HIP_CHECK(hipMemcpyAsync(want, a, bytes, hipMemcpyDeviceToDevice, m));
+  MXS_HIP_CHECK(hipMemcpyAsync(cur_, before, bytes, hipMemcpyDeviceToDevice, m));
   poison_ghost(cur_);
-  exchange(cur_, m);
-  MXS_HIP_CHECK(hipMemcpyAsync(ref_.get(), cur_, bytes, hipMemcpyDeviceToDevice, m));
-  poison_ghost(cur_);
+  a = cur_;
+  b = nxt_;
+  // Fault injection: a first pass that does not wait for the neighbours'
+  // pushes, made certain to lose the race (it completes before any rank pushes).
+  if (inject_skip_wait_) update(a, b, S, 0, w, 0, h, m);
   wait_idle("prepare: direct halo validation");
   device_barrier("prepare: direct halo validation");  // every ring poisoned before any push lands
-  direct_->push(cur_, m);
+  direct_->push(a, m);
+  for (int k = 0; k < kSteps; ++k) {  // the direct schedule
+    if (!(inject_skip_wait_ && k == 0)) {
+      direct_->wait(m);
+      update(a, b, S, 0, w, 0, h, m);
+    }
+    direct_->push(b, m);
+    std::swap(a, b);
+  }
   direct_->wait(m);
   if (inject_mismatch_) {  // fault injection: one received cell differs
     const HaloPlan& plan = ex_->plan();
     Array2D one = !plan.recvs.empty() ? plan.recvs[0].segments[0].region : plan.self_copies[0].dst;
     one.width = one.height = 1;
-    kernels::fill_region<T>(cur_, one, T(42), m);
+    kernels::fill_region<T>(a, one, T(42), m);
   }
-  kernels::count_diff(cur_, ref_.get(), index_t(bytes), diff_.get(), m);
+  kernels::count_diff(a, want, index_t(bytes), diff_.get(), m);
   unsigned diff = 0;
   MXS_HIP_CHECK(hipMemcpyAsync(&diff, diff_.get(), sizeof(unsigned), hipMemcpyDeviceToHost, m));
   wait_idle("prepare: direct halo validation");
   std::vector<double> bad{double(diff)};
-  agree_max(bad, "prepare: direct halo validation");
-  exchange(cur_, m);  // whatever the push delivered, the ring is the backend's again
+  agree_max(bad, "prepare: direct halo validation");  // also: every rank's last pushes have landed
+  MXS_HIP_CHECK(hipMemcpyAsync(cur_, before, bytes, hipMemcpyDeviceToDevice, m));
+  ex_->exchange(cur_, m);  // the ring is the backend's again
   ghost_fresh_ = true;
   if (bad[0] != 0.0) {
-    direct_state_ = "rejected: the direct push differs from the " + std::string(cfg_.backend == HaloBackend::Rccl
-                                                                                  ? "RCCL" : "IPC") +
-                    " exchange in " + std::to_string(int(bad[0])) + " words on some rank";
+    direct_state_ = "rejected: the direct push differs from the " +
+                    std::string(cfg_.backend == HaloBackend::Rccl ? "RCCL" : "IPC") + " exchange in " +
+                    std::to_string(long(bad[0])) + " words on some rank over " + std::to_string(kSteps) +
+                    " super-steps";
     wait_idle("prepare: direct halo validation");
     return;
   }
   // Timing (GPU events, as choose_opening), from drained streams after a
-  // barrier, each sample behind a state-preserving pass of its own path
-  // (clocks), medians of 8 + IQR, agreed.
+  // barrier, each sample behind a state-preserving pass of its own path.
   Event e0(true), e1(true), e2(true);
   auto timed = [&](bool starts_on_side, auto&& warm, auto&& enqueue) {
     join_side();
@@ -853,16 +821,16 @@ void StencilSolver<T>::validate_direct(int S) {
     wait_idle("prepare: direct halo timing");
     return std::max(double(e1.since(e0)), double(e2.since(e0)));
   };
-  constexpr int kReps = 13;
-  std::vector<double> t_backend, t_direct, ratio;
-  const index_t w = tile_.width, h = tile_.height;
+  auto direct_opening = [&] {  // the priming push, the wait for the neighbours' pushes, the pass
+    direct_->push(cur_, m);
+    direct_->wait(m);
+    update(cur_, nxt_, S, 0, w, 0, h, m);
+  };
+  constexpr int kReps = 13, nr = kReps - 1;
+  std::vector<double> v(size_t(2 * nr), 0.0);  // [backend x nr, direct x nr]
   for (int rep = 0; rep < kReps; ++rep) {
     const double tb = timed(
-        halo_last_on_ && halo_last_pass(S, false),
-        [&] {
-          enqueue_block(cur_, nxt_, S);
-          ensure_packed(cur_, m);
-        },
+        halo_last_on_ && halo_last_pass(S, false), [&] { enqueue_block(cur_, nxt_, S); },
         [&] {
           if (halo_last_on_) {
             enqueue_opening(S, false);
@@ -871,47 +839,27 @@ void StencilSolver<T>::validate_direct(int S) {
             core_pass(cur_, nxt_, S, m);
           }
         });
-    // Direct: the priming push of the current bands, the wait for the
-    // neighbours' pushes, the pass (a call's bare last super-step).
-    const double td = timed(
-        false,
-        [&] {
-          direct_->push(cur_, m);
-          direct_->wait(m);
-          update(cur_, nxt_, S, 0, w, 0, h, m);
-          note_written(nxt_, false);
-        },
-        [&] {
-          direct_->push(cur_, m);
-          direct_->wait(m);
-          update(cur_, nxt_, S, 0, w, 0, h, m);
-          note_written(nxt_, false);
-        });
+    const double td = timed(false, direct_opening, direct_opening);
     if (rep > 0) {
-      t_backend.push_back(tb);
-      t_direct.push_back(td);
-      ratio.push_back(td / std::max(tb, 1e-9));  // paired: the same round's clock (choose_opening)
+      v[size_t(rep - 1)] = tb;
+      v[size_t(nr + rep - 1)] = td;
     }
   }
-  std::vector<double> v(4);
-  v[0] = median_iqr(t_backend).first;
-  v[1] = median_iqr(t_direct).first;
-  std::tie(v[2], v[3]) = median_iqr(ratio);
   agree_max(v, "prepare: direct halo timing");
-  direct_ms_[0] = v[0];
-  direct_ms_[1] = v[1];
-  const int n = kReps - 1;
-  const double notch = median_notch(v[2], v[3], n);
-  const bool win = paired_win(v[2], v[3], n, cfg_.min_gain);
+  const RoundDecision d = decide_on_maxima(std::vector<double>(v.begin(), v.begin() + nr),
+                                           {std::vector<double>(v.begin() + nr, v.end())}, cfg_.min_gain);
+  direct_ms_[0] = d.baseline_ms;
+  direct_ms_[1] = d.candidate_ms;
   char buf[320];
   std::snprintf(buf, sizeof(buf),
-                "bitwise equal on every rank; worst-rank paired ratio direct / %s over %d rounds: median %.3f, "
-                "IQR %.3f, notch %.3f; medians %.4f / %.4f ms",
-                cfg_.backend == HaloBackend::Rccl ? "RCCL" : "IPC", n, v[2], v[3], notch, v[1], v[0]);
-  direct_state_ = std::string(win ? "validated: " : "rejected (slower): ") + buf;
+                "bitwise equal on every rank over %d super-steps; paired ratio of the per-round maxima, direct / "
+                "%s, %d rounds: median %.3f, IQR %.3f, notch %.3f; medians %.4f / %.4f ms",
+                kSteps, cfg_.backend == HaloBackend::Rccl ? "RCCL" : "IPC", nr, d.ratio, d.ratio_iqr, d.notch,
+                d.candidate_ms, d.baseline_ms);
+  direct_state_ = std::string(d.win ? "validated: " : "rejected (slower): ") + buf;
   // The timing pushes advanced the direct epochs and wrote the scratch
   // buffer's neighbours only; the current ring is the backend's (fresh).
-  if (win) {
+  if (d.win) {
     direct_on_ = true;
     ghost_fresh_ = false;
     graphs_.clear();  // captured for the backend's schedule
@@ -976,20 +924,6 @@ std::unique_ptr<typename StencilSolver<T>::HaloLastPass> StencilSolver<T>::build
   hl->inner_shape.blocks = hl->sched.inner.blocks;
   hl->outer_shape = shape;
   hl->outer_shape.blocks = hl->sched.outer.blocks;
-  // The fused pack goes to the outer launch only if no inner chunk stores a
-  // cell of a send window (a ghost ring deeper than the pass could put one
-  // there, and the inner launch runs while RCCL reads the send buffer).
-  if (pack_.send) {
-    hl->outer_packs = true;
-    for (const auto& c : hl->sched.inner.table) {
-      if (c.r1 <= c.r0) continue;
-      const index_t x0 = index_t(c.group) * shape.owg, x1 = std::min<index_t>(x0 + shape.owg, tile_.width);
-      for (int k = 0; k < pack_.segs.n; ++k) {
-        const kernels::PackSeg& q = pack_.segs.seg[k];
-        if (x0 < q.x0 + q.w && q.x0 < x1 && c.r0 < q.y0 + q.h && q.y0 < c.r1) hl->outer_packs = false;
-      }
-    }
-  }
   hl->inner_table.reset(index_t(hl->sched.inner.table.size()));
   hl->outer_table.reset(index_t(hl->sched.outer.table.size()));
   MXS_HIP_CHECK(hipMemcpy(hl->inner_table.get(), hl->sched.inner.table.data(), hl->inner_table.bytes(),
@@ -1035,11 +969,6 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
   MXS_TRACE_RANGE("stencil.superstep_halo_last");
   hipStream_t m = main_.get(), side = side_.get();
   join_side();
-  if (!marks && cfg_.opening_graph && !hl->chain_tried) {
-    // Captured at first use (prepare()'s untimed warm pass of the opening).
-    hl->chain_tried = true;
-    hl->chain_ok = capture_chain(hl);
-  }
   // The inner launch reads cur: it must follow everything enqueued on main.
   // When main has drained (a call after synchronize()) the fork is skipped: a
   // cross-stream wait costs ~15 us of queue-to-queue latency, and the timed
@@ -1051,166 +980,29 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
     ++last_forks_;
   }
   if (marks) marks->mark("side:start", side);
-  // The inner chunks never take the fused pack: RCCL reads the send buffer
-  // while they run.
   kernels::stencil5_chunk_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->inner_shape, hl->inner_table.get(),
                                   hl->sched.inner.entries, side);
   if (marks) marks->mark("side:inner chunks", side);
   side_pending_ = true;
-  const bool fuse = hl->outer_packs && pack_.send != nullptr;
-  if (!marks && hl->chain_ok) {
-    // The main stream's chain from its graph: one launch instead of the RCCL
-    // group calls and the kernel launches. Captured without the pack launch
-    // when the outer chunks fuse it: the send buffer must hold cur's bands.
-    if (fuse) {
-      if (packed_ == cur) ++last_fused_packs_;
-      ensure_packed(cur, m);
-    }
-    hl->chain[cur == buf_a_ ? 0 : 1].launch(m);
-    packed_ = fuse ? nxt : cur;
-    return;
-  }
   const int copy_wgs = halo_last_copy_wgs();
   ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
   ex_->set_copy_grid(copy_wgs);
   if (marks) {
     marks->mark("main:start", m);
-    if (pack_.send && packed_ == cur) {  // the pass before packed cur's bands
-      ++last_fused_packs_;
-    } else {
-      ex_->pack(cur, m);
-      marks->mark("main:pack", m);
-      packed_ = cur;
-    }
+    ex_->pack(cur, m);
+    marks->mark("main:pack", m);
     ex_->transfer(m);
     marks->mark("main:rccl", m);
     ex_->unpack(cur, m);
     marks->mark("main:unpack", m);
   } else {
-    exchange(cur, m);
+    ex_->exchange(cur, m);
   }
   ex_->set_copy_grid(0);
   ex_->set_copy_block(0);
-  kernels::PackTarget<T> pk = pack_;
   kernels::stencil5_chunk_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->outer_shape, hl->outer_table.get(),
-                                  hl->sched.outer.entries, m, fuse ? &pk : nullptr);
-  note_written(nxt, fuse && pk.applied);
+                                  hl->sched.outer.entries, m);
   if (marks) marks->mark("main:outer chunks", m);
-}
-
-template <typename T>
-bool StencilSolver<T>::capture_chain(HaloLastPass* hl) {
-  MXS_TRACE_RANGE("stencil.graph_capture_opening");
-  hipStream_t m = main_.get();
-  const bool fuse = hl->outer_packs && pack_.send != nullptr;
-  T* const saved = packed_;
-  const int fused_before = last_fused_packs_;
-  bool all = true;
-  for (int k = 0; k < 2 && all; ++k) {
-    T* cur = k == 0 ? buf_a_ : buf_b_;
-    T* nxt = k == 0 ? buf_b_ : buf_a_;
-    hipGraph_t g = nullptr;
-    if (hipStreamBeginCapture(m, hipStreamCaptureModeThreadLocal) != hipSuccess) {
-      (void)hipGetLastError();
-      all = false;
-      break;
-    }
-    bool ok = true;
-    try {
-      const int copy_wgs = halo_last_copy_wgs();
-      // With the fused pack the chain starts at the transfer (the launch site
-      // sees to the send buffer), else with the pack launch.
-      packed_ = fuse ? cur : nullptr;
-      ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
-      ex_->set_copy_grid(copy_wgs);
-      exchange(cur, m);
-      ex_->set_copy_grid(0);
-      ex_->set_copy_block(0);
-      kernels::PackTarget<T> pk = pack_;
-      kernels::stencil5_chunk_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->outer_shape, hl->outer_table.get(),
-                                      hl->sched.outer.entries, m, fuse ? &pk : nullptr);
-    } catch (const std::exception&) {
-      ok = false;
-      ex_->set_copy_grid(0);
-      ex_->set_copy_block(0);
-    }
-    const hipError_t end = hipStreamEndCapture(m, &g);
-    if (!ok || end != hipSuccess || g == nullptr) {
-      (void)hipGetLastError();
-      if (g) (void)hipGraphDestroy(g);
-      all = false;
-      break;
-    }
-    if (!hl->chain[k].adopt(g)) {
-      all = false;
-      break;
-    }
-    hl->chain[k].upload(m);
-  }
-  packed_ = saved;
-  last_fused_packs_ = fused_before;
-  return all;
-}
-
-template <typename T>
-void StencilSolver<T>::prime_exchange() {
-  hipStream_t m = main_.get();
-  if (!cfg_.opening_graph || !post_exchange()) {
-    exchange(cur_, m);
-    return;
-  }
-  // Captured with the pack launch, or without it when the passes fuse the
-  // pack (the launch site then sees to the send buffer, as for the chain).
-  const bool fuse = pack_.send != nullptr;
-  if (!prime_graph_.tried) {
-    MXS_TRACE_RANGE("stencil.graph_capture_prime");
-    prime_graph_.tried = true;
-    T* const saved = packed_;
-    const int fused_before = last_fused_packs_;
-    bool all = true;
-    for (int k = 0; k < 2 && all; ++k) {
-      T* tile = k == 0 ? buf_a_ : buf_b_;
-      hipGraph_t g = nullptr;
-      if (hipStreamBeginCapture(m, hipStreamCaptureModeThreadLocal) != hipSuccess) {
-        (void)hipGetLastError();
-        all = false;
-        break;
-      }
-      bool ok = true;
-      try {
-        packed_ = fuse ? tile : nullptr;
-        ex_->set_copy_block(0);
-        exchange(tile, m);
-      } catch (const std::exception&) {
-        ok = false;
-      }
-      const hipError_t end = hipStreamEndCapture(m, &g);
-      if (!ok || end != hipSuccess || g == nullptr) {
-        (void)hipGetLastError();
-        if (g) (void)hipGraphDestroy(g);
-        all = false;
-        break;
-      }
-      if (!prime_graph_.g[k].adopt(g)) {  // adopt() releases g when instantiation fails
-        all = false;
-        break;
-      }
-      prime_graph_.g[k].upload(m);
-    }
-    packed_ = saved;
-    last_fused_packs_ = fused_before;
-    prime_graph_.ok = all;
-  }
-  if (!prime_graph_.ok) {
-    exchange(cur_, m);
-    return;
-  }
-  if (fuse) {
-    if (packed_ == cur_) ++last_fused_packs_;
-    ensure_packed(cur_, m);
-  }
-  prime_graph_.g[cur_ == buf_a_ ? 0 : 1].launch(m);
-  packed_ = cur_;
 }
 
 template <typename T>
@@ -1251,7 +1043,7 @@ void StencilSolver<T>::prepare(int iters) {
   for (const Group& g : gr) {
     if (g.count <= 0) continue;
     if (post_exchange() && !ghost_fresh_) {
-      prime_exchange();  // (captures the serial opening's graph, opening_graph)
+      prime_exchange();
       ghost_fresh_ = true;
     }
     (void)graphs_for(g.S, g.count);
@@ -1267,9 +1059,6 @@ void StencilSolver<T>::prepare(int iters) {
     warmed_.push_back(g.S);
   }
   join_side();
-  // The warm-up passes wrote the scratch buffer's bands into the send buffer:
-  // back to the field's, as the call before left them (its last pass packed).
-  if (post_exchange()) ensure_packed(cur_, main_.get());
   wait_idle("prepare");
 }
 
@@ -1296,7 +1085,6 @@ void StencilSolver<T>::warm(int iters, int passes) {
     enqueue_opening(first.S, false);
   }
   join_side();
-  if (post_exchange()) ensure_packed(cur_, main_.get());  // as prepare()
   wait_idle("warm");
 }
 
@@ -1306,16 +1094,22 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
   WindowPhases out;
   if (iters <= 0) return out;
   maybe_stall("profile_window");
-  begin_run(true);
+  // begin_run() without its priming push: the direct halo is not profiled, and
+  // a push no pass consumes would shift its epochs. Whether to profile is
+  // agreed (the thin-strip overlap is a per-rank property).
+  if (multi_rank_) ghost_fresh_ = false;
+  ensure_range(true);
+  std::vector<double> skip{direct_on_ || (!fused_ && !post_exchange()) ? 1.0 : 0.0};
+  agree_max(skip, "profile_window");
+  if (skip[0] != 0.0) {
+    out.opening = direct_on_ ? "direct (not profiled)" : "overlap (not profiled)";
+    return out;
+  }
   Group gr[2];
   split(iters, gr);
   const int S = gr[0].count > 0 ? gr[0].S : gr[1].S;
   const int supersteps = gr[0].count + gr[1].count;
   hipStream_t m = main_.get();
-  if (direct_on_ || (!fused_ && !post_exchange())) {
-    out.opening = direct_on_ ? "direct (not profiled)" : "overlap (not profiled)";
-    return out;
-  }
   join_side();
   wait_idle("profile_window");
   device_barrier("profile_window");
@@ -1330,13 +1124,8 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
     marks.mark("main:pass", m);
   } else {
     auto exchange = [&](T* tile) {
-      if (pack_.send && packed_ == tile) {  // the pass before packed it (as in the window)
-        ++last_fused_packs_;
-      } else {
-        ex_->pack(tile, m);
-        marks.mark("main:pack", m);
-        packed_ = tile;
-      }
+      ex_->pack(tile, m);
+      marks.mark("main:pack", m);
       ex_->transfer(m);
       marks.mark("main:rccl", m);
       ex_->unpack(tile, m);
@@ -1365,10 +1154,6 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
   join_side();
   wait_idle("profile_window");
   out.wall_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-  if (!fused_ && post_exchange()) {  // the replica packed the scratch buffer's bands (as prepare())
-    ensure_packed(cur_, m);
-    wait_idle("profile_window");
-  }
   // Phases: each marker closes the interval since the previous marker of its stream.
   const Event* first = nullptr;
   for (const auto& e : marks.ev)
@@ -1400,7 +1185,7 @@ void StencilSolver<T>::step() {
 template <typename T>
 void StencilSolver<T>::exchange_only() {
   join_side();
-  exchange(cur_, main_.get());
+  prime_exchange();
   ghost_fresh_ = true;
 }
 

@@ -80,11 +80,12 @@ class StencilConfig:
     direct_halo: bool | str | None = None
     # Opening super-step of a call with peers (RCCL): its priming exchange runs
     # under the chunks that read only core cells ("interior-first") or before
-    # the pass ("serial"). "auto" (default): prepare() times both on every rank,
-    # agrees the worst-rank medians and keeps interior-first only when it wins
-    # by >= min_gain and by more than the measured spread.
+    # the pass ("serial"). "auto" (default): prepare() times both on every rank
+    # in paired rounds, agrees the per-round maxima over ranks (the window is
+    # the max over ranks) and keeps interior-first when the median ratio of the
+    # maxima is below 1 - min_gain with 95% confidence (runtime/decision.hpp).
     opening: str = "auto"
-    min_gain: float = 0.03
+    min_gain: float = 0.0
     # Single GPU with loopback: follow the peers' schedule (every call primes,
     # the last pass of a call is bare, the opening is chosen as with peers), so
     # one GPU rehearses the window an N-GPU run executes.
@@ -93,13 +94,10 @@ class StencilConfig:
     # at most this many workgroups (0 = RCCL's default): the interior-first
     # opening's exchange runs on the 32-48 CUs the inner launch leaves free.
     halo_max_ctas: int = 0
-    # Interior-first opening: replay the main stream's chain (pack, RCCL,
-    # unpack, outer chunks) from a hipGraph captured in prepare().
-    opening_graph: bool = False
-    # Fused halo pack: the pipeline passes also write their send bands into the
-    # exchange's send buffer, so the next exchange is RCCL + unpack. Off by
-    # default (measured slower: the pack launch hides the host's RCCL enqueue).
-    fused_pack: bool = False
+    # One-GPU rehearsal (loopback, rehearse_peers): every RCCL transfer is
+    # followed by a single-wave kernel holding the stream this long (us), in
+    # place of the xGMI wire time the loopback does not have.
+    wire_delay_us: float = 0.0
     # HIP stream priorities of the solver's main (exchange chain) and side streams.
     main_priority: int = -1
     side_priority: int = 0
@@ -191,10 +189,13 @@ class Stencil2D:
             torch.cuda.synchronize()
             kind = H.StencilKind.BOX if cfg.kind == "box" else H.StencilKind.JACOBI5
             be = {"rccl": H.HaloBackend.RCCL, "local": H.HaloBackend.LOCAL, "ipc": H.HaloBackend.IPC}[backend]
-            # Host allgather: the IPC backend's set-up and the solver's collective
-            # agreements (time block, opening, sum-form range) without RCCL.
+            # Host allgather (through the rendezvous store): the IPC backend's
+            # set-up and every collective agreement of the solver (time block,
+            # opening, sum-form range, direct-halo validation) — the same path
+            # whatever the backend, so the one-GPU multi-rank tests run the code
+            # an N-GPU RCCL run agrees with.
             boot = None
-            if backend == "ipc" or (self.ctx.world_size > 1 and backend != "rccl"):
+            if backend == "ipc" or self.ctx.world_size > 1:
                 def boot(blob: bytes, _ctx=self.ctx, _H=H) -> list[bytes]:
                     return _ctx.allgather_bytes(blob, timeout_s=_H.comm_timeout() or None)
             weights = [float(w) for w in cfg.box_weights] if cfg.kind == "box" else []
@@ -205,8 +206,8 @@ class Stencil2D:
                                           self.time_block, boot, cfg.graph_supersteps, self.sum_form,
                                           self._direct_mode(backend),
                                           cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain,
-                                          cfg.halo_max_ctas, cfg.opening_graph, cfg.fused_pack,
-                                          cfg.main_priority, cfg.side_priority)
+                                          cfg.halo_max_ctas, cfg.main_priority, cfg.side_priority,
+                                          cfg.wire_delay_us)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
@@ -406,10 +407,9 @@ class Stencil2D:
         if self.solver.direct_halo():
             how = "HIP IPC direct push of each pass's edge bands into the neighbours' tiles"
         text = f"{what}; {ex} halo exchange{'s' if ex != 1 else ''} by {how}"
-        fp = self.solver.last_run_fused_packs()
-        if fp:
-            text += (f" ({fp} of them with the pack fused into the preceding pass: the pass wrote its send bands "
-                     "into the send buffer)")
+        wd = self.solver.wire_delay_us()
+        if wd:
+            text += f" (+ {wd:g} us of rehearsed wire time after each transfer)"
         if opening == "interior-first":
             text += ("; opening interior-first (the priming exchange ran under the chunks that read only core "
                      "cells, the ghost-ring chunks after it)")

@@ -3,8 +3,8 @@ schedule: prepare()'s agreed numbers (paired ratio, notch, reason) for a few
 fresh solvers, and event-timed replicas (profile_window) of the serial and the
 interior-first openings, interleaved, as the bench records them.
 
-usage: python scripts/exp/opening_probe.py [TILE] [SOLVERS] [REPLICAS] [graph]
-(graph: the openings' exchange chains from hipGraphs, SolverConfig::opening_graph)"""
+usage: python scripts/exp/opening_probe.py [TILE] [SOLVERS] [REPLICAS] [WIRE_US]
+(WIRE_US: rehearsed wire time after each RCCL transfer, SolverConfig::wire_delay_us)"""
 import json
 import sys
 
@@ -22,7 +22,7 @@ def main() -> int:
     reps = int(sys.argv[3]) if len(sys.argv) > 3 else 12
     w, h = (int(x) for x in tile.split("x"))
     kw = dict(global_width=w, global_height=h, dims="1x1", dtype="f32", backend="rccl", loopback=True,
-              rehearse_peers=True, seed=5, opening_graph="graph" in sys.argv[4:])
+              rehearse_peers=True, seed=5, wire_delay_us=float(sys.argv[4]) if len(sys.argv) > 4 else 0.0)
     for i in range(solvers):
         st = Stencil2D(StencilConfig(**kw))
         st.run(20)

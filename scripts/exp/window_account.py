@@ -30,8 +30,7 @@ def run(args) -> int:
     w, h = (int(x) for x in args.tile.split("x"))
     kw = dict(global_width=w, global_height=h, dims="1x1", dtype="f32", seed=5)
     if not args.fused:
-        kw.update(backend="rccl", loopback=True, rehearse_peers=True, opening=args.opening,
-                  opening_graph=args.graph)
+        kw.update(backend="rccl", loopback=True, rehearse_peers=True, opening=args.opening)
     st = Stencil2D(StencilConfig(**kw))
     st.run(5)
     st.prepare(20)
@@ -51,7 +50,7 @@ def run(args) -> int:
         torch.cuda.synchronize()
         t1 = time.monotonic_ns()
         rec = {"window": i, "t0": t0, "run_returned": t_run, "sync_returned": t_sync, "t1": t1,
-               "opening": st.solver.last_run_opening() + (" (graph)" if args.graph else "")}
+               "opening": st.solver.last_run_opening()}
         st.warm(20, 0.02)  # clocks back up between windows (bench runs 200 ms of this before its one window)
         if args.replica:  # the same super-step, event-timed (no profiler): its GPU span
             rec["replica"] = st.profile_window(20)
@@ -123,7 +122,6 @@ def main() -> int:
     p.add_argument("windows", nargs="?", type=int, default=12)
     p.add_argument("--opening", default="auto")
     p.add_argument("--fused", action="store_true")
-    p.add_argument("--graph", action="store_true", help="the opening's main-stream chain from a hipGraph")
     p.add_argument("--torch-sync-only", action="store_true",
                    help="end the window with torch.cuda.synchronize() alone (no solver.synchronize() poll)")
     p.add_argument("--replica", action="store_true", help="run mode: also an event-timed replica per window")

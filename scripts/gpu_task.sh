@@ -15,10 +15,10 @@
 #                          interleaved single-shot bench-flow windows on TILE: RCCL loopback in the
 #                          peers' schedule against the fused-periodic tile (no exchange). MODES (default
 #                          "auto fused"; --serial = "auto serial fused"): auto, serial, ifirst (forced
-#                          interior-first), graph (interior-first, its main-stream chain as a hipGraph),
-#                          sgraph (serial, its priming exchange as a hipGraph),
-#                          fused; suffixes: -fp adds --fused-pack, -ssync / -tsync --window-sync solver /
-#                          torch, -spin --device-schedule spin (in that order, e.g. ifirst-fp-tsync-spin)
+#                          interior-first), fused; suffixes: -wNN adds NN us of rehearsed wire time per
+#                          transfer (--wire-delay-us), -cNN --halo-max-ctas NN, -ssync / -tsync
+#                          --window-sync solver / torch, -p00 / -p11 stream priorities
+#                          (in that order, e.g. ifirst-c16-w40)
 #                          -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
 #   final                  tests + smoke + the driver's bench command + its kernel-trace profile
@@ -92,19 +92,16 @@ task_window() {
     for mode in $modes; do
       local args=(--global "$tile" --steps "${WINDOW_STEPS:-20}" --warmup 5 --no-extras)
       local base=$mode
-      case $base in *-spin) args+=(--device-schedule spin); base=${base%-spin} ;; esac
       case $base in *-p00) args+=(--stream-priorities=0,0); base=${base%-p00} ;; esac
       case $base in *-p11) args+=(--stream-priorities=-1,-1); base=${base%-p11} ;; esac
       case $base in *-tsync) args+=(--window-sync torch); base=${base%-tsync} ;; esac
       case $base in *-ssync) args+=(--window-sync solver); base=${base%-ssync} ;; esac
-      case $base in *-fp) args+=(--fused-pack); base=${base%-fp} ;; esac
+      if [[ $base =~ ^(.*)-w([0-9]+)$ ]]; then args+=(--wire-delay-us "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi
+      if [[ $base =~ ^(.*)-c([0-9]+)$ ]]; then args+=(--halo-max-ctas "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi
       case $base in
         auto) args+=(--loopback --rehearse-peers) ;;
         serial) args+=(--loopback --rehearse-peers --opening serial) ;;
         ifirst) args+=(--loopback --rehearse-peers --opening interior-first) ;;
-        graph) args+=(--loopback --rehearse-peers --opening interior-first --opening-graph) ;;
-        sgraph) args+=(--loopback --rehearse-peers --opening serial --opening-graph) ;;
-        agraph) args+=(--loopback --rehearse-peers --opening-graph) ;;
         fused) ;;
         *) echo "unknown window mode '$mode'"; exit 2 ;;
       esac
@@ -117,12 +114,13 @@ task_window() {
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1]); e = d["extras"]
 print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["ms_per_step"] * d["steps"], 4),
-                  "opening": e.get("opening"), "opening_graph": e.get("opening_graph"),
-                  "fused_packs": e.get("timed_fused_packs"), "side_stream": e.get("side_stream"),
+                  "opening": e.get("opening"), "wire_delay_us": e.get("rehearsed_wire_delay_us", 0),
+                  "halo_max_ctas": e.get("halo_max_ctas"), "side_stream": e.get("side_stream"),
                   "forks": e.get("timed_forks"), "run_host_us": e.get("timed_run_host_us"),
-                  "window_sync": e.get("window_sync"), "device_schedule": e.get("device_schedule"),
+                  "window_sync": e.get("window_sync"),
                   "choice": {k: (e.get("schedule_choice") or {}).get(k) for k in ("opening", "ratio", "ratio_iqr",
-                                                                                   "outer_wgs")},
+                                                                                   "outer_wgs", "serial_ms",
+                                                                                   "interior_first_ms")},
                   "phases": e.get("window_phases")}))
 PY
     done

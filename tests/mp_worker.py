@@ -104,10 +104,12 @@ def task_gpu_solver(args):
                         overlap=args.get("overlap", True), graph=args.get("graph", True),
                         time_block=args.get("time_block", 12), direct_halo=args.get("direct", None),
                         sum_form=args.get("sum_form", True), opening=args.get("opening", "auto"),
-                        min_gain=args.get("min_gain", 0.03))
+                        min_gain=args.get("min_gain", 0.0))
     st = Stencil2D(cfg, ctx)
     if args.get("mismatch_rank") == ctx.rank:
         st.solver.inject_direct_mismatch(True)
+    if args.get("skip_wait_rank") == ctx.rank:
+        st.solver.inject_direct_skip_wait(True)
     stall = args.get("stall")
     if stall and ctx.rank == stall["rank"]:
         st.solver.inject_stall(stall["phase"], float(stall["seconds"]))
@@ -133,6 +135,7 @@ def task_gpu_solver(args):
            "native": st.solver is not None, "time_block": st.time_block}
     if st.solver is not None:
         out["choice"] = dict(st.solver.schedule_times())
+        out["agreement"] = st.solver.agreement_path()
         out["halo_last"] = bool(st.solver.halo_last(st.time_block))
         out["exchanges"] = per_run  # halo exchanges each run() enqueued, and its super-steps
         out["openings"] = openings

@@ -3,7 +3,6 @@ import itertools
 import os
 import subprocess
 
-import numpy as np
 import pytest
 
 import cuda_mpi_scratch_amd as pkg
@@ -96,31 +95,3 @@ def test_aligned_geometry_properties():
         assert (g.x_origin + g.halo_x) % vec == 0
         assert g.pitch % (256 // eb) == 0
         assert g.pitch >= g.x_origin + halo + ((w + vec - 1) // vec) * vec + vec
-
-
-@pytest.mark.parametrize("rows,cols,loopback", [(4, 2, False), (2, 4, False), (2, 2, False), (1, 1, True), (3, 5, False)])
-def test_send_windows_tile_the_send_buffer(rows, cols, loopback):
-    """The fused pack's windows (send_windows): one per sent segment, inside the
-    core, each the segment's own region, and together they fill the packed send
-    buffer exactly once (offsets are the plan's). Plans with self copies have none."""
-    topo = C.CartTopology(rows, cols)
-    g = C.TileGeom.aligned(16384 // cols, 8192 // rows, 20, 20, 4)
-    p = C.make_halo_plan(topo, 0, g, True, loopback)
-    ws = C.send_windows(p)
-    segs = [s for m in p.sends for s in m.segments]
-    assert len(ws) == len(segs) <= 8
-    covered = np.zeros(p.send_elems, dtype=np.int32)
-    cx, cy = g.x_origin + g.halo_x, g.halo_y
-    for (x0, y0, w, h, off), s in zip(ws, segs):
-        assert (x0 + cx, y0 + cy, w, h) == (s.region.x_offset, s.region.y_offset, s.region.width, s.region.height)
-        assert 0 <= x0 and x0 + w <= g.width and 0 <= y0 and y0 + h <= g.height
-        assert off == s.offset and x0 % 4 == 0 and w % 4 == 0 and off % 4 == 0
-        covered[off:off + w * h] += 1
-    assert (covered == 1).all()
-
-
-def test_send_windows_none_with_self_copies():
-    topo = C.CartTopology(1, 1)
-    g = C.TileGeom.aligned(64, 64, 4, 4, 4)
-    assert C.send_windows(C.make_halo_plan(topo, 0, g, True, False)) == []   # self copies
-    assert len(C.send_windows(C.make_halo_plan(topo, 0, g, True, True))) == 8  # RCCL loopback: 8 sends

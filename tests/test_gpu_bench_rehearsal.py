@@ -48,20 +48,20 @@ def test_bench_8gpu_tile_window_through_loopback(gpu):
     ph = ex["window_phases"]
     assert ph["opening"] == ex["opening"] and ph["exchanges"] == 1
     assert {"main:pack", "main:rccl", "main:unpack"} <= set(ph["phases_us"])
-    assert ex["fused_pack"] is False and ex["timed_fused_packs"] == 0  # default: the pack launch
+    assert ex["agreement"] == "none (one rank)" and "rehearsed_wire_delay_us" not in ex
     assert ph["gpu_span_us"] > 0 and ph["wall_us"] > 0
     assert isinstance(ex["env"], dict) and ex["experiments_build"] is False
     # 16384 x 8192 x 20 cell-updates: one pass (~0.25 ms) + one loopback exchange.
     assert d["value"] > 5000, d
 
 
-@pytest.mark.parametrize("extra", [["--window-sync", "torch"], ["--fused-pack"]])
+@pytest.mark.parametrize("extra", [["--window-sync", "torch"], ["--wire-delay-us", "40", "--opening", "serial"]])
 def test_bench_window_options_through_loopback(gpu, extra):
     """--window-sync torch (the window ends at torch.cuda.synchronize() alone,
     under the timer-thread watchdog; with a communicator the default is the
-    solver's polled wait, then torch.cuda.synchronize()) and --fused-pack (the passes write
-    their send bands: the window's priming exchange has no pack launch) run and
-    say so in the record."""
+    solver's polled wait, then torch.cuda.synchronize()) and --wire-delay-us
+    (the rehearsal's stand-in for xGMI wire time: a kernel holding the stream
+    after each RCCL transfer) run and say so in the record."""
     env = dict(os.environ, PYTHONUNBUFFERED="1")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--global", "16384x8192", "--loopback",
                         "--rehearse-peers", "--steps", "20", "--warmup", "5", "--no-extras", "--clock-warmup-ms", "20",
@@ -70,11 +70,11 @@ def test_bench_window_options_through_loopback(gpu, extra):
     ex = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])["extras"]
     assert ex["timed_exchanges"] == 1
     if extra[0] == "--window-sync":
-        assert ex["window_sync"] == "torch" and ex["timed_fused_packs"] == 0
+        assert ex["window_sync"] == "torch"
     else:
-        assert ex["fused_pack"] is True and ex["timed_fused_packs"] == 1
-        assert "main:pack" not in ex["window_phases"]["phases_us"]
-        assert "pack fused" in ex["halo"]
+        assert ex["rehearsed_wire_delay_us"] == 40 and "rehearsed wire time" in ex["halo"]
+        t0, t1 = ex["window_phases"]["phases_us"]["main:rccl"]
+        assert t1 - t0 >= 40, ex["window_phases"]  # the transfer phase holds the rehearsed wire time
 
 
 def test_bench_pingpong_and_dot_record_keys_through_loopback(gpu):

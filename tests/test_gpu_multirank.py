@@ -134,21 +134,28 @@ def test_rank_stalled_in_prepare_fails_the_job_within_the_watchdog(gpu, direct):
     assert "[fault-inject] stalling" in res[1]["stderr"]
 
 
-@pytest.mark.parametrize("mismatch", [False, True])
-def test_direct_halo_validation_and_fallback(gpu, mismatch):
+@pytest.mark.parametrize("fault", [None, "mismatch", "skip_wait"])
+def test_direct_halo_validation_and_fallback(gpu, fault):
     """DirectHalo validate (the mode that lets the device-initiated push run
-    between GPUs): prepare() compares one push with one exchange through the
-    backend (here the IPC transport: ranks share the GPU) bitwise on every rank
+    between GPUs): prepare() runs three super-steps through the backend (here
+    the IPC transport: ranks share the GPU) and three through the direct push
+    from a sentinel-filled ring, compares the whole tiles bitwise on every rank
     and times both. Equal everywhere: validated (used if faster) or rejected as
-    slower, on every rank alike. One rank's corrupted cell (fault injection):
-    every rank rejects it and keeps the backend. The field is exact either way."""
+    slower, on every rank alike. One rank's corrupted cell, or one rank's
+    skipped wait for its neighbours' pushes (the visibility race the check
+    guards; fault injection): every rank rejects it and keeps the backend. The
+    field is exact either way, and the agreements went through the host
+    allgather."""
     w, h, seed, runs = 272, 216, 23, [20, 20, 7]
     res = run_ranks("gpu_solver", 2, {"w": w, "h": h, "dims": "1x2", "iters": sum(runs), "runs": runs, "seed": seed,
                                       "time_block": 20, "overlap": False, "direct": "validate", "prepare": 20,
-                                      "mismatch_rank": 1 if mismatch else None, "comm_timeout": 60}, gpu=True)
+                                      "mismatch_rank": 1 if fault == "mismatch" else None,
+                                      "skip_wait_rank": 0 if fault == "skip_wait" else None,
+                                      "comm_timeout": 60}, gpu=True)
     states = [r["direct_state"] for r in res]
     assert len({s.split(":")[0] for s in states}) == 1, states  # one collective decision
-    if mismatch:
+    assert all(r["agreement"] == "host allgather" for r in res)
+    if fault:
         assert states[0].startswith("rejected: the direct push differs"), states
         assert not any(r["direct"] for r in res)
     else:
