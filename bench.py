@@ -139,9 +139,16 @@ def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync
         t0 = time.perf_counter()
         st.run(steps)
         tr = time.perf_counter()
-        st.synchronize()  # polls under the communication watchdog when a peer can hang
+        st.synchronize()  # polls the solver's streams (under the communication watchdog when a peer can hang)
+        tp = time.perf_counter()
         _sync()
         t1 = time.perf_counter()
+        # "poll": the window ends when the solver's streams have drained — every
+        # one of the K steps' launches is on them — and the device-wide sync
+        # that follows (all streams idle: it only returns) is left outside it.
+        st.window_device_sync_us = (t1 - tp) * 1e6
+        if window_sync == "poll":
+            t1 = tp
     st.timed_host_us = (tr - t0) * 1e6  # the window's enqueue on this rank (diagnostics)
     ctx.barrier()
     return ctx.allreduce_max(t1 - t0)
@@ -260,11 +267,50 @@ def pingpong_extras(ctx, extras: dict, max_bytes: int, with_ipc: bool = False, l
 
 
 def pingpong_ipc_isolated(ctx, extras: dict, max_bytes: int, timeout_s: float = 180.0) -> None:
-    """The device-initiated IPC ping-pong between the GPUs of ranks 0 and 1, run
-    in two child processes (one per GPU, their own rendezvous, gloo control
-    plane): whatever the transport does across GPUs — a wrong flag, a deadline,
-    a fault — ends a child, not this rank, and lands in the record as an error
-    next to the RCCL figures. Collective over all ranks (only 0 and 1 launch)."""
+    """The two transports that map the peer's memory through HIP IPC, between the
+    GPUs of ranks 0 and 1, each run in two child processes (one per GPU, their
+    own rendezvous, gloo control plane): whatever a transport does across GPUs —
+    a wrong flag, a deadline, a fault — ends a child, not this rank, and lands in
+    the record as an error next to the RCCL figures. Collective over all ranks
+    (only 0 and 1 launch).
+      * ``ipc``: device-initiated, one persistent kernel per side (async);
+      * ``peer-copy``: the copy engines — SDMA copies into the peer's mailbox,
+        one-lane flag kernels (async, bidirectional and overlap modes)."""
+    # (transport, record name, key prefix of the rates, modes, reps)
+    specs = (("ipc", "ipc", "ipc_device", "async", 50),
+             ("peer-copy", "peer_copy", "peer_copy", "async,bidir,overlap", 20))
+    for transport, name, prefix, modes, reps in specs:
+        recs, err = _pingpong_children(ctx, transport, name, modes, max_bytes, reps, timeout_s)
+        if not ctx.is_root:
+            continue
+        if err:
+            extras[f"pingpong_{name}_error"] = err[:400]
+            continue
+        for rec in recs:
+            mode = rec.get("mode", "async")
+            k = prefix if transport == "ipc" else f"{prefix}_{mode}"
+            if rec["bytes"] == 8 and mode == "async":
+                extras[f"pingpong_{k}_8B_latency_us"] = round(rec["latency_us"], 2)
+            for label, nb in SUMMARY_SIZES.items():
+                if rec["bytes"] == nb:
+                    extras[f"pingpong_{k}_{label}_gbps"] = round(rec["gbps"], 2)
+                    if "bidir_gbps" in rec:
+                        extras[f"pingpong_{k}_{label}_both_directions_gbps"] = round(rec["bidir_gbps"], 2)
+            if mode == "overlap" and rec["bytes"] == SUMMARY_SIZES["256MiB"] and rec.get("overlapped_us"):
+                alone = rec.get("compute_alone_us", 0.0) + rec.get("comm_alone_us", 0.0)
+                extras[f"pingpong_{k}_256MiB_overlap_speedup"] = round(alone / rec["overlapped_us"], 3)
+        extras[f"pingpong_{name}_verified"] = all(r.get("passed", False) for r in recs)
+        extras[f"pingpong_{name}_sweep_file"] = os.path.join("gpurun_out", f"bench_pingpong_{name}.jsonl")
+    if ctx.is_root:
+        extras["pingpong_ipc"] = ("device-initiated HIP IPC and the copy-engine (SDMA) transport between the GPUs of "
+                                  "ranks 0 and 1, each run isolated in two child processes (a failure there cannot "
+                                  "take this record)")
+
+
+def _pingpong_children(ctx, transport: str, key: str, modes: str, max_bytes: int, reps: int, timeout_s: float):
+    """Ranks 0 and 1 run ``models.pingpong`` over ``transport`` in child processes
+    (a fresh rendezvous on a free port); returns rank 0's records and the joint
+    error (or None). Collective over all ranks."""
     import socket
     import subprocess
 
@@ -273,8 +319,8 @@ def pingpong_ipc_isolated(ctx, extras: dict, max_bytes: int, timeout_s: float = 
         with socket.socket() as sk:
             sk.bind(("127.0.0.1", 0))
             port = str(sk.getsockname()[1]).encode()
-    port = ctx.broadcast_bytes(port, src=0, key="mxs/bench/ipc_pingpong_port").decode()
-    out = os.path.join("gpurun_out", "bench_pingpong_ipc.jsonl")
+    port = ctx.broadcast_bytes(port, src=0, key=f"mxs/bench/{key}_pingpong_port").decode()
+    out = os.path.join("gpurun_out", f"bench_pingpong_{key}.jsonl")
     err = None
     if ctx.rank < 2:
         if ctx.rank == 0:
@@ -284,8 +330,8 @@ def pingpong_ipc_isolated(ctx, extras: dict, max_bytes: int, timeout_s: float = 
         env = dict(os.environ, RANK=str(ctx.rank), WORLD_SIZE="2", LOCAL_RANK=str(ctx.device.index),
                    LOCAL_WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=port, MXS_IPC_CROSS_DEVICE="1",
                    HSA_ENABLE_IPC_MODE_LEGACY="0")
-        cmd = [sys.executable, "-m", "cuda_mpi_scratch_amd.models.pingpong", "--transport", "ipc", "--mode", "async",
-               "--sweep", f"8:{max_bytes}", "--reps", "50", "--warmup", "5", "--pg-backend", "gloo"]
+        cmd = [sys.executable, "-m", "cuda_mpi_scratch_amd.models.pingpong", "--transport", transport, "--mode", modes,
+               "--sweep", f"8:{max_bytes}", "--reps", str(reps), "--warmup", "5", "--pg-backend", "gloo"]
         if ctx.rank == 0:
             cmd += ["--json", out]
         try:
@@ -295,27 +341,15 @@ def pingpong_ipc_isolated(ctx, extras: dict, max_bytes: int, timeout_s: float = 
                 err = f"rank {ctx.rank} child rc={r.returncode}: {r.stderr.strip()[-300:]}"
         except subprocess.TimeoutExpired:
             err = f"rank {ctx.rank} child timed out after {timeout_s:g} s"
-    errs = [e.decode() for e in ctx.allgather_bytes((err or "").encode(), key="mxs/bench/ipc_pingpong_err") if e]
+    errs = [e.decode() for e in ctx.allgather_bytes((err or "").encode(), key=f"mxs/bench/{key}_pingpong_err") if e]
     if not ctx.is_root:
-        return
+        return [], None
     if errs:
-        extras["pingpong_ipc_error"] = "; ".join(errs)[:400]
-        return
+        return [], "; ".join(errs)
     try:
-        recs = [json.loads(line) for line in open(out)]
+        return [json.loads(line) for line in open(out)], None
     except OSError as e:
-        extras["pingpong_ipc_error"] = f"no records: {e}"[:200]
-        return
-    for rec in recs:
-        if rec["bytes"] == 8:
-            extras["pingpong_ipc_device_8B_latency_us"] = round(rec["latency_us"], 2)
-        for label, nb in SUMMARY_SIZES.items():
-            if rec["bytes"] == nb:
-                extras[f"pingpong_ipc_device_{label}_gbps"] = round(rec["gbps"], 2)
-    extras["pingpong_ipc_verified"] = all(r.get("passed", False) for r in recs)
-    extras["pingpong_ipc_sweep_file"] = out
-    extras["pingpong_ipc"] = ("device-initiated HIP IPC between the GPUs of ranks 0 and 1, run isolated in two "
-                              "child processes (a failure there cannot take this record)")
+        return [], f"no records: {e}"
 
 
 def main(argv=None) -> int:
@@ -354,13 +388,15 @@ def main(argv=None) -> int:
     p.add_argument("--wire-delay-us", type=float, default=0.0,
                    help="with --loopback --rehearse-peers: a single-wave kernel holds the stream this long after "
                         "every RCCL transfer, standing in for xGMI wire time (one-GPU rehearsal only)")
-    p.add_argument("--window-sync", default="auto", choices=["auto", "solver", "torch"],
+    p.add_argument("--window-sync", default="auto", choices=["auto", "solver", "poll", "torch"],
                    help="how the timed window ends: torch = torch.cuda.synchronize() alone, under a timer-thread "
                         "watchdog that aborts the halo's RCCL communicators past --comm-timeout; solver = "
                         "solver.synchronize() (polls the solver's streams, RCCL watchdog) then "
                         "torch.cuda.synchronize(); auto (default): torch for a solver without a communicator (the "
                         "1-GPU fused tile: 8-20 us less per window), solver otherwise (with two streams in flight "
-                        "the device sync alone returned ~0.2 ms late in 2-4 of 16 windows; profiles/r04_sync)")
+                        "the device sync alone returned ~0.2 ms late in 2-4 of 16 windows; profiles/r04_sync); "
+                        "poll = the solver's polled wait alone ends the window (its streams carry every launch of "
+                        "the K steps), torch.cuda.synchronize() follows outside it")
     p.add_argument("--stream-priorities", default="-1,0",
                    help="HIP priorities of the solver's main (exchange chain) and side streams, 'MAIN,SIDE' "
                         "(lower = higher priority)")
@@ -368,6 +404,8 @@ def main(argv=None) -> int:
                    help="N > 1: validate: prepare() compares the device-initiated push of the edge bands into the "
                         "neighbours' tiles (HIP IPC over xGMI) bitwise with the RCCL exchange on every rank and times "
                         "both; the push is used only if equal everywhere and faster (default off)")
+    p.add_argument("--direct-engine", default="kernel", choices=["kernel", "copy-engine"],
+                   help="with --direct-halo validate: what pushes the bands, a CU kernel or the SDMA copy engines")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-extras", action="store_true")
     p.add_argument("--clock-warmup-ms", type=float, default=200.0,
@@ -425,6 +463,7 @@ def main(argv=None) -> int:
                         sum_form=not args.no_sum_form, opening=args.opening, rehearse_peers=args.rehearse_peers,
                         direct_halo=("validate" if args.direct_halo == "validate" else None),
                         halo_max_ctas=args.halo_max_ctas, wire_delay_us=args.wire_delay_us,
+                        direct_engine=args.direct_engine,
                         main_priority=int(args.stream_priorities.split(",")[0]),
                         side_priority=int(args.stream_priorities.split(",")[1]),
                         fuse_periodic=not args.no_fuse_periodic)
@@ -482,6 +521,8 @@ def main(argv=None) -> int:
                 extras["timed_exchanges"] = int(st.solver.last_run_exchanges())
                 extras["timed_forks"] = int(st.solver.last_run_forks())
                 extras["timed_run_host_us"] = round(getattr(st, "timed_host_us", 0.0), 1)
+                if hasattr(st, "window_device_sync_us"):
+                    extras["window_device_sync_us"] = round(st.window_device_sync_us, 1)
                 if st.solver.stream_note():
                     extras["side_stream"] = st.solver.stream_note()
                 extras["schedule_choice"] = {k: (round(v, 4) if isinstance(v, float) else v)
@@ -547,8 +588,9 @@ def main(argv=None) -> int:
                     extras["pingpong_ipc_error"] = str(e)[:200]
                 if ctx.is_root:
                     lat = extras.setdefault("pingpong_8B_latency_us", {})
-                    if "pingpong_ipc_device_8B_latency_us" in extras:
-                        lat["ipc_device"] = extras["pingpong_ipc_device_8B_latency_us"]
+                    for k in ("ipc_device", "peer_copy_async"):
+                        if f"pingpong_{k}_8B_latency_us" in extras:
+                            lat[k] = extras[f"pingpong_{k}_8B_latency_us"]
         ctx.barrier()
 
     if ctx.is_root:

@@ -22,6 +22,11 @@
 // a super-step is graph-replayable. Self-neighbours (a periodic dimension of
 // size 1) are plain local copies in the same launch; physical edges are
 // skipped.
+//
+// Push engines: Kernel (the one launch above, 16-byte system-coherent stores
+// from CUs) or CopyEngine (one hipMemcpy2DAsync per band with
+// hipMemcpyDeviceToDeviceNoCU: the SDMA engines move the bands and no CU is
+// taken from the pass; the ready counters stay the same one-lane kernels).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -33,6 +38,8 @@
 #include "mxs/topo/cart.hpp"
 
 namespace mxs {
+
+enum class PushEngine : int { Kernel = 0, CopyEngine = 1 };
 
 template <typename T>
 class IpcDirectHalo {
@@ -56,6 +63,8 @@ class IpcDirectHalo {
   // Raises if a device-side wait timed out (call with the stream idle).
   void check() const;
   int remote_peers() const;
+  void set_engine(PushEngine e);
+  PushEngine engine() const;
 
  private:
   struct Impl;

@@ -88,4 +88,28 @@ PingPongStats pingpong_ipc(const IpcMailbox& mine, unsigned char* peer_base, con
 // between two local mailboxes (no IPC mapping) — the same kernels and protocol.
 PingPongStats pingpong_ipc_loopback(size_t bytes, int warmup, int reps, int workgroups = 0);
 
+// Copy-engine ping-pong (transport "peer-copy", SURVEY C16's "HIP peer copy"):
+// the payload moves by hipMemcpyAsync(kind hipMemcpyDeviceToDeviceNoCU) — an
+// SDMA engine, no compute unit — straight into the peer's IPC-mapped mailbox;
+// a one-thread kernel then publishes the sequence number with a system-scope
+// release store, and the receiver's stream waits on its own flag in a
+// one-thread kernel with a device deadline. The only CU work is those two
+// single-lane kernels per message, so a transfer hides behind compute on
+// another stream (mode Overlap), unlike RCCL's p2p kernels or the IPC push
+// kernel. Modes: Blocking (host-timed, stream sync per round trip), Async
+// (event-timed batches), Overlap, Bidirectional (both sides copy at once).
+struct PeerCopyConfig {
+  size_t bytes = 8;
+  int warmup = 3;
+  int reps = 20;
+  PingPongMode mode = PingPongMode::Async;
+  double timeout_s = 20;  // device-side deadline of any flag wait
+};
+PingPongStats pingpong_peer_copy(const IpcMailbox& mine, unsigned char* peer_base, const void* src, bool ping,
+                                 const PeerCopyConfig& cfg, hipStream_t stream);
+// One process: the same protocol between two local mailboxes, ping and pong on
+// two streams (on one GPU the copies are same-device SDMA copies; with two
+// devices, dev_b's mailbox is reached by hipMemcpyPeerAsync).
+PingPongStats pingpong_peer_copy_local(size_t bytes, int warmup, int reps, int dev_a, int dev_b);
+
 }  // namespace mxs

@@ -20,6 +20,7 @@
 #pragma once
 
 #include <cstddef>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -52,6 +53,15 @@ struct PingPongStats {
 // `sendbuf`/`recvbuf` are device buffers of at least `bytes` bytes.
 PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void* recvbuf, size_t bytes,
                             int warmup, int reps, PingPongMode mode, hipStream_t stream);
+
+// The overlap mode's measurement, shared by the transports: `trips()` enqueues
+// a batch of round trips on `stream` and `drain(what)` waits for it (under the
+// watchdog). Times the batch alone, an ALU-bound kernel on a second stream
+// calibrated to about the same time alone, then both started together; fills
+// comm_alone_us, compute_alone_us and overlapped_us. Both sides of a pair call
+// it (the peer's trips must run too).
+void measure_overlap(const std::function<void()>& trips, const std::function<void(const char*)>& drain,
+                     hipStream_t stream, PingPongStats& st);
 
 // Device-local baselines on one GPU (no communicator): D2D copy round trip, and
 // pinned / pageable host staging round trip (D2H + H2D, the HOST_COPY path).

@@ -163,6 +163,9 @@ struct SolverConfig {
   //              bitwise equal on every rank and faster (agreed). The decision
   //              and its reason are recorded (direct_state()).
   DirectHalo direct = DirectHalo::Off;
+  // What moves the direct halo's bands: a CU kernel, or the SDMA copy engines
+  // (no CU taken from the pass; halo/ipc_direct.hpp).
+  PushEngine direct_engine = PushEngine::Kernel;
   // Opening super-step of a call with peers (see above): measured (Auto),
   // always prime + pass (Serial), always interior-first where the tile has the
   // form (InteriorFirst).

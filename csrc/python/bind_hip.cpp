@@ -419,8 +419,11 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        py::object bootstrap, int graph_supersteps, bool sum_form, const std::string& direct_halo,
                        double graph_max_superstep_us, const std::string& opening, bool rehearse_peers,
                        double min_gain, int halo_max_ctas, int main_priority, int side_priority,
-                       double wire_delay_us) {
+                       double wire_delay_us, const std::string& direct_engine) {
              SolverConfig cfg;
+             if (direct_engine == "kernel") cfg.direct_engine = PushEngine::Kernel;
+             else if (direct_engine == "copy-engine") cfg.direct_engine = PushEngine::CopyEngine;
+             else throw std::invalid_argument("direct_engine must be kernel or copy-engine, got '" + direct_engine + "'");
              cfg.main_priority = main_priority;
              cfg.side_priority = side_priority;
              cfg.halo_max_ctas = halo_max_ctas;
@@ -466,7 +469,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("graph_supersteps") = 0, py::arg("sum_form") = true, py::arg("direct_halo") = "off",
            py::arg("graph_max_superstep_us") = 150.0, py::arg("opening") = "auto", py::arg("rehearse_peers") = false,
            py::arg("min_gain") = 0.0, py::arg("halo_max_ctas") = 0, py::arg("main_priority") = -1,
-           py::arg("side_priority") = 0, py::arg("wire_delay_us") = 0.0,
+           py::arg("side_priority") = 0, py::arg("wire_delay_us") = 0.0, py::arg("direct_engine") = "kernel",
            py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")
@@ -669,4 +672,23 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>());
   m.def("pingpong_ipc_loopback", &pingpong_ipc_loopback, py::arg("nbytes"), py::arg("warmup") = 5,
         py::arg("reps") = 50, py::arg("workgroups") = 0, py::call_guard<py::gil_scoped_release>());
+  // Copy-engine ping-pong (SDMA copies into the peer's IPC-mapped mailbox).
+  m.def(
+      "pingpong_peer_copy",
+      [](const IpcMailbox& mine, std::uintptr_t peer_base, std::uintptr_t src, bool ping, size_t bytes, int warmup,
+         int reps, PingPongMode mode, double timeout_s, std::uintptr_t s) {
+        PeerCopyConfig cfg;
+        cfg.bytes = bytes;
+        cfg.warmup = warmup;
+        cfg.reps = reps;
+        cfg.mode = mode;
+        cfg.timeout_s = timeout_s;
+        return pingpong_peer_copy(mine, ptr<unsigned char>(peer_base), ptr<void>(src), ping, cfg, strm(s));
+      },
+      py::arg("mailbox"), py::arg("peer_base"), py::arg("src"), py::arg("ping"), py::arg("nbytes"),
+      py::arg("warmup") = 3, py::arg("reps") = 20, py::arg("mode") = PingPongMode::Async, py::arg("timeout_s") = 20.0,
+      py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>());
+  m.def("pingpong_peer_copy_local", &pingpong_peer_copy_local, py::arg("nbytes"), py::arg("warmup") = 3,
+        py::arg("reps") = 20, py::arg("dev_a") = 0, py::arg("dev_b") = 0, py::call_guard<py::gil_scoped_release>(),
+        "one process: the copy-engine protocol between two local mailboxes (dev_a != dev_b: hipMemcpyPeerAsync)");
 }

@@ -1,11 +1,13 @@
 #include "mxs/runtime/ipc.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <vector>
 
 #include "mxs/core/error.hpp"
 #include "mxs/core/trace.hpp"
+#include "mxs/kernels/kernels.hpp"
 #include "mxs/runtime/hip_utils.hpp"
 
 namespace mxs {
@@ -189,6 +191,122 @@ bool echo_matches(const unsigned char* box_data, const void* src, size_t bytes) 
   return std::memcmp(a.data(), b.data(), bytes) == 0;
 }
 
+// ------------------------------------------------------- copy-engine transport
+// Publish `seq` into the peer's flag (one lane; the copy before it on the
+// stream has completed, its bytes are in the peer's memory).
+__global__ void pc_signal_kernel(u64* peer_flag, u64 seq) {
+  __threadfence_system();
+  __hip_atomic_store(peer_flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Hold the stream until `*flag >= seq` (one lane, system-scope acquire), or
+// the deadline passes (status = kTimeoutFlag, the wait gives up).
+__global__ void pc_wait_kernel(const u64* flag, u64 seq, u64 timeout_ticks, int* status) {
+  const u64 t0 = wall_clock64();
+  while (load_acquire_system(flag) < seq) {
+    if (wall_clock64() - t0 > timeout_ticks) {
+      atomicCAS(status, kOk, kTimeoutFlag);
+      return;
+    }
+    if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kOk) return;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+struct PeerCopySide {
+  unsigned char* my_box;
+  unsigned char* peer_box;
+  const void* src;     // ping payload (device)
+  bool ping;
+  size_t bytes;
+  u64 ticks;
+  int* status;
+  int peer_dev = -1, my_dev = -1;  // >= 0: copy with hipMemcpyPeerAsync (one process, two devices)
+  void copy(const void* from, hipStream_t s) const {
+    void* to = peer_box + kIpcFlagBytes;
+    if (bytes == 0) return;
+    if (peer_dev >= 0 && peer_dev != my_dev)
+      MXS_HIP_CHECK(hipMemcpyPeerAsync(to, peer_dev, from, my_dev, bytes, s));
+    else
+      MXS_HIP_CHECK(hipMemcpyAsync(to, from, bytes, hipMemcpyDeviceToDeviceNoCU, s));
+  }
+  void signal(u64 seq, hipStream_t s) const {
+    pc_signal_kernel<<<1, 1, 0, s>>>(reinterpret_cast<u64*>(peer_box), seq);
+    MXS_HIP_CHECK_LAUNCH();
+  }
+  void wait(u64 seq, hipStream_t s) const {
+    pc_wait_kernel<<<1, 1, 0, s>>>(reinterpret_cast<const u64*>(my_box), seq, ticks, status);
+    MXS_HIP_CHECK_LAUNCH();
+  }
+  // One round trip (or, bidirectional, one simultaneous exchange).
+  void trip(u64 seq, bool bidir, hipStream_t s) const {
+    if (bidir || ping) {
+      copy(src, s);
+      signal(seq, s);
+      wait(seq, s);
+    } else {  // pong: echo what arrived
+      wait(seq, s);
+      copy(my_box + kIpcFlagBytes, s);
+      signal(seq, s);
+    }
+  }
+};
+
+void check_status(const int* status_dev) {
+  int status = 0;
+  MXS_HIP_CHECK(hipMemcpy(&status, status_dev, sizeof(int), hipMemcpyDeviceToHost));
+  MXS_CHECK(status == kOk, "peer-copy ping-pong: the peer's flag did not arrive before the device deadline "
+                           "(peer not running?)");
+}
+
+// Drives one side: warm-up, timed samples per mode. `seq` continues the
+// mailbox's sequence (both sides advance it identically).
+PingPongStats run_peer_copy(const PeerCopySide& side, u64& seq, const PeerCopyConfig& cfg, hipStream_t stream) {
+  PingPongStats st;
+  st.bytes = cfg.bytes;
+  const bool bidir = cfg.mode == PingPongMode::Bidirectional;
+  st.bidirectional = bidir;
+  auto drain = [&](const char*) {
+    MXS_HIP_CHECK(hipStreamSynchronize(stream));
+    check_status(side.status);
+  };
+  auto trips = [&](int n) {
+    for (int i = 0; i < n; ++i) side.trip(++seq, bidir, stream);
+  };
+  trips(cfg.warmup);
+  drain("warm-up");
+  std::vector<double> rtts;
+  if (cfg.mode == PingPongMode::Blocking) {
+    for (int i = 0; i < cfg.reps; ++i) {
+      const auto t0 = std::chrono::steady_clock::now();
+      trips(1);
+      drain("round trip");
+      rtts.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+  } else {
+    const int batches = std::max(1, std::min(cfg.reps, 10));
+    const int per = std::max(1, cfg.reps / batches);
+    Event e0(true), e1(true);
+    for (int b = 0; b < batches; ++b) {
+      e0.record(stream);
+      trips(per);
+      e1.record(stream);
+      drain("batch");
+      rtts.push_back(double(e1.since(e0)) * 1000.0 / per);
+    }
+    if (cfg.mode == PingPongMode::Overlap) measure_overlap([&] { trips(per); }, drain, stream, st);
+  }
+  st.reps = int(rtts.size());
+  if (!rtts.empty()) {
+    std::sort(rtts.begin(), rtts.end());
+    const size_t n = rtts.size();
+    st.min_rtt_us = rtts.front();
+    st.max_rtt_us = rtts.back();
+    st.median_rtt_us = n % 2 ? rtts[n / 2] : 0.5 * (rtts[n / 2 - 1] + rtts[n / 2]);
+  }
+  return st;
+}
+
 }  // namespace
 
 IpcMailbox::IpcMailbox(size_t capacity) : capacity_(capacity) {
@@ -257,6 +375,101 @@ PingPongStats pingpong_ipc_loopback(size_t bytes, int warmup, int reps, int work
   finish(pong, warmup, false, st);
   finish(ping, warmup, true, st);
   st.verified = echo_matches(a.data(), src.get(), bytes);
+  return st;
+}
+
+}  // namespace mxs
+
+namespace mxs {
+
+PingPongStats pingpong_peer_copy(const IpcMailbox& mine, unsigned char* peer_base, const void* src, bool ping,
+                                 const PeerCopyConfig& cfg, hipStream_t stream) {
+  MXS_TRACE_RANGE("pingpong.peer_copy");
+  MXS_CHECK(cfg.bytes <= mine.capacity(), "peer-copy ping-pong: message larger than the mailbox");
+  DeviceBuffer<int> status(1);
+  MXS_HIP_CHECK(hipMemsetAsync(status.get(), 0, sizeof(int), stream));
+  PeerCopySide side{mine.base(), peer_base, src, ping, cfg.bytes,
+                    u64(cfg.timeout_s * wall_clock_hz()), status.get()};
+  // Every trip uses one sequence number on both sides (a flag left by an
+  // earlier run never satisfies a later wait).
+  const int trips = cfg.warmup + cfg.reps + (cfg.mode == PingPongMode::Overlap ? 2 * std::max(1, cfg.reps / 10) : 0);
+  u64 seq = mine.take_sequence(trips + cfg.reps);  // generous: batches may round reps down
+  PingPongStats st = run_peer_copy(side, seq, cfg, stream);
+  const bool bidir = cfg.mode == PingPongMode::Bidirectional;
+  // Ping: the echo equals the payload; bidirectional: the peer's copy of the
+  // same pattern arrived; pong: it completed.
+  st.verified = ping || bidir ? echo_matches(mine.data(), src, cfg.bytes) : true;
+  return st;
+}
+
+PingPongStats pingpong_peer_copy_local(size_t bytes, int warmup, int reps, int dev_a, int dev_b) {
+  MXS_TRACE_RANGE("pingpong.peer_copy_local");
+  int cur = 0;
+  MXS_HIP_CHECK(hipGetDevice(&cur));
+  const size_t cap = std::max<size_t>(bytes, 16);
+  std::vector<unsigned char> pattern(bytes);
+  for (size_t i = 0; i < bytes; ++i) pattern[i] = static_cast<unsigned char>((i * 131 + 7) % 251);
+  MXS_HIP_CHECK(hipSetDevice(dev_b));
+  if (dev_b != dev_a) (void)hipDeviceEnablePeerAccess(dev_a, 0), (void)hipGetLastError();
+  IpcMailbox b(cap);
+  Stream s_pong;
+  DeviceBuffer<int> st_b(1);
+  MXS_HIP_CHECK(hipMemset(st_b.get(), 0, sizeof(int)));
+  MXS_HIP_CHECK(hipSetDevice(dev_a));
+  if (dev_b != dev_a) (void)hipDeviceEnablePeerAccess(dev_b, 0), (void)hipGetLastError();
+  IpcMailbox a(cap);
+  Stream s_ping;
+  DeviceBuffer<int> st_a(1);
+  MXS_HIP_CHECK(hipMemset(st_a.get(), 0, sizeof(int)));
+  DeviceBuffer<unsigned char> src{index_t(cap)};
+  MXS_HIP_CHECK(hipMemcpy(src.get(), pattern.data(), bytes, hipMemcpyHostToDevice));
+  MXS_HIP_CHECK(hipDeviceSynchronize());
+  // All pong trips are enqueued before the ping's: on one device the two
+  // streams must sit on different hardware queues, or the pong's first wait
+  // would hold the ping's work behind it until the deadline.
+  if (dev_a == dev_b)
+    MXS_CHECK(kernels::streams_concurrent(s_pong.get(), s_ping.get()),
+              "peer-copy loopback: the two streams share a hardware queue");
+  const u64 ticks = u64(10.0 * wall_clock_hz());
+  PeerCopySide ping{a.base(), b.base(), src.get(), true, bytes, ticks, st_a.get(), dev_b, dev_a};
+  PeerCopySide pong{b.base(), a.base(), nullptr, false, bytes, ticks, st_b.get(), dev_a, dev_b};
+  // All trips are enqueued (pong first, so its waits are in place), then
+  // timed on the ping side from its events: 10 batches of reps / 10.
+  const int batches = std::max(1, std::min(reps, 10)), per = std::max(1, reps / batches);
+  const int total = warmup + batches * per;
+  MXS_HIP_CHECK(hipSetDevice(dev_b));
+  for (int i = 0; i < total; ++i) pong.trip(u64(i) + 1, false, s_pong.get());
+  MXS_HIP_CHECK(hipSetDevice(dev_a));
+  std::vector<std::unique_ptr<Event>> ev;
+  for (int i = 0; i < total; ++i) {
+    if (i >= warmup && (i - warmup) % per == 0) {
+      ev.push_back(std::make_unique<Event>(true));
+      ev.back()->record(s_ping.get());
+    }
+    ping.trip(u64(i) + 1, false, s_ping.get());
+  }
+  ev.push_back(std::make_unique<Event>(true));
+  ev.back()->record(s_ping.get());
+  s_ping.sync();
+  MXS_HIP_CHECK(hipSetDevice(dev_b));
+  s_pong.sync();
+  MXS_HIP_CHECK(hipSetDevice(dev_a));
+  check_status(st_a.get());
+  check_status(st_b.get());
+  std::vector<double> rtts;
+  for (size_t k = 0; k + 1 < ev.size(); ++k) rtts.push_back(double(ev[k + 1]->since(*ev[k])) * 1000.0 / per);
+  PingPongStats st;
+  st.bytes = bytes;
+  st.reps = int(rtts.size());
+  std::sort(rtts.begin(), rtts.end());
+  if (!rtts.empty()) {
+    const size_t n = rtts.size();
+    st.min_rtt_us = rtts.front();
+    st.max_rtt_us = rtts.back();
+    st.median_rtt_us = n % 2 ? rtts[n / 2] : 0.5 * (rtts[n / 2 - 1] + rtts[n / 2]);
+  }
+  st.verified = echo_matches(a.data(), src.get(), bytes);
+  MXS_HIP_CHECK(hipSetDevice(cur));
   return st;
 }
 

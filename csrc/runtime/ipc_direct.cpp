@@ -170,6 +170,7 @@ struct IpcDirectHalo<T>::Impl {
   std::vector<void*> opened;
   double timeout_s = 60.0;
   u64 timeout_ticks = 0;
+  PushEngine engine = PushEngine::Kernel;
   u64* epoch() const { return ctrl + world; }
   u64* status() const { return ctrl + world + 1; }
 };
@@ -290,7 +291,13 @@ void IpcDirectHalo<T>::push(const T* tile, hipStream_t s) {
   MXS_CHECK(tile == I.a || tile == I.b, "IpcDirectHalo::push: not one of the registered tiles");
   const PushBatch& b = I.push[tile == I.a ? 0 : 1];
   MXS_TRACE_RANGE("halo.ipc_direct_push");
-  if (b.n > 0) {
+  if (b.n > 0 && I.engine == PushEngine::CopyEngine) {
+    for (int i = 0; i < b.n; ++i) {
+      const PtrCopy& c = b.op[i];
+      MXS_HIP_CHECK(hipMemcpy2DAsync(c.dst, size_t(c.dst_stride) * sizeof(T), c.src, size_t(c.src_stride) * sizeof(T),
+                                     size_t(c.width) * sizeof(T), size_t(c.height), hipMemcpyDeviceToDeviceNoCU, s));
+    }
+  } else if (b.n > 0) {
     index_t biggest = 0;
     for (int i = 0; i < b.n; ++i) biggest = std::max(biggest, b.op[i].width * b.op[i].height);
     const index_t units = (biggest * index_t(sizeof(T)) + 15) / 16;
@@ -303,6 +310,16 @@ void IpcDirectHalo<T>::push(const T* tile, hipStream_t s) {
     signal_kernel<<<1, 64, 0, s>>>(I.signal, I.epoch());
     MXS_HIP_CHECK_LAUNCH();
   }
+}
+
+template <typename T>
+void IpcDirectHalo<T>::set_engine(PushEngine e) {
+  impl_->engine = e;
+}
+
+template <typename T>
+PushEngine IpcDirectHalo<T>::engine() const {
+  return impl_->engine;
 }
 
 template <typename T>

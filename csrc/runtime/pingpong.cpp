@@ -134,41 +134,9 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
       drain("pingpong batch (RCCL)");
       rtts.push_back(double(e1.since(e0)) * 1000.0 / per);
     }
-    if (mode == PingPongMode::Overlap) {
-      // Comm alone, then compute alone (calibrated to about the same time),
-      // then both on separate streams.
-      OverlapScratch& ov = overlap_scratch();
-      hipStream_t cs = ov.stream.get();
-      const int grid = device_cu_count() * 4;
-      Event t0(true), t1(true), t2(true);
-      t0.record(stream);
-      for (int i = 0; i < per; ++i) round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
-      t1.record(stream);
-      drain("pingpong overlap, comm alone (RCCL)");
-      st.comm_alone_us = t1.since(t0) * 1000.0;
-      const int probe = 4096;
-      t0.record(cs);
-      fma_burn_kernel<<<grid, 256, 0, cs>>>(ov.sink.get(), probe);
-      t1.record(cs);
-      t1.sync();
-      const double probe_us = std::max(1.0, double(t1.since(t0)) * 1000.0);
-      const int iters = int(std::min(1e8, std::max(256.0, probe * st.comm_alone_us / probe_us)));
-      t0.record(cs);
-      fma_burn_kernel<<<grid, 256, 0, cs>>>(ov.sink.get(), iters);
-      t1.record(cs);
-      t1.sync();
-      st.compute_alone_us = t1.since(t0) * 1000.0;
-      // Both: the comm stream starts with the compute launch, then join.
-      t0.record(cs);
-      t0.wait_on(stream);
-      fma_burn_kernel<<<grid, 256, 0, cs>>>(ov.sink.get(), iters);
-      for (int i = 0; i < per; ++i) round_trip(comm, peer, sendbuf, recvbuf, bytes, stream);
-      t1.record(stream);
-      t2.record(cs);
-      drain("pingpong overlap, comm + compute (RCCL)");
-      t2.sync();
-      st.overlapped_us = std::max(t1.since(t0), t2.since(t0)) * 1000.0;
-    }
+    if (mode == PingPongMode::Overlap)
+      measure_overlap([&] { for (int i = 0; i < per; ++i) round_trip(comm, peer, sendbuf, recvbuf, bytes, stream); },
+                      drain, stream, st);
   }
   fill_stats(st, rtts);
 
@@ -180,6 +148,43 @@ PingPongStats pingpong_rccl(const RcclComm& comm, int peer, void* sendbuf, void*
     st.verified = true;
   }
   return st;
+}
+
+void measure_overlap(const std::function<void()>& trips, const std::function<void(const char*)>& drain,
+                     hipStream_t stream, PingPongStats& st) {
+  // Comm alone, then compute alone (calibrated to about the same time), then
+  // both on separate streams.
+  OverlapScratch& ov = overlap_scratch();
+  hipStream_t cs = ov.stream.get();
+  const int grid = device_cu_count() * 4;
+  Event t0(true), t1(true), t2(true);
+  t0.record(stream);
+  trips();
+  t1.record(stream);
+  drain("pingpong overlap, comm alone");
+  st.comm_alone_us = t1.since(t0) * 1000.0;
+  const int probe = 4096;
+  t0.record(cs);
+  fma_burn_kernel<<<grid, 256, 0, cs>>>(ov.sink.get(), probe);
+  t1.record(cs);
+  t1.sync();
+  const double probe_us = std::max(1.0, double(t1.since(t0)) * 1000.0);
+  const int iters = int(std::min(1e8, std::max(256.0, probe * st.comm_alone_us / probe_us)));
+  t0.record(cs);
+  fma_burn_kernel<<<grid, 256, 0, cs>>>(ov.sink.get(), iters);
+  t1.record(cs);
+  t1.sync();
+  st.compute_alone_us = t1.since(t0) * 1000.0;
+  // Both: the comm stream starts with the compute launch, then join.
+  t0.record(cs);
+  t0.wait_on(stream);
+  fma_burn_kernel<<<grid, 256, 0, cs>>>(ov.sink.get(), iters);
+  trips();
+  t1.record(stream);
+  t2.record(cs);
+  drain("pingpong overlap, comm + compute");
+  t2.sync();
+  st.overlapped_us = std::max(t1.since(t0), t2.since(t0)) * 1000.0;
 }
 
 PingPongStats pingpong_local(LocalPath path, void* dbuf_a, void* dbuf_b, size_t bytes, int warmup, int reps,

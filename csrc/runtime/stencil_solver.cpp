@@ -107,6 +107,7 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
       direct_state_ = "pending validation";
     }
   }
+  if (direct_) direct_->set_engine(cfg_.direct_engine);
   // cfg_.bootstrap stays: it is the host agreement of backends without an RCCL
   // communicator (agree_max). It may hold a Python callable; the solver is
   // destroyed from Python with the GIL held.

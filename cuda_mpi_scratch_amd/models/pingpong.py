@@ -18,6 +18,13 @@ Transports:
              persistent kernel per rank writes the payload into the peer's
              mailbox over xGMI and spins on a system-scope flag for the echo
              (no host in the loop; ``ipc-loopback``: both kernels on one GPU);
+  ``peer-copy`` the copy engines: each message is an SDMA copy
+             (hipMemcpyAsync, hipMemcpyDeviceToDeviceNoCU) straight into the
+             peer's IPC-mapped mailbox, then a one-lane flag kernel; no CU moves
+             data, so in overlap mode the transfer hides behind compute (modes
+             blocking / async / overlap / bidir; ``peer-copy-loopback``: one
+             process, two mailboxes, hipMemcpyPeerAsync between two devices
+             when given);
   ``torch``  torch.distributed send/recv on the default group (RCCL or gloo);
   ``local``  single-GPU baselines: D2D copy, pinned and pageable host staging
              (the HOST_COPY / PAGE_LOCKED paths), and RCCL self-loopback.
@@ -64,9 +71,12 @@ class PingPong:
             self.comm = ctx.native_comm()
         self.peer = 1 - ctx.rank if ctx.world_size > 1 else ctx.rank
         self.mailbox = self.peer_mailbox = None
-        if transport == "ipc":
+        # peer-copy-loopback: the second mailbox's device (another GPU of this
+        # process when there is one, else the same GPU).
+        self.peer_device = ((dev.index or 0) + 1) % max(1, torch.cuda.device_count()) if dev.type == "cuda" else 0
+        if transport in ("ipc", "peer-copy"):
             if ctx.world_size < 2:
-                raise ValueError("transport ipc needs 2 ranks (use ipc-loopback on one)")
+                raise ValueError(f"transport {transport} needs 2 ranks (use {transport}-loopback on one)")
             H = hip()
             self.mailbox = H.IpcMailbox(max_bytes) if self.active else None
             h0 = ctx.broadcast_bytes(self.mailbox.handle() if ctx.rank == 0 else None, src=0)
@@ -108,6 +118,16 @@ class PingPong:
                                 nbytes, warmup, max(reps, 1), 0, 20.0, stream)
         elif self.transport == "ipc-loopback":
             st = H.pingpong_ipc_loopback(nbytes, warmup, max(reps, 1))
+        elif self.transport == "peer-copy":
+            if not self.active:
+                return rec
+            m = {"blocking": H.PingPongMode.BLOCKING, "async": H.PingPongMode.ASYNC,
+                 "overlap": H.PingPongMode.OVERLAP, "bidir": H.PingPongMode.BIDIRECTIONAL}[mode]
+            st = H.pingpong_peer_copy(self.mailbox, self.peer_mailbox.base(), self.send.data_ptr(),
+                                      self.ctx.rank == 0, nbytes, warmup, max(reps, 1), m, 20.0, stream)
+        elif self.transport == "peer-copy-loopback":
+            dev = self.ctx.device.index or 0
+            st = H.pingpong_peer_copy_local(nbytes, warmup, max(reps, 1), dev, self.peer_device)
         elif self.transport == "torch":
             return self._run_torch(nbytes, warmup, reps, rec)
         else:
@@ -171,8 +191,10 @@ def main(argv=None) -> int:
                    help="reference positional arg: number of doubles (one size)")
     p.add_argument("--sweep", default="8:268435456")
     p.add_argument("--transport", default="rccl",
-                   choices=["rccl", "loopback", "ipc", "ipc-loopback", "torch", "d2d", "pinned", "pageable"])
-    p.add_argument("--mode", default="blocking", choices=["blocking", "async", "overlap", "bidir"])
+                   choices=["rccl", "loopback", "ipc", "ipc-loopback", "peer-copy", "peer-copy-loopback", "torch", "d2d",
+                            "pinned", "pageable"])
+    p.add_argument("--mode", default="blocking",
+                   help="blocking | async | overlap | bidir, or several comma-separated (one sweep each)")
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--reps", type=int, default=20)
     p.add_argument("--json", default=None)
@@ -182,17 +204,22 @@ def main(argv=None) -> int:
     args = p.parse_args(argv)
     ctx = dist_init(backend=args.pg_backend)
     sizes = [args.n_doubles * 8] if args.n_doubles else parse_sweep(args.sweep)
+    modes = args.mode.split(",")
+    bad = [m for m in modes if m not in ("blocking", "async", "overlap", "bidir")]
+    if bad:
+        p.error(f"unknown mode(s) {bad}")
     pp = PingPong(ctx, args.transport, max(sizes))
-    for nb in sizes:
-        rec = pp.run(nb, args.mode, args.warmup, args.reps)
-        if ctx.is_root and "rtt_us" in rec:
-            if args.n_doubles:
-                sys.stdout.write(reference_report(rec))
-            else:
-                print(json.dumps(rec))
-            if args.json:
-                with open(args.json, "a") as f:
-                    f.write(json.dumps(rec) + "\n")
+    for mode in modes:
+        for nb in sizes:
+            rec = pp.run(nb, mode, args.warmup, args.reps)
+            if ctx.is_root and "rtt_us" in rec:
+                if args.n_doubles:
+                    sys.stdout.write(reference_report(rec))
+                else:
+                    print(json.dumps(rec))
+                if args.json:
+                    with open(args.json, "a") as f:
+                        f.write(json.dumps(rec) + "\n")
     ctx.barrier()
     ctx.destroy()
     return 0

@@ -78,6 +78,9 @@ class StencilConfig:
     # direct push with one backend exchange bitwise on every rank and times both
     # openings; direct runs only if equal everywhere and faster (agreed).
     direct_halo: bool | str | None = None
+    # What moves the direct halo's bands: "kernel" (a CU push kernel) or
+    # "copy-engine" (hipMemcpy2DAsync on the SDMA engines, no CU).
+    direct_engine: str = "kernel"
     # Opening super-step of a call with peers (RCCL): its priming exchange runs
     # under the chunks that read only core cells ("interior-first") or before
     # the pass ("serial"). "auto" (default): prepare() times both on every rank
@@ -207,7 +210,7 @@ class Stencil2D:
                                           self._direct_mode(backend),
                                           cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain,
                                           cfg.halo_max_ctas, cfg.main_priority, cfg.side_priority,
-                                          cfg.wire_delay_us)
+                                          cfg.wire_delay_us, cfg.direct_engine)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
@@ -405,7 +408,8 @@ class Stencil2D:
         how = {"rccl": "RCCL send/recv per peer (pack -> ncclSend/ncclRecv -> unpack)",
                "ipc": "HIP IPC", "local": "local self-copy"}.get(self.backend, self.backend)
         if self.solver.direct_halo():
-            how = "HIP IPC direct push of each pass's edge bands into the neighbours' tiles"
+            how = ("HIP IPC direct push of each pass's edge bands into the neighbours' tiles"
+                   + (" by the SDMA copy engines" if self.cfg.direct_engine == "copy-engine" else ""))
         text = f"{what}; {ex} halo exchange{'s' if ex != 1 else ''} by {how}"
         wd = self.solver.wire_delay_us()
         if wd:

@@ -16,8 +16,8 @@
 #                          peers' schedule against the fused-periodic tile (no exchange). MODES (default
 #                          "auto fused"; --serial = "auto serial fused"): auto, serial, ifirst (forced
 #                          interior-first), fused; suffixes: -wNN adds NN us of rehearsed wire time per
-#                          transfer (--wire-delay-us), -cNN --halo-max-ctas NN, -ssync / -tsync
-#                          --window-sync solver / torch, -p00 / -p11 stream priorities
+#                          transfer (--wire-delay-us), -cNN --halo-max-ctas NN, -ssync / -psync / -tsync
+#                          --window-sync solver / poll / torch, -p00 / -p11 stream priorities
 #                          (in that order, e.g. ifirst-c16-w40)
 #                          -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
@@ -96,6 +96,7 @@ task_window() {
       case $base in *-p11) args+=(--stream-priorities=-1,-1); base=${base%-p11} ;; esac
       case $base in *-tsync) args+=(--window-sync torch); base=${base%-tsync} ;; esac
       case $base in *-ssync) args+=(--window-sync solver); base=${base%-ssync} ;; esac
+      case $base in *-psync) args+=(--window-sync poll); base=${base%-psync} ;; esac
       if [[ $base =~ ^(.*)-w([0-9]+)$ ]]; then args+=(--wire-delay-us "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi
       if [[ $base =~ ^(.*)-c([0-9]+)$ ]]; then args+=(--halo-max-ctas "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi
       case $base in
@@ -117,7 +118,7 @@ print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["
                   "opening": e.get("opening"), "wire_delay_us": e.get("rehearsed_wire_delay_us", 0),
                   "halo_max_ctas": e.get("halo_max_ctas"), "side_stream": e.get("side_stream"),
                   "forks": e.get("timed_forks"), "run_host_us": e.get("timed_run_host_us"),
-                  "window_sync": e.get("window_sync"),
+                  "window_sync": e.get("window_sync"), "device_sync_us": e.get("window_device_sync_us"),
                   "choice": {k: (e.get("schedule_choice") or {}).get(k) for k in ("opening", "ratio", "ratio_iqr",
                                                                                    "outer_wgs", "serial_ms",
                                                                                    "interior_first_ms")},

@@ -104,7 +104,7 @@ def task_gpu_solver(args):
                         overlap=args.get("overlap", True), graph=args.get("graph", True),
                         time_block=args.get("time_block", 12), direct_halo=args.get("direct", None),
                         sum_form=args.get("sum_form", True), opening=args.get("opening", "auto"),
-                        min_gain=args.get("min_gain", 0.0))
+                        min_gain=args.get("min_gain", 0.0), direct_engine=args.get("direct_engine", "kernel"))
     st = Stencil2D(cfg, ctx)
     if args.get("mismatch_rank") == ctx.rank:
         st.solver.inject_direct_mismatch(True)

@@ -60,14 +60,32 @@ def test_ipc_direct_halo_matches_global_reference(gpu, n, dims, dtype, time_bloc
     assert (got - ref).abs().max().item() < (1e-5 if dtype == "f32" else 1e-12)
 
 
-def test_ipc_direct_halo_bitwise_vs_classic_exchange(gpu):
-    """The push and the pack -> put -> unpack exchange deliver the same ghost
-    cells: identical results, bit for bit (4 ranks, 2 x 2)."""
+@pytest.mark.parametrize("engine", ["kernel", "copy-engine"])
+def test_ipc_direct_halo_bitwise_vs_classic_exchange(gpu, engine):
+    """The push (by a CU kernel, or by the SDMA copy engines: one
+    hipMemcpy2DAsync per band) and the pack -> put -> unpack exchange deliver
+    the same ghost cells: identical results, bit for bit (4 ranks, 2 x 2)."""
     args = {"w": 264, "h": 200, "dims": "2x2", "iters": 40, "seed": 4, "time_block": 20, "overlap": False}
-    direct = run_ranks("gpu_solver", 4, dict(args, direct=True), gpu=True)
+    direct = run_ranks("gpu_solver", 4, dict(args, direct=True, direct_engine=engine), gpu=True)
     classic = run_ranks("gpu_solver", 4, dict(args, direct=False), gpu=True)
     assert "IPC direct push" in direct[0]["halo"] and "IPC direct push" not in classic[0]["halo"]
+    assert ("SDMA copy engines" in direct[0]["halo"]) == (engine == "copy-engine")
     assert torch.equal(torch.tensor(direct[0]["grid"]), torch.tensor(classic[0]["grid"]))
+
+
+def test_copy_engine_direct_halo_validated(gpu):
+    """The copy-engine push behind the validation gate (three super-steps from
+    a poisoned ring, bitwise against the IPC exchange, then timed): bitwise
+    equal on every rank, whatever the timing decides; the field stays exact."""
+    w, h, seed, runs = 272, 216, 29, [20, 20]
+    res = run_ranks("gpu_solver", 2, {"w": w, "h": h, "dims": "1x2", "iters": sum(runs), "runs": runs, "seed": seed,
+                                      "time_block": 20, "overlap": False, "direct": "validate",
+                                      "direct_engine": "copy-engine", "prepare": 20, "comm_timeout": 60}, gpu=True)
+    states = [r["direct_state"] for r in res]
+    assert states[0].startswith(("validated: bitwise equal", "rejected (slower): bitwise equal")), states
+    got = torch.tensor(res[0]["grid"], dtype=torch.float64)
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed), sum(runs)).double()
+    assert (got - ref).abs().max().item() < 1e-5
 
 
 def test_one_rank_reading_its_field_keeps_ranks_in_step(gpu):
@@ -179,4 +197,32 @@ def test_bench_isolated_ipc_pingpong_two_ranks(gpu):
     assert "pingpong_ipc_error" not in ex, ex
     assert ex["pingpong_ipc_device_8B_latency_us"] > 0 and ex["pingpong_ipc_device_1MiB_gbps"] > 0
     assert ex["pingpong_ipc_verified"] is True and "isolated" in ex["pingpong_ipc"]
+    # The copy-engine transport, in the same isolation: latency, rates, both
+    # directions and the overlap speedup of its largest message.
+    assert "pingpong_peer_copy_error" not in ex, ex
+    assert ex["pingpong_peer_copy_async_8B_latency_us"] > 0 and ex["pingpong_peer_copy_async_1MiB_gbps"] > 0
+    assert ex["pingpong_peer_copy_bidir_1MiB_both_directions_gbps"] > 0
+    assert ex["pingpong_peer_copy_verified"] is True
     assert res[1]["extras"] == {}
+
+
+@pytest.mark.parametrize("mode", ["blocking", "async", "bidir", "overlap"])
+def test_peer_copy_pingpong_two_processes(gpu, mode):
+    """The copy-engine transport between two processes (here sharing the GPU):
+    SDMA copies into the peer's IPC-mapped mailbox, flags published by one-lane
+    kernels. Every size echoes bitwise (bidirectional: each side received the
+    other's payload); the overlap mode reports all three timings, and the copy
+    engine hides the transfer behind the ALU-bound kernel at least as well as
+    running them one after the other."""
+    sizes = [8, 4096, 1 << 20, 16 << 20]
+    res = run_ranks("pingpong", 2, {"transport": "peer-copy", "sizes": sizes, "mode": mode}, gpu=True, timeout=300)
+    for r in res:
+        recs = r["records"]
+        assert [x["bytes"] for x in recs] == sizes
+        assert all(x["passed"] for x in recs), recs
+    r0 = res[0]["records"]
+    assert all(x["rtt_us"] > 0 and x["gbps"] > 0 for x in r0), r0
+    if mode == "overlap":
+        big = r0[-1]
+        assert big["comm_alone_us"] > 0 and big["compute_alone_us"] > 0 and big["overlapped_us"] > 0
+        assert big["overlapped_us"] < 1.05 * (big["comm_alone_us"] + big["compute_alone_us"]), big
