@@ -184,6 +184,13 @@ def dot_extras(ctx, extras: dict, n_global: int) -> None:
             if n > 1:
                 extras[f"{tag}_allreduce_us"] = round(br["allreduce_us"], 2)
             extras[f"{tag}_kernel_tbytes_per_s_per_gpu"] = round(dp.bytes_read / n / (br["kernel_us"] * 1e-6) / 1e12, 3)
+        # Which figure is authoritative: the wall-clock one (the reference's timed
+        # region, mpicuda3.cu:176-179 / :315-316).
+        extras[f"{tag}_timing"] = ("us / gbytes_per_s: wall clock over 20 back-to-back dots (each: counter reset + "
+                                   "single-pass kernel + all-reduce, stream-ordered, one sync at the end) / 20, "
+                                   "authoritative; kernel_us: median of 10 isolated event-timed reps (host sync "
+                                   "after each), a diagnostic whose event brackets and cold starts make it slightly "
+                                   "longer")
         extras[f"{tag}_us"] = round(dt * 1e6, 2)
         extras[f"{tag}_gbytes_per_s"] = round(dp.bytes_read / dt / 1e9, 1)
         extras[f"{tag}_per_gpu_tbytes_per_s"] = round(dp.bytes_read / dt / 1e12 / n, 3)
@@ -375,6 +382,9 @@ def main(argv=None) -> int:
                    help="multi-GPU: a call's opening super-step (its priming exchange) serial, or interior-first "
                         "(under the chunks that read only core cells); auto: prepare() times both on every rank "
                         "and all ranks adopt the same choice")
+    p.add_argument("--steady", default="serial", choices=["serial", "interior-first"],
+                   help="multi-GPU super-steps after the opening: serial (pass, then its exchange) or "
+                        "interior-first like the opening (when the opening is interior-first)")
     p.add_argument("--overlap", action="store_true", help="force the thin-strip interior/exchange overlap schedule")
     p.add_argument("--loopback", action="store_true",
                    help="1 GPU: route the self-neighbour halos through RCCL (exercises the multi-GPU schedule)")
@@ -463,7 +473,7 @@ def main(argv=None) -> int:
                         sum_form=not args.no_sum_form, opening=args.opening, rehearse_peers=args.rehearse_peers,
                         direct_halo=("validate" if args.direct_halo == "validate" else None),
                         halo_max_ctas=args.halo_max_ctas, wire_delay_us=args.wire_delay_us,
-                        direct_engine=args.direct_engine,
+                        direct_engine=args.direct_engine, steady=args.steady,
                         main_priority=int(args.stream_priorities.split(",")[0]),
                         side_priority=int(args.stream_priorities.split(",")[1]),
                         fuse_periodic=not args.no_fuse_periodic)

@@ -170,6 +170,10 @@ struct SolverConfig {
   // always prime + pass (Serial), always interior-first where the tile has the
   // form (InteriorFirst).
   Opening opening = Opening::Auto;
+  // Every super-step of a call interior-first (not only the opening) when the
+  // opening is interior-first: two cross-stream waits per super-step against
+  // an exchange hidden under the core chunks each time.
+  bool steady_interior_first = false;
   // Auto: the upper end of the median paired ratio's 95% notch must be below
   // 1 - min_gain (0: the notch alone guards against noise; decision.hpp).
   double min_gain = 0.0;

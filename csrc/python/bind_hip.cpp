@@ -419,8 +419,9 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        py::object bootstrap, int graph_supersteps, bool sum_form, const std::string& direct_halo,
                        double graph_max_superstep_us, const std::string& opening, bool rehearse_peers,
                        double min_gain, int halo_max_ctas, int main_priority, int side_priority,
-                       double wire_delay_us, const std::string& direct_engine) {
+                       double wire_delay_us, const std::string& direct_engine, bool steady_interior_first) {
              SolverConfig cfg;
+             cfg.steady_interior_first = steady_interior_first;
              if (direct_engine == "kernel") cfg.direct_engine = PushEngine::Kernel;
              else if (direct_engine == "copy-engine") cfg.direct_engine = PushEngine::CopyEngine;
              else throw std::invalid_argument("direct_engine must be kernel or copy-engine, got '" + direct_engine + "'");
@@ -470,6 +471,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("graph_max_superstep_us") = 150.0, py::arg("opening") = "auto", py::arg("rehearse_peers") = false,
            py::arg("min_gain") = 0.0, py::arg("halo_max_ctas") = 0, py::arg("main_priority") = -1,
            py::arg("side_priority") = 0, py::arg("wire_delay_us") = 0.0, py::arg("direct_engine") = "kernel",
+           py::arg("steady_interior_first") = false,
            py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")

@@ -424,29 +424,37 @@ PingPongStats pingpong_peer_copy_local(size_t bytes, int warmup, int reps, int d
   DeviceBuffer<unsigned char> src{index_t(cap)};
   MXS_HIP_CHECK(hipMemcpy(src.get(), pattern.data(), bytes, hipMemcpyHostToDevice));
   MXS_HIP_CHECK(hipDeviceSynchronize());
-  // All pong trips are enqueued before the ping's: on one device the two
-  // streams must sit on different hardware queues, or the pong's first wait
-  // would hold the ping's work behind it until the deadline.
+  // On one device the two streams must sit on different hardware queues, or a
+  // pong wait would hold the ping's work queued behind it until the deadline.
   if (dev_a == dev_b)
     MXS_CHECK(kernels::streams_concurrent(s_pong.get(), s_ping.get()),
               "peer-copy loopback: the two streams share a hardware queue");
   const u64 ticks = u64(10.0 * wall_clock_hz());
   PeerCopySide ping{a.base(), b.base(), src.get(), true, bytes, ticks, st_a.get(), dev_b, dev_a};
   PeerCopySide pong{b.base(), a.base(), nullptr, false, bytes, ticks, st_b.get(), dev_a, dev_b};
-  // All trips are enqueued (pong first, so its waits are in place), then
-  // timed on the ping side from its events: 10 batches of reps / 10.
+  // Trips are enqueued in their causal order: ping's copy + flag, pong's wait +
+  // echo copy + flag, ping's wait. The two streams' copies may share one SDMA
+  // queue, and a copy held behind an unsatisfied wait would block the copies
+  // queued after it; in this order every copy is runnable when it reaches the
+  // engine. Timed on the ping side from its events: batches of reps / 10.
   const int batches = std::max(1, std::min(reps, 10)), per = std::max(1, reps / batches);
   const int total = warmup + batches * per;
-  MXS_HIP_CHECK(hipSetDevice(dev_b));
-  for (int i = 0; i < total; ++i) pong.trip(u64(i) + 1, false, s_pong.get());
-  MXS_HIP_CHECK(hipSetDevice(dev_a));
   std::vector<std::unique_ptr<Event>> ev;
   for (int i = 0; i < total; ++i) {
+    const u64 seq = u64(i) + 1;
+    MXS_HIP_CHECK(hipSetDevice(dev_a));
     if (i >= warmup && (i - warmup) % per == 0) {
       ev.push_back(std::make_unique<Event>(true));
       ev.back()->record(s_ping.get());
     }
-    ping.trip(u64(i) + 1, false, s_ping.get());
+    ping.copy(src.get(), s_ping.get());
+    ping.signal(seq, s_ping.get());
+    MXS_HIP_CHECK(hipSetDevice(dev_b));
+    pong.wait(seq, s_pong.get());
+    pong.copy(b.data(), s_pong.get());
+    pong.signal(seq, s_pong.get());
+    MXS_HIP_CHECK(hipSetDevice(dev_a));
+    ping.wait(seq, s_ping.get());
   }
   ev.push_back(std::make_unique<Event>(true));
   ev.back()->record(s_ping.get());

@@ -371,6 +371,19 @@ template <typename T>
 void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
   if (count <= 0) return;
   last_blocks_.emplace_back(S, count);
+  // SolverConfig::steady_interior_first: every super-step exchanges its own
+  // input under the core chunks (the same exchanges in the same order as the
+  // serial schedule: one per super-step, the first one the call's priming one).
+  if (cfg_.steady_interior_first && halo_last_on_ && post_exchange()) {
+    join_side();
+    if (first) last_opening_ = halo_last_pass(S, true) ? "interior-first" : "serial";
+    for (int i = 0; i < count; ++i) {
+      enqueue_opening(S, true);
+      ++last_exchanges_;
+    }
+    ghost_fresh_ = false;
+    return;
+  }
   // The call's first super-step starts with a priming exchange (with peers:
   // every call): interior-first when the opening is on (exactly one exchange
   // whether or not this rank has the form, see enqueue_opening).

@@ -89,6 +89,10 @@ class StencilConfig:
     # maxima is below 1 - min_gain with 95% confidence (runtime/decision.hpp).
     opening: str = "auto"
     min_gain: float = 0.0
+    # Super-steps after the opening: "serial" (pass, then the exchange of its
+    # output) or "interior-first" (each super-step like the opening, when the
+    # opening is interior-first).
+    steady: str = "serial"
     # Single GPU with loopback: follow the peers' schedule (every call primes,
     # the last pass of a call is bare, the opening is chosen as with peers), so
     # one GPU rehearses the window an N-GPU run executes.
@@ -210,7 +214,7 @@ class Stencil2D:
                                           self._direct_mode(backend),
                                           cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain,
                                           cfg.halo_max_ctas, cfg.main_priority, cfg.side_priority,
-                                          cfg.wire_delay_us, cfg.direct_engine)
+                                          cfg.wire_delay_us, cfg.direct_engine, cfg.steady == "interior-first")
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
@@ -414,14 +418,18 @@ class Stencil2D:
         wd = self.solver.wire_delay_us()
         if wd:
             text += f" (+ {wd:g} us of rehearsed wire time after each transfer)"
-        if opening == "interior-first":
+        if opening == "interior-first" and self.cfg.steady == "interior-first" and passes > 1:
+            text += ("; every super-step interior-first (its exchange ran under the chunks that read only core "
+                     "cells, the ghost-ring chunks after it)")
+        elif opening == "interior-first":
             text += ("; opening interior-first (the priming exchange ran under the chunks that read only core "
                      "cells, the ghost-ring chunks after it)")
         elif opening == "serial":
             text += "; opening serial (priming exchange, then the pass)"
         elif opening == "overlap":
             text += "; thin-strip overlap (interior on a second stream while each exchange runs)"
-        if self.solver.multi_rank() and not self.solver.direct_halo() and not self.solver.overlapped():
+        if (self.solver.multi_rank() and not self.solver.direct_halo() and not self.solver.overlapped()
+                and not (self.cfg.steady == "interior-first" and opening == "interior-first")):
             text += "; the call's last pass is bare (the next call primes)"
         return text
 

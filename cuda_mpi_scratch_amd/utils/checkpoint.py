@@ -99,7 +99,7 @@ def load(stencil, path: str) -> GridHeader:
     if (header.width, header.height) != (d.global_width, d.global_height):
         raise ValueError(f"{path}: {header.width}x{header.height} grid, expected "
                          f"{d.global_width}x{d.global_height}")
-    block = np.ascontiguousarray(arr[d.y0:d.y0 + d.height, d.x0:d.x0 + d.width])
+    block = np.array(arr[d.y0:d.y0 + d.height, d.x0:d.x0 + d.width], copy=True)  # writable: torch.from_numpy warns on a read-only map
     stencil.synchronize()  # no queued solver work may land after the copy
     stencil.core_view().copy_(torch.from_numpy(block))
     if stencil.device.type == "cuda":

@@ -293,6 +293,27 @@ def test_interior_first_bitwise_vs_serial(gpu, w, h, dtype, S, runs, sum_form):
     assert torch.equal(a.core_view(), b.core_view())
 
 
+@pytest.mark.parametrize("runs", [(60,), (20, 40), (47,)])
+def test_steady_interior_first_bitwise_vs_serial(gpu, runs):
+    """steady = interior-first: every super-step of a call runs like the
+    opening (its exchange under the core chunks); same exchanges, one per
+    super-step, and bitwise the serial schedule's field (47 = 24 + 23: two
+    super-step sizes, the second without a chunk-list form at S = 23 runs its
+    exchange + pass serially)."""
+    a = _loopback(16384, 8192, seed=83, opening="interior-first", rehearse_peers=True, time_block=24,
+                  steady="interior-first")
+    b = _loopback(16384, 8192, seed=83, opening="serial", rehearse_peers=True, time_block=24)
+    for n in runs:
+        a.run(n)
+        b.run(n)
+        assert a.solver.last_run_exchanges() == b.solver.last_run_exchanges() == sum(c for _, c in a.last_run_blocks())
+        assert a.solver.last_run_opening() == "interior-first"
+    assert "every super-step interior-first" in a.halo_mode() or runs == (47,)
+    a.synchronize()
+    b.synchronize()
+    assert torch.equal(a.core_view(), b.core_view())
+
+
 def test_interior_first_warm_prepare_keep_the_state(gpu):
     """prepare() launches the interior-first opening into the scratch buffer
     (cur -> nxt, cur's ring re-exchanged with the same values), warm() the
