@@ -19,6 +19,11 @@
 //                         payload straight into the peer's HBM over xGMI and spins on a
 //                         system-scope flag (device-initiated, no host in the loop)
 // --transport ipc-loopback 1 rank: the same kernels, ping and pong on two streams
+// --transport peer-copy   the copy engines (SURVEY C16's HIP peer copy): each message is
+//                         one SDMA hipMemcpyAsync into the peer's IPC-mapped mailbox, then a
+//                         one-lane flag kernel; modes blocking | async | overlap | bidir
+// --transport peer-copy-loopback 1 rank: the same protocol between two local mailboxes
+//                         (hipMemcpyPeerAsync to the next device when there is one)
 #include <mpi.h>
 
 #include <algorithm>
@@ -127,7 +132,8 @@ int main(int argc, char** argv) {
                                                          : "loopback";
   const std::string mode = cli.get("mode", "blocking");
   const int warmup = int(cli.get_int("warmup", 5)), reps = int(cli.get_int("reps", 20));
-  if (env.size() < 2 && (transport == "rccl" || transport == "mpi-staged" || transport == "ipc")) {
+  if (env.size() < 2 &&
+      (transport == "rccl" || transport == "mpi-staged" || transport == "ipc" || transport == "peer-copy")) {
     if (env.rank() == 0) std::cerr << "transport " << transport << " needs 2 ranks" << std::endl;
     return 1;
   }
@@ -156,7 +162,7 @@ int main(int argc, char** argv) {
   // HIP IPC: mailboxes exchanged between ranks 0 and 1 (runtime/ipc.hpp).
   std::unique_ptr<IpcMailbox> mailbox;
   std::unique_ptr<IpcPeerMailbox> peer_box;
-  if (transport == "ipc" && active) {
+  if ((transport == "ipc" || transport == "peer-copy") && active) {
     mailbox = std::make_unique<IpcMailbox>(maxb);
     std::string mine = mailbox->handle(), theirs(mine.size(), '\0');
     const int other = 1 - env.rank();
@@ -167,14 +173,14 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < maxb; ++i) pattern[i] = static_cast<unsigned char>((i * 131 + 7) % 251);
     MXS_HIP_CHECK(hipMemcpy(dsend.get(), pattern.data(), maxb, hipMemcpyHostToDevice));
   }
+  const PingPongMode m = mode == "async"     ? PingPongMode::Async
+                       : mode == "overlap" ? PingPongMode::Overlap
+                       : mode == "bidir"   ? PingPongMode::Bidirectional
+                                           : PingPongMode::Blocking;
   for (size_t bytes : sizes) {
     PingPongStats st;
     if (!active) continue;
     if (transport == "rccl" || transport == "loopback") {
-      const PingPongMode m = mode == "async"     ? PingPongMode::Async
-                           : mode == "overlap" ? PingPongMode::Overlap
-                           : mode == "bidir"   ? PingPongMode::Bidirectional
-                                               : PingPongMode::Blocking;
       const int peer = transport == "loopback" ? env.rank() : 1 - env.rank();
       st = pingpong_rccl(*comm, peer, dsend.get(), drecv.get(), bytes, warmup, reps, m, stream.get());
     } else if (transport == "ipc") {
@@ -190,6 +196,18 @@ int main(int argc, char** argv) {
       MXS_HIP_CHECK(hipMemcpy(drecv.get(), mailbox->data(), bytes, hipMemcpyDeviceToDevice));
     } else if (transport == "ipc-loopback") {
       st = pingpong_ipc_loopback(bytes, warmup, std::max(reps, 1));
+    } else if (transport == "peer-copy") {
+      PeerCopyConfig c;
+      c.bytes = bytes;
+      c.warmup = warmup;
+      c.reps = std::max(reps, 1);
+      c.mode = m;
+      st = pingpong_peer_copy(*mailbox, peer_box->base(), dsend.get(), env.rank() == 0, c, stream.get());
+      MXS_HIP_CHECK(hipMemcpy(drecv.get(), mailbox->data(), bytes, hipMemcpyDeviceToDevice));
+    } else if (transport == "peer-copy-loopback") {
+      int n = 1;
+      MXS_HIP_CHECK(hipGetDeviceCount(&n));
+      st = pingpong_peer_copy_local(bytes, warmup, std::max(reps, 1), dev.device, (dev.device + 1) % std::max(n, 1));
     } else if (transport == "mpi-staged") {
       st = pinned ? staged(env, pin_s, pin_r, dsend.get(), drecv.get(), bytes, warmup, reps, mode == "async")
                   : staged(env, pg_s, pg_r, dsend.get(), drecv.get(), bytes, warmup, reps, mode == "async");

@@ -166,6 +166,24 @@ def test_pingpong_ipc_two_processes_one_gpu(gpu):
     assert r.stdout.count('"passed": true') == 4, r.stdout
 
 
+@pytest.mark.parametrize("mode", ["async", "bidir", "overlap"])
+def test_pingpong_peer_copy_two_processes_one_gpu(gpu, mode):
+    """The copy-engine transport in the MPI app (SDMA copies into the peer's
+    IPC-mapped mailbox, one-lane flag kernels): every size echoes bitwise."""
+    r = mpirun(2, "pingpong", "--transport", "peer-copy", "--mode", mode, "--sweep", "8,4099,1048576,16777216",
+               "--reps", "20")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count('"passed": true') == 4, r.stdout
+    if mode == "overlap":
+        assert '"overlapped_us"' in r.stdout
+
+
+def test_pingpong_peer_copy_loopback_app(gpu):
+    r = mpirun(1, "pingpong", "--transport", "peer-copy-loopback", "--sweep", "8,1048576", "--reps", "10")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert r.stdout.count('"passed": true') == 2, r.stdout
+
+
 def test_pingpong_ipc_reference_output(gpu):
     r = mpirun(2, "pingpong", "--transport", "ipc", "131072")
     assert r.returncode == 0, r.stderr[-3000:]
