@@ -177,6 +177,10 @@ bool streams_concurrent(hipStream_t a, hipStream_t b);
 // 10 ms) of the GPU's constant-rate wall clock (kernels/queue_probe.hip): the
 // wire time an RCCL-loopback rehearsal adds after each transfer.
 void spin_delay(double us, hipStream_t s);
+// out[0] = the shader clock counter (SCLK cycles: its rate follows DVFS),
+// out[1] = the constant-rate wall clock: two stamps around a launch give the
+// clock the launch ran at (device pointer, one lane).
+void clock_stamp(unsigned long long* out, hipStream_t s);
 // Number of 32-bit words that differ between a and b (bytes % 4 == 0) into
 // *out (device pointer, overwritten): the direct halo's bitwise validation.
 void count_diff(const void* a, const void* b, index_t bytes, unsigned* out, hipStream_t s);

@@ -32,7 +32,19 @@ __global__ __launch_bounds__(64) void spin_delay_kernel(unsigned long long ticks
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
 }
 
+// One lane records the shader clock (s_memtime: SCLK cycles, follows DVFS) and
+// the constant-rate wall clock (100 MHz) into out[0..1].
+__global__ void clock_stamp_kernel(unsigned long long* out) {
+  out[0] = clock64();
+  out[1] = wall_clock64();
+}
+
 }  // namespace
+
+void clock_stamp(unsigned long long* out, hipStream_t s) {
+  clock_stamp_kernel<<<1, 1, 0, s>>>(out);
+  MXS_HIP_CHECK_LAUNCH();
+}
 
 void spin_delay(double us, hipStream_t s) {
   static const double ticks_per_us = [] {

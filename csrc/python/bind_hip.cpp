@@ -276,6 +276,20 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("a"), py::arg("b"), py::call_guard<py::gil_scoped_release>(),
       "whether work on stream b runs while a kernel on stream a still runs (different hardware queues)");
   m.def(
+      "clock_stamp",
+      [](std::uintptr_t out, std::uintptr_t s) { kernels::clock_stamp(ptr<unsigned long long>(out), strm(s)); },
+      py::arg("out"), py::arg("stream") = 0,
+      "one lane writes (shader clock cycles, wall clock ticks) to out[0..1] (int64 device buffer)");
+  m.def(
+      "wall_clock_rate_khz",
+      [] {
+        int dev = 0, khz = 0;
+        MXS_HIP_CHECK(hipGetDevice(&dev));
+        MXS_HIP_CHECK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+        return khz;
+      },
+      "rate of wall_clock64() on the current device (kHz)");
+  m.def(
       "spin_delay", [](double us, std::uintptr_t s) { kernels::spin_delay(us, strm(s)); }, py::arg("us"),
       py::arg("stream") = 0, "a single-wave kernel holding `stream` for `us` microseconds (wire-time rehearsal)");
   m.def(
