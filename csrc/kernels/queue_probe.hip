@@ -32,17 +32,23 @@ __global__ __launch_bounds__(64) void spin_delay_kernel(unsigned long long ticks
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
 }
 
-// One lane records the shader clock (s_memtime: SCLK cycles, follows DVFS) and
-// the constant-rate wall clock (100 MHz) into out[0..1].
-__global__ void clock_stamp_kernel(unsigned long long* out) {
-  out[0] = clock64();
-  out[1] = wall_clock64();
+// kClockStampWgs one-wave workgroups (dealt over the XCDs); lane 0 of each
+// records (XCC id, shader clock, wall clock) at out[3 b ..]. The shader clock
+// counter (s_memtime: SCLK cycles, its rate follows DVFS) is per XCD and not
+// synchronised between XCDs, so two stamps are compared XCD by XCD; the wall
+// clock (100 MHz) is global.
+__global__ __launch_bounds__(64) void clock_stamp_kernel(unsigned long long* out) {
+  if (threadIdx.x != 0) return;
+  const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID[3:0]
+  out[3 * blockIdx.x] = xcc;
+  out[3 * blockIdx.x + 1] = clock64();
+  out[3 * blockIdx.x + 2] = wall_clock64();
 }
 
 }  // namespace
 
 void clock_stamp(unsigned long long* out, hipStream_t s) {
-  clock_stamp_kernel<<<1, 1, 0, s>>>(out);
+  clock_stamp_kernel<<<kClockStampWgs, 64, 0, s>>>(out);
   MXS_HIP_CHECK_LAUNCH();
 }
 

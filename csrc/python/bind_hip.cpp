@@ -279,7 +279,9 @@ PYBIND11_MODULE(_mxs_hip, m) {
       "clock_stamp",
       [](std::uintptr_t out, std::uintptr_t s) { kernels::clock_stamp(ptr<unsigned long long>(out), strm(s)); },
       py::arg("out"), py::arg("stream") = 0,
-      "one lane writes (shader clock cycles, wall clock ticks) to out[0..1] (int64 device buffer)");
+      "kClockStampWgs workgroups write (XCC id, shader clock cycles, wall clock ticks) to out[3b..3b+2] "
+      "(int64 device buffer of 3 * clock_stamp_slots())");
+  m.def("clock_stamp_slots", [] { return kernels::kClockStampWgs; });
   m.def(
       "wall_clock_rate_khz",
       [] {

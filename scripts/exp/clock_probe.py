@@ -1,8 +1,9 @@
 """Is the pass-to-pass spread the chip's clock? (round-4 verdict, Weak 2a.)
-Every 20-level pass on the 8-GPU tile is bracketed by one-lane clock stamps
-(shader clock cycles, which follow DVFS, and the constant 100 MHz wall clock):
-the wall time of the pass and the mean shader clock it ran at come from the
-same two stamps.
+Every 20-level pass on the 8-GPU tile is bracketed by clock stamps (one wave
+per workgroup, 16 workgroups over the XCDs: the XCC id, the shader clock
+counter, which follows DVFS and is per XCD, and the constant 100 MHz wall
+clock): the wall time of the pass and the mean shader clock it ran at (median
+over the XCDs seen in both stamps) come from the same two stamps.
 
   A. continuous: PASSES passes back to back on one stream (no host sync), the
      GPU's clock under sustained load;
@@ -52,27 +53,37 @@ def main() -> int:
     fill_random(a, g, 0, 0, w, 1234)
     torch.cuda.synchronize()
     s = torch.cuda.current_stream().cuda_stream
-    stamps = torch.zeros(2 * (passes + 1), dtype=torch.int64, device="cuda")
+    K = H.clock_stamp_slots()
+    SB = 3 * K * 8  # bytes per stamp
+    stamps = torch.zeros(3 * K * (passes + 1), dtype=torch.int64, device="cuda")
 
     def launch():
         H.stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, w, 0, h, 0.2, 0.2, wrap, dtype="f32", stream=s)
 
     def series(st, k):
-        v = st.cpu().tolist()
+        """(pass ms, median over XCDs of the mean shader clock in MHz) for stamps i -> i + 1."""
+        v = st.cpu().view(-1, K, 3).tolist()
         out = []
         for i in range(k):
-            c0, w0, c1, w1 = v[2 * i], v[2 * i + 1], v[2 * i + 2], v[2 * i + 3]
-            dt_us = (w1 - w0) / (khz / 1e3)
-            out.append((dt_us / 1e3, (c1 - c0) / dt_us if dt_us > 0 else 0.0))  # (ms, MHz)
+            d0 = {int(x): (c, t) for x, c, t in v[i]}
+            d1 = {int(x): (c, t) for x, c, t in v[i + 1]}
+            dt_us = (max(t for _, t in d1.values()) - min(t for _, t in d0.values())) / (khz / 1e3)
+            mhz = []
+            for x in set(d0) & set(d1):
+                c0, t0 = d0[x]
+                c1, t1 = d1[x]
+                if t1 > t0:
+                    mhz.append((c1 - c0) / ((t1 - t0) / (khz / 1e3)))
+            out.append((dt_us / 1e3, statistics.median(mhz) if mhz else 0.0))
         return out
 
     # A. continuous
     for _ in range(20):
         launch()
     for i in range(passes):
-        H.clock_stamp(stamps.data_ptr() + 16 * i, s)
+        H.clock_stamp(stamps.data_ptr() + SB * i, s)
         launch()
-    H.clock_stamp(stamps.data_ptr() + 16 * passes, s)
+    H.clock_stamp(stamps.data_ptr() + SB * passes, s)
     torch.cuda.synchronize()
     a_ser = series(stamps, passes)
     ms = [x[0] for x in a_ser]
@@ -84,7 +95,7 @@ def main() -> int:
              "series": [[round(x, 4), round(y)] for x, y in a_ser]}
     print(json.dumps(rec_a), flush=True)
     # B. windows in the bench's shape
-    wst = torch.zeros(4, dtype=torch.int64, device="cuda")
+    wst = torch.zeros(6 * K, dtype=torch.int64, device="cuda")
     rows = []
     for _ in range(windows):
         t_end = time.perf_counter() + 0.2
@@ -95,7 +106,7 @@ def main() -> int:
         time.sleep(0.0002)  # the drain + barrier gap before t0
         H.clock_stamp(wst.data_ptr(), s)
         launch()
-        H.clock_stamp(wst.data_ptr() + 16, s)
+        H.clock_stamp(wst.data_ptr() + SB, s)
         torch.cuda.synchronize()
         rows.append(series(wst, 1)[0])
     ms = [x[0] for x in rows]
