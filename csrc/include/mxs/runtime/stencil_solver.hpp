@@ -284,6 +284,10 @@ class StencilSolver {
   double opening_halo_last_ms() const { return opening_ms_[1]; }
   double opening_serial_spread_ms() const { return opening_spread_[0]; }
   double opening_ratio() const { return opening_ratio_; }
+  // The interior-first schedule's measured inputs (us, agreed max over ranks):
+  // the exchange's delay of the outer launch beside the inner one, the bare pass.
+  double opening_lead_us() const { return lead_us_; }
+  double opening_pass_us() const { return lead_pass_us_; }
   double opening_ratio_iqr() const { return opening_spread_[1]; }
   int opening_samples() const { return opening_samples_; }
   // Paired ratios of the per-round maxima over ranks, per candidate (outer
@@ -390,6 +394,10 @@ class StencilSolver {
   void prime_exchange() { ex_->exchange(cur_, main_.get()); }
   HaloLastPass* halo_last_pass(int S, bool build);  // nullptr: not in use / no form for S
   std::unique_ptr<HaloLastPass> build_halo_last(int S, int outer_wgs);  // nullptr: no form for S
+  // The exchange's delay of the outer launch as a share of the pass, measured
+  // by choose_opening() on this run's real path (0: the model's estimate).
+  double lead_frac_ = 0;
+  double lead_us_ = 0, lead_pass_us_ = 0;  // the agreed measurements behind it
   void enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks* marks = nullptr);
   // The priming exchange of a call's first super-step, interior-first where
   // this rank has the form, else exchange + pass: exactly one exchange either

@@ -517,6 +517,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
                d["candidate_ratios"] = rs;
                d["local_candidate_ratios"] = ls;
                d["agreement"] = s.agreement_path();
+               d["lead_us"] = s.opening_lead_us();
+               d["lead_pass_us"] = s.opening_pass_us();
                return d;
              });
            },

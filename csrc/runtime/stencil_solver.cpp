@@ -629,6 +629,59 @@ void StencilSolver<T>::choose_opening(int S) {
     opening_reason_ = "no rank has an interior-first form at depth " + std::to_string(S);
     return;
   }
+  if (!ghost_fresh_) {
+    prime_exchange();
+    ghost_fresh_ = true;
+  }
+  // The schedule's model needs the delay the exchange puts in front of the
+  // outer launch (pack, wire, unpack beside the inner launch) as a share of the
+  // pass. Both are measured here on the run's real path — an xGMI wire makes
+  // the exchange several times the loopback's — and agreed (max over ranks),
+  // then the model's outer set is rebuilt from them. Ranks without the form
+  // run prime + pass in the same places (the same exchanges everywhere).
+  if (!experiment_env("MXS_HALO_LAST_LEAD")) {
+    constexpr int kLeadReps = 5;
+    std::vector<double> lead, pass;
+    for (int rep = 0; rep <= kLeadReps; ++rep) {
+      join_side();
+      enqueue_block(cur_, nxt_, S);  // warm, state-preserving
+      join_side();
+      wait_idle("prepare: exchange lead");
+      device_barrier("prepare: exchange lead");
+      Event p0(true), p1(true);
+      p0.record(main_.get());
+      core_pass(cur_, nxt_, S, main_.get());
+      p1.record(main_.get());
+      wait_idle("prepare: exchange lead");
+      device_barrier("prepare: exchange lead");
+      Marks marks;
+      if (hl) {
+        enqueue_halo_last(cur_, nxt_, hl, &marks);
+      } else {
+        prime_exchange();
+        core_pass(cur_, nxt_, S, main_.get());
+      }
+      wait_idle("prepare: exchange lead");
+      if (rep == 0) continue;  // round 0 warms every shape
+      pass.push_back(double(p1.since(p0)) * 1e3);
+      double t_unpack = 0;  // the end of the exchange, from the inner launch's start (the first mark)
+      for (size_t i = 0; i < marks.ev.size(); ++i)
+        if (marks.name[i] == "main:unpack") t_unpack = double(marks.ev[i]->since(*marks.ev[0])) * 1e3;
+      lead.push_back(t_unpack);
+    }
+    std::vector<double> v{median_iqr(lead).first, median_iqr(pass).first};
+    agree_max(v, "prepare: exchange lead");
+    lead_us_ = v[0];
+    lead_pass_us_ = v[1];
+    if (lead_us_ > 0 && lead_pass_us_ > 0) {
+      lead_frac_ = std::min(0.6, std::max(0.03, lead_us_ / lead_pass_us_));
+      for (auto& h : halo_lasts_)
+        if (h->S == S) {
+          if (auto nh = build_halo_last(S, 0)) h = std::move(nh);
+          hl = h.get();
+        }
+    }
+  }
   constexpr int kCands = 3;  // slots: model outer set, model - 8, model + 8 workgroups (one XCD step)
   std::unique_ptr<HaloLastPass> alt[kCands];
   HaloLastPass* cands[kCands] = {hl, nullptr, nullptr};
@@ -638,10 +691,6 @@ void StencilSolver<T>::choose_opening(int S) {
       const int k = m + (c == 1 ? -kXcds : kXcds);
       if (k >= 32 && k < hl->inner_shape.blocks + m && (alt[c] = build_halo_last(S, k))) cands[c] = alt[c].get();
     }
-  }
-  if (!ghost_fresh_) {
-    prime_exchange();
-    ghost_fresh_ = true;
   }
   // GPU time of one opening, from drained streams after a device barrier and
   // behind one state-preserving pass (cur -> nxt, the same exchange), so the
@@ -717,16 +766,16 @@ void StencilSolver<T>::choose_opening(int S) {
   }
   halo_last_on_ = d.win;
   opening_choice_ = d.win ? "interior-first" : "serial";
-  char buf[360];
+  char buf[480];
   if (d.best < 0) {
     std::snprintf(buf, sizeof(buf), "no rank-wide interior-first candidate (serial median %.4f ms)", d.baseline_ms);
   } else {
     std::snprintf(buf, sizeof(buf),
                   "paired ratio of the per-round maxima over %d rank(s), interior-first / serial, %d rounds (GPU "
                   "event spans): median %.3f, IQR %.3f, notch %.3f (switch at notch < %.3f); medians %.4f / %.4f "
-                  "ms: %s",
+                  "ms: %s; outer set %d workgroups from the measured exchange lead %.1f us of a %.1f us pass",
                   world_, nr, d.ratio, d.ratio_iqr, d.notch, 1.0 - cfg_.min_gain, d.candidate_ms, d.baseline_ms,
-                  d.win ? "interior-first" : "serial kept");
+                  d.win ? "interior-first" : "serial kept", halo_last_outer_wgs(S), lead_us_, lead_pass_us_);
   }
   opening_reason_ = buf;
 }
@@ -917,7 +966,8 @@ std::unique_ptr<typename StencilSolver<T>::HaloLastPass> StencilSolver<T>::build
   // every tile (pack, RCCL, unpack beside the inner launch; profiles/r04_op2),
   // a fixed cost, so its share falls with the tile's area (est. ~10 T cell-steps/s).
   const double est_pass_us = double(tile_.width) * double(tile_.height) * S / 10e6;
-  const double lead_frac = std::min(0.35, std::max(0.03, 60.0 / std::max(est_pass_us, 1.0)));
+  const double lead_frac =
+      lead_frac_ > 0 ? lead_frac_ : std::min(0.35, std::max(0.03, 60.0 / std::max(est_pass_us, 1.0)));
   auto hl = std::make_unique<HaloLastPass>();
   hl->S = S;
   try {

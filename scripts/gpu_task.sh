@@ -122,7 +122,8 @@ print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["
                   "window_sync": e.get("window_sync"), "device_sync_us": e.get("window_device_sync_us"),
                   "choice": {k: (e.get("schedule_choice") or {}).get(k) for k in ("opening", "ratio", "ratio_iqr",
                                                                                    "outer_wgs", "serial_ms",
-                                                                                   "interior_first_ms")},
+                                                                                   "interior_first_ms", "lead_us",
+                                                                                   "lead_pass_us")},
                   "phases": e.get("window_phases")}))
 PY
     done

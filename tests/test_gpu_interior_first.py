@@ -220,6 +220,8 @@ def test_auto_opening_is_recorded_thresholded_and_exact(gpu):
     wins = t["ratio"] + 1.58 * t["ratio_iqr"] / math.sqrt(20) < 1.0
     assert (t["opening"] == "interior-first") == wins == auto.solver.halo_last(20)
     assert "paired ratio of the per-round maxima" in t["reason"] and t["agreement"] == "none (one rank)"
+    # The outer set was rebuilt from the measured exchange lead and bare pass.
+    assert 0 < t["lead_us"] < t["lead_pass_us"] and "measured exchange lead" in t["reason"]
     # One rank: the maxima are this rank's own samples.
     assert [r for _, r in t["candidate_ratios"]] == [r for _, r in t["local_candidate_ratios"]]
     auto.run(20)
