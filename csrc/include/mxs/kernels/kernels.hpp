@@ -177,11 +177,11 @@ bool streams_concurrent(hipStream_t a, hipStream_t b);
 // 10 ms) of the GPU's constant-rate wall clock (kernels/queue_probe.hip): the
 // wire time an RCCL-loopback rehearsal adds after each transfer.
 void spin_delay(double us, hipStream_t s);
-// kClockStampWgs triples (XCC id, shader clock counter — SCLK cycles, its rate
-// follows DVFS, per XCD —, constant-rate wall clock) at out[3 b ..], one per
-// one-wave workgroup: two stamps around a launch, matched XCD by XCD, give the
-// clock the launch ran at (device pointer).
-constexpr int kClockStampWgs = 16;
+// kClockStampWgs triples (XCD << 16 | SE/SH/CU id, shader clock counter — SCLK
+// cycles, its rate follows DVFS —, constant-rate wall clock) at out[3 b ..],
+// one per one-wave workgroup: two stamps around a launch, matched CU by CU,
+// give the clock the launch ran at (device pointer).
+constexpr int kClockStampWgs = 512;
 void clock_stamp(unsigned long long* out, hipStream_t s);
 // Number of 32-bit words that differ between a and b (bytes % 4 == 0) into
 // *out (device pointer, overwritten): the direct halo's bitwise validation.

@@ -32,15 +32,16 @@ __global__ __launch_bounds__(64) void spin_delay_kernel(unsigned long long ticks
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
 }
 
-// kClockStampWgs one-wave workgroups (dealt over the XCDs); lane 0 of each
-// records (XCC id, shader clock, wall clock) at out[3 b ..]. The shader clock
-// counter (s_memtime: SCLK cycles, its rate follows DVFS) is per XCD and not
-// synchronised between XCDs, so two stamps are compared XCD by XCD; the wall
-// clock (100 MHz) is global.
+// kClockStampWgs one-wave workgroups (dealt over the CUs); lane 0 of each
+// records (XCD and CU id, shader clock, wall clock) at out[3 b ..]. The shader
+// clock counter (s_memtime: SCLK cycles, its rate follows DVFS) is not
+// synchronised between counters, so two stamps are compared CU by CU; the
+// wall clock (100 MHz) is global.
 __global__ __launch_bounds__(64) void clock_stamp_kernel(unsigned long long* out) {
   if (threadIdx.x != 0) return;
   const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // HW_REG_XCC_ID[3:0]
-  out[3 * blockIdx.x] = xcc;
+  const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | (0 << 6) | 4);   // HW_REG_HW_ID: SE, SH, CU
+  out[3 * blockIdx.x] = (xcc << 16) | ((hw >> 8) & 0x7Fu);                  // XCD, SE/SH/CU: one counter's id
   out[3 * blockIdx.x + 1] = clock64();
   out[3 * blockIdx.x + 2] = wall_clock64();
 }

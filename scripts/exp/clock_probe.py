@@ -1,9 +1,9 @@
 """Is the pass-to-pass spread the chip's clock? (round-4 verdict, Weak 2a.)
-Every 20-level pass on the 8-GPU tile is bracketed by clock stamps (one wave
-per workgroup, 16 workgroups over the XCDs: the XCC id, the shader clock
-counter, which follows DVFS and is per XCD, and the constant 100 MHz wall
-clock): the wall time of the pass and the mean shader clock it ran at (median
-over the XCDs seen in both stamps) come from the same two stamps.
+Every 20-level pass on the 8-GPU tile is bracketed by clock stamps (512
+one-wave workgroups over the CUs: the CU's id, its shader clock counter, which
+follows DVFS, and the constant 100 MHz wall clock): the wall time of the pass
+and the mean shader clock it ran at (median over the CUs seen in both stamps)
+come from the same two stamps.
 
   A. continuous: PASSES passes back to back on one stream (no host sync), the
      GPU's clock under sustained load;
@@ -61,7 +61,7 @@ def main() -> int:
         H.stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, w, 0, h, 0.2, 0.2, wrap, dtype="f32", stream=s)
 
     def series(st, k):
-        """(pass ms, median over XCDs of the mean shader clock in MHz) for stamps i -> i + 1."""
+        """(pass ms, median over the CUs seen in both stamps of the mean shader clock in MHz)."""
         v = st.cpu().view(-1, K, 3).tolist()
         out = []
         for i in range(k):
