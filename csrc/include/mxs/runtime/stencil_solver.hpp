@@ -288,6 +288,7 @@ class StencilSolver {
   // the exchange's delay of the outer launch beside the inner one, the bare pass.
   double opening_lead_us() const { return lead_us_; }
   double opening_pass_us() const { return lead_pass_us_; }
+  const std::vector<std::vector<double>>& opening_lead_phases() const { return lead_phases_; }
   double opening_ratio_iqr() const { return opening_spread_[1]; }
   int opening_samples() const { return opening_samples_; }
   // Paired ratios of the per-round maxima over ranks, per candidate (outer
@@ -398,6 +399,7 @@ class StencilSolver {
   // by choose_opening() on this run's real path (0: the model's estimate).
   double lead_frac_ = 0;
   double lead_us_ = 0, lead_pass_us_ = 0;  // the agreed measurements behind it
+  std::vector<std::vector<double>> lead_phases_;  // this rank's (exchange end, inner end, outer end) per sample
   void enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks* marks = nullptr);
   // The priming exchange of a call's first super-step, interior-first where
   // this rank has the form, else exchange + pass: exactly one exchange either

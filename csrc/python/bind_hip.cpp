@@ -519,6 +519,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
                d["agreement"] = s.agreement_path();
                d["lead_us"] = s.opening_lead_us();
                d["lead_pass_us"] = s.opening_pass_us();
+               d["lead_phases_us"] = s.opening_lead_phases();  // (exchange end, inner end, outer end)
                return d;
              });
            },

@@ -664,10 +664,17 @@ void StencilSolver<T>::choose_opening(int S) {
       wait_idle("prepare: exchange lead");
       if (rep == 0) continue;  // round 0 warms every shape
       pass.push_back(double(p1.since(p0)) * 1e3);
-      double t_unpack = 0;  // the end of the exchange, from the inner launch's start (the first mark)
-      for (size_t i = 0; i < marks.ev.size(); ++i)
-        if (marks.name[i] == "main:unpack") t_unpack = double(marks.ev[i]->since(*marks.ev[0])) * 1e3;
+      // Phases from the inner launch's start (the first mark): the end of the
+      // exchange (the lead), the inner and outer launches' ends (diagnostics).
+      double t_unpack = 0, t_inner = 0, t_outer = 0;
+      for (size_t i = 0; i < marks.ev.size(); ++i) {
+        const double t = double(marks.ev[i]->since(*marks.ev[0])) * 1e3;
+        if (marks.name[i] == "main:unpack") t_unpack = t;
+        if (marks.name[i] == "side:inner chunks") t_inner = t;
+        if (marks.name[i] == "main:outer chunks") t_outer = t;
+      }
       lead.push_back(t_unpack);
+      lead_phases_.push_back({t_unpack, t_inner, t_outer});
     }
     std::vector<double> v{median_iqr(lead).first, median_iqr(pass).first};
     agree_max(v, "prepare: exchange lead");
