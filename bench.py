@@ -108,7 +108,7 @@ def _sync():
 
 
 def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync: str = "torch",
-              comm_timeout: float = 300.0, host_spin_s: float = 0.0) -> float:
+              comm_timeout: float = 300.0) -> float:
     """K steps bracketed by barrier + device synchronisation on both sides; the
     max over ranks. Each rank's clock stops when its own device work is done,
     before the closing barrier: a 20-step window at N = 8 is one ~0.3 ms pass,
@@ -122,14 +122,6 @@ def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync
     _sync()
     ctx.barrier()
     _sync()
-    if host_spin_s > 0:
-        # The thread that enqueues the window comes out of blocking waits (the
-        # device syncs, the barrier): spin it briefly so the window's host
-        # enqueue runs on an awake core (outside the window, like the GPU's
-        # clock warm-up).
-        t_spin = time.perf_counter() + host_spin_s
-        while time.perf_counter() < t_spin:
-            pass
     if window_sync == "torch":
         # The window ends at torch.cuda.synchronize() alone (it waits for every
         # stream of the device, the solver's included); a timer thread armed
@@ -429,8 +421,6 @@ def main(argv=None) -> int:
     p.add_argument("--clock-warmup-ms", type=float, default=200.0,
                    help="untimed, state-preserving passes of the timed kernel shapes before the window, so a "
                         "short window runs at sustained clocks (0 = off)")
-    p.add_argument("--host-spin-ms", type=float, default=0.0,
-                   help="spin the host thread this long right before the timed window (outside it)")
     p.add_argument("--dot-n", type=int, default=2**30, help="global dot-product length (extras)")
     p.add_argument("--pingpong-max", type=int, default=256 << 20, help="largest ping-pong message (extras)")
     p.add_argument("--pingpong-ipc", action="store_true",
@@ -491,8 +481,7 @@ def main(argv=None) -> int:
     window_sync = args.window_sync
     if window_sync == "auto":
         window_sync = "torch" if st.comm is None else "solver"
-    dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3, window_sync, args.comm_timeout,
-                   args.host_spin_ms / 1e3)
+    dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3, window_sync, args.comm_timeout)
     timed_blocks = st.last_run_blocks()  # the super-steps the timed window executed
     value = st.cells_per_step * args.steps / dt / 1e9
     halo = st.halo_mode()  # what the timed run() executed

@@ -297,6 +297,9 @@ class StencilSolver {
   const std::vector<std::pair<int, std::vector<double>>>& opening_local_ratio_samples() const {
     return opening_local_ratio_samples_;
   }
+  const std::vector<std::pair<int, std::vector<double>>>& opening_host_ratio_samples() const {
+    return opening_host_ratio_samples_;
+  }
   // How collective agreements travel: "host allgather", "rccl all-reduce" or
   // "none (one rank)"; the device barrier before timed samples uses RCCL when
   // a communicator exists.
@@ -421,7 +424,8 @@ class StencilSolver {
   double opening_spread_[2] = {0, 0};        // IQRs: serial maxima (ms), paired ratio of maxima
   double opening_ratio_ = 0;                 // median paired ratio of the maxima, interior-first / serial
   int opening_samples_ = 0;
-  std::vector<std::pair<int, std::vector<double>>> opening_ratio_samples_, opening_local_ratio_samples_;
+  std::vector<std::pair<int, std::vector<double>>> opening_ratio_samples_, opening_local_ratio_samples_,
+      opening_host_ratio_samples_;  // the same rounds by the host clock (diagnostics)
   std::string opening_choice_;               // "" before prepare() decided, "serial" or "interior-first"
   std::string opening_reason_;
   void choose_opening(int S);                // Opening::Auto: time both, agree, keep the faster

@@ -511,11 +511,13 @@ PYBIND11_MODULE(_mxs_hip, m) {
                d["outer_wgs"] = s.halo_last_outer_wgs(s.time_block());
                // Paired ratios of the per-round maxima over ranks per candidate
                // outer set, and this rank's own ratios (diagnostics).
-               py::list rs, ls;
+               py::list rs, ls, hs;
                for (const auto& c : s.opening_ratio_samples()) rs.append(py::make_tuple(c.first, c.second));
                for (const auto& c : s.opening_local_ratio_samples()) ls.append(py::make_tuple(c.first, c.second));
+               for (const auto& c : s.opening_host_ratio_samples()) hs.append(py::make_tuple(c.first, c.second));
                d["candidate_ratios"] = rs;
                d["local_candidate_ratios"] = ls;
+               d["local_host_candidate_ratios"] = hs;
                d["agreement"] = s.agreement_path();
                d["lead_us"] = s.opening_lead_us();
                d["lead_pass_us"] = s.opening_pass_us();

@@ -709,29 +709,33 @@ void StencilSolver<T>::choose_opening(int S) {
   // cross-stream join (~15 us) would be charged to the interior-first opening
   // alone (it measured 1.0x serial that way, 0.92x as the window runs it).
   Event e0(true), e1(true), e2(true);
+  double host_ms = 0;  // the last sample's host-clock span (diagnostics: enqueue to drained)
   auto timed = [&](bool starts_on_side, auto&& enqueue) {
     join_side();
     enqueue_block(cur_, nxt_, S);
     join_side();
     wait_idle("prepare: opening timing");
     device_barrier("prepare: opening timing");
+    const auto h0 = std::chrono::steady_clock::now();
     e0.record(starts_on_side ? side_.get() : main_.get());
     enqueue();
     e1.record(main_.get());
     e2.record(side_.get());
     wait_idle("prepare: opening timing");
+    host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
     return std::max(double(e1.since(e0)), double(e2.since(e0)));
   };
   constexpr int kReps = 21;  // round 0 warms every shape (20 paired rounds: the notch is 1.58 IQR / sqrt(20))
   constexpr int nr = kReps - 1;
   // Per round: serial, then the three slots. v = [serial x nr, slot 0 x nr, slot 1 x nr, slot 2 x nr].
-  std::vector<double> v(size_t((1 + kCands) * nr), kMissingSample);
+  std::vector<double> v(size_t((1 + kCands) * nr), kMissingSample), vh(v.size(), 0.0);
   for (int rep = 0; rep < kReps; ++rep) {
     const double serial = timed(false, [&] {
       prime_exchange();
       enqueue_bare_pass(cur_, nxt_, S);
     });
     if (rep > 0) v[size_t(rep - 1)] = serial;
+    if (rep > 0) vh[size_t(rep - 1)] = host_ms;
     for (int c = 0; c < kCands; ++c) {
       const double ms = timed(cands[c] != nullptr, [&] {
         if (cands[c]) {
@@ -742,15 +746,21 @@ void StencilSolver<T>::choose_opening(int S) {
         }
       });
       if (rep > 0 && cands[c]) v[size_t((1 + c) * nr + rep - 1)] = ms;
+      if (rep > 0 && cands[c]) vh[size_t((1 + c) * nr + rep - 1)] = host_ms;
     }
   }
   // This rank's own paired ratios (diagnostics), then the agreed maxima.
   opening_local_ratio_samples_.clear();
+  opening_host_ratio_samples_.clear();
   for (int c = 0; c < kCands; ++c) {
     if (!cands[c]) continue;
-    std::vector<double> r(nr);
-    for (int i = 0; i < nr; ++i) r[size_t(i)] = v[size_t((1 + c) * nr + i)] / std::max(v[size_t(i)], 1e-12);
+    std::vector<double> r(nr), rh(nr);
+    for (int i = 0; i < nr; ++i) {
+      r[size_t(i)] = v[size_t((1 + c) * nr + i)] / std::max(v[size_t(i)], 1e-12);
+      rh[size_t(i)] = vh[size_t((1 + c) * nr + i)] / std::max(vh[size_t(i)], 1e-12);
+    }
     opening_local_ratio_samples_.emplace_back(cands[c]->sched.outer.blocks, std::move(r));
+    opening_host_ratio_samples_.emplace_back(cands[c]->sched.outer.blocks, std::move(rh));
   }
   agree_max(v, "prepare: opening agreement");
   std::vector<double> base(v.begin(), v.begin() + nr);

@@ -97,7 +97,6 @@ task_window() {
       case $base in *-tsync) args+=(--window-sync torch); base=${base%-tsync} ;; esac
       case $base in *-ssync) args+=(--window-sync solver); base=${base%-ssync} ;; esac
       case $base in *-psync) args+=(--window-sync poll); base=${base%-psync} ;; esac
-      case $base in *-hs) args+=(--host-spin-ms 2); base=${base%-hs} ;; esac
       case $base in *-st) args+=(--steady interior-first); base=${base%-st} ;; esac
       if [[ $base =~ ^(.*)-w([0-9]+)$ ]]; then args+=(--wire-delay-us "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi
       if [[ $base =~ ^(.*)-c([0-9]+)$ ]]; then args+=(--halo-max-ctas "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi
