@@ -699,17 +699,21 @@ void StencilSolver<T>::choose_opening(int S) {
       if (k >= 32 && k < hl->inner_shape.blocks + m && (alt[c] = build_halo_last(S, k))) cands[c] = alt[c].get();
     }
   }
-  // GPU time of one opening, from drained streams after a device barrier and
-  // behind one state-preserving pass (cur -> nxt, the same exchange), so the
-  // sample runs at the clocks a window after warm() sees. The start event goes
-  // on the stream that receives the opening's first launch (the side stream
-  // for interior-first: an event on main would itself force the fork the
-  // opening skips). The end is the later of an event on each stream, with no
-  // join between them: a window ends when both streams have drained, and a
-  // cross-stream join (~15 us) would be charged to the interior-first opening
-  // alone (it measured 1.0x serial that way, 0.92x as the window runs it).
+  // One opening timed as the bench times a window: from drained streams after
+  // a device barrier (behind one state-preserving pass, cur -> nxt with the
+  // same exchange, so the sample runs at the clocks a window after warm()
+  // sees), host clock from the enqueue to both streams drained, no event
+  // recorded on either stream, no join. Round 4 bracketed the sample with GPU
+  // events (the start event on the stream of the first launch); in some
+  // solvers that harness serialised the interior-first opening's two launches
+  // in almost every round (paired ratio ~1.55 with 40 or 48 outer workgroups)
+  // while bench-shaped windows of a solver forced to interior-first, timed at
+  // the same moment in the same process, ran 5% faster than serial
+  // (profiles/r05_decision/decision_vs_window.txt), so the decision kept
+  // serial where it should not have.
+  constexpr bool kEventSamples = false;
   Event e0(true), e1(true), e2(true);
-  double host_ms = 0;  // the last sample's host-clock span (diagnostics: enqueue to drained)
+  double host_ms = 0;  // the last sample's host-clock span (enqueue to drained)
   auto timed = [&](bool starts_on_side, auto&& enqueue) {
     join_side();
     enqueue_block(cur_, nxt_, S);
@@ -717,13 +721,15 @@ void StencilSolver<T>::choose_opening(int S) {
     wait_idle("prepare: opening timing");
     device_barrier("prepare: opening timing");
     const auto h0 = std::chrono::steady_clock::now();
-    e0.record(starts_on_side ? side_.get() : main_.get());
+    if (kEventSamples) e0.record(starts_on_side ? side_.get() : main_.get());
     enqueue();
-    e1.record(main_.get());
-    e2.record(side_.get());
+    if (kEventSamples) {
+      e1.record(main_.get());
+      e2.record(side_.get());
+    }
     wait_idle("prepare: opening timing");
     host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
-    return std::max(double(e1.since(e0)), double(e2.since(e0)));
+    return kEventSamples ? std::max(double(e1.since(e0)), double(e2.since(e0))) : host_ms;
   };
   constexpr int kReps = 21;  // round 0 warms every shape (20 paired rounds: the notch is 1.58 IQR / sqrt(20))
   constexpr int nr = kReps - 1;
