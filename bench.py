@@ -382,9 +382,10 @@ def main(argv=None) -> int:
                    help="multi-GPU: a call's opening super-step (its priming exchange) serial, or interior-first "
                         "(under the chunks that read only core cells); auto: prepare() times both on every rank "
                         "and all ranks adopt the same choice")
-    p.add_argument("--steady", default="serial", choices=["serial", "interior-first"],
-                   help="multi-GPU super-steps after the opening: serial (pass, then its exchange) or "
-                        "interior-first like the opening (when the opening is interior-first)")
+    p.add_argument("--steady", default="auto", choices=["auto", "serial", "interior-first"],
+                   help="multi-GPU super-steps after an interior-first opening: serial (pass, then its exchange), "
+                        "interior-first like the opening, or auto (prepare() of a window with >= 2 super-steps "
+                        "times both; all ranks adopt the faster)")
     p.add_argument("--overlap", action="store_true", help="force the thin-strip interior/exchange overlap schedule")
     p.add_argument("--loopback", action="store_true",
                    help="1 GPU: route the self-neighbour halos through RCCL (exercises the multi-GPU schedule)")

@@ -98,6 +98,7 @@
 // (e.g. an RCCL build without graph support) the solver falls back to eager launches.
 #pragma once
 
+#include <chrono>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -170,10 +171,13 @@ struct SolverConfig {
   // always prime + pass (Serial), always interior-first where the tile has the
   // form (InteriorFirst).
   Opening opening = Opening::Auto;
-  // Every super-step of a call interior-first (not only the opening) when the
-  // opening is interior-first: two cross-stream waits per super-step against
-  // an exchange hidden under the core chunks each time.
-  bool steady_interior_first = false;
+  // Super-steps after the opening when the opening is interior-first: Serial
+  // (pass, then the exchange of its output), InteriorFirst (every super-step
+  // like the opening: its exchange under the core chunks, two cross-stream
+  // waits per super-step), or Auto: prepare() of a call with two or more
+  // super-steps times two back-to-back super-steps both ways (paired rounds,
+  // per-round maxima over ranks, decision.hpp) and keeps the faster.
+  Opening steady = Opening::Auto;
   // Auto: the upper end of the median paired ratio's 95% notch must be below
   // 1 - min_gain (0: the notch alone guards against noise; decision.hpp).
   double min_gain = 0.0;
@@ -280,6 +284,10 @@ class StencilSolver {
   // and the statistics of the per-round maxima over ranks it was taken from.
   const std::string& opening_choice() const { return opening_choice_; }
   const std::string& opening_reason() const { return opening_reason_; }
+  // prepare()'s steady decision ("" before it decided, "serial" or
+  // "interior-first") and why.
+  const std::string& steady_choice() const { return steady_choice_; }
+  const std::string& steady_reason() const { return steady_reason_; }
   double opening_serial_ms() const { return opening_ms_[0]; }
   double opening_halo_last_ms() const { return opening_ms_[1]; }
   double opening_serial_spread_ms() const { return opening_spread_[0]; }
@@ -297,9 +305,7 @@ class StencilSolver {
   const std::vector<std::pair<int, std::vector<double>>>& opening_local_ratio_samples() const {
     return opening_local_ratio_samples_;
   }
-  const std::vector<std::pair<int, std::vector<double>>>& opening_host_ratio_samples() const {
-    return opening_host_ratio_samples_;
-  }
+
   // How collective agreements travel: "host allgather", "rccl all-reduce" or
   // "none (one rank)"; the device barrier before timed samples uses RCCL when
   // a communicator exists.
@@ -424,11 +430,22 @@ class StencilSolver {
   double opening_spread_[2] = {0, 0};        // IQRs: serial maxima (ms), paired ratio of maxima
   double opening_ratio_ = 0;                 // median paired ratio of the maxima, interior-first / serial
   int opening_samples_ = 0;
-  std::vector<std::pair<int, std::vector<double>>> opening_ratio_samples_, opening_local_ratio_samples_,
-      opening_host_ratio_samples_;  // the same rounds by the host clock (diagnostics)
+  std::vector<std::pair<int, std::vector<double>>> opening_ratio_samples_, opening_local_ratio_samples_;
+  // Host time (ms) from enqueue() to both streams drained: a timed window's
+  // measure. No event goes on either stream (see choose_opening).
+  template <typename F>
+  double host_span_ms(F&& enqueue, const char* phase) {
+    const auto h0 = std::chrono::steady_clock::now();
+    enqueue();
+    wait_idle(phase);
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
+  }
   std::string opening_choice_;               // "" before prepare() decided, "serial" or "interior-first"
   std::string opening_reason_;
   void choose_opening(int S);                // Opening::Auto: time both, agree, keep the faster
+  void choose_steady(int S);                 // SolverConfig::steady Auto: the same for two super-steps
+  bool steady_on_ = false;                   // every super-step interior-first (with the opening)
+  std::string steady_choice_, steady_reason_;
   bool side_pending_ = false;                // side-stream work not yet joined to main
   void join_side();                          // main stream waits for the side stream's work
   // Collective agreement: element-wise max over ranks (the host allgather when

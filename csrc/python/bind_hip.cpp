@@ -435,9 +435,12 @@ PYBIND11_MODULE(_mxs_hip, m) {
                        py::object bootstrap, int graph_supersteps, bool sum_form, const std::string& direct_halo,
                        double graph_max_superstep_us, const std::string& opening, bool rehearse_peers,
                        double min_gain, int halo_max_ctas, int main_priority, int side_priority,
-                       double wire_delay_us, const std::string& direct_engine, bool steady_interior_first) {
+                       double wire_delay_us, const std::string& direct_engine, const std::string& steady) {
              SolverConfig cfg;
-             cfg.steady_interior_first = steady_interior_first;
+             if (steady == "auto") cfg.steady = Opening::Auto;
+             else if (steady == "serial") cfg.steady = Opening::Serial;
+             else if (steady == "interior-first") cfg.steady = Opening::InteriorFirst;
+             else throw std::invalid_argument("steady must be auto, serial or interior-first, got '" + steady + "'");
              if (direct_engine == "kernel") cfg.direct_engine = PushEngine::Kernel;
              else if (direct_engine == "copy-engine") cfg.direct_engine = PushEngine::CopyEngine;
              else throw std::invalid_argument("direct_engine must be kernel or copy-engine, got '" + direct_engine + "'");
@@ -487,7 +490,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
            py::arg("graph_max_superstep_us") = 150.0, py::arg("opening") = "auto", py::arg("rehearse_peers") = false,
            py::arg("min_gain") = 0.0, py::arg("halo_max_ctas") = 0, py::arg("main_priority") = -1,
            py::arg("side_priority") = 0, py::arg("wire_delay_us") = 0.0, py::arg("direct_engine") = "kernel",
-           py::arg("steady_interior_first") = false,
+           py::arg("steady") = "auto",
            py::keep_alive<1, 7>())
       .def("field_changed", [](SolverHandle& h) { h.visit([](auto& s) { s.field_changed(); }); },
            "the caller wrote the field: re-exchange the ghost ring and re-check the sum form's range next run")
@@ -511,14 +514,14 @@ PYBIND11_MODULE(_mxs_hip, m) {
                d["outer_wgs"] = s.halo_last_outer_wgs(s.time_block());
                // Paired ratios of the per-round maxima over ranks per candidate
                // outer set, and this rank's own ratios (diagnostics).
-               py::list rs, ls, hs;
+               py::list rs, ls;
                for (const auto& c : s.opening_ratio_samples()) rs.append(py::make_tuple(c.first, c.second));
                for (const auto& c : s.opening_local_ratio_samples()) ls.append(py::make_tuple(c.first, c.second));
-               for (const auto& c : s.opening_host_ratio_samples()) hs.append(py::make_tuple(c.first, c.second));
                d["candidate_ratios"] = rs;
                d["local_candidate_ratios"] = ls;
-               d["local_host_candidate_ratios"] = hs;
                d["agreement"] = s.agreement_path();
+               d["steady"] = s.steady_choice();
+               d["steady_reason"] = s.steady_reason();
                d["lead_us"] = s.opening_lead_us();
                d["lead_pass_us"] = s.opening_pass_us();
                d["lead_phases_us"] = s.opening_lead_phases();  // (exchange end, inner end, outer end)

@@ -150,6 +150,8 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
                             " replacements): the two-stream schedules serialise";
   }
   halo_last_on_ = halo_last_allowed_ && cfg_.opening == Opening::InteriorFirst;
+  steady_on_ = cfg_.steady == Opening::InteriorFirst;
+  if (cfg_.steady != Opening::Auto) steady_choice_ = steady_on_ ? "interior-first" : "serial";
   if (halo_last_on_) {
     opening_choice_ = "interior-first";
     opening_reason_ = "forced (opening = interior-first)";
@@ -371,10 +373,10 @@ template <typename T>
 void StencilSolver<T>::run_group(int S, int count, bool last_bare, bool first) {
   if (count <= 0) return;
   last_blocks_.emplace_back(S, count);
-  // SolverConfig::steady_interior_first: every super-step exchanges its own
-  // input under the core chunks (the same exchanges in the same order as the
-  // serial schedule: one per super-step, the first one the call's priming one).
-  if (cfg_.steady_interior_first && halo_last_on_ && post_exchange()) {
+  // Steady interior-first (SolverConfig::steady): every super-step exchanges
+  // its own input under the core chunks (the same exchanges in the same order
+  // as the serial schedule: one per super-step, the first the priming one).
+  if (steady_on_ && halo_last_on_ && post_exchange()) {
     join_side();
     if (first) last_opening_ = halo_last_pass(S, true) ? "interior-first" : "serial";
     for (int i = 0; i < count; ++i) {
@@ -711,39 +713,26 @@ void StencilSolver<T>::choose_opening(int S) {
   // the same moment in the same process, ran 5% faster than serial
   // (profiles/r05_decision/decision_vs_window.txt), so the decision kept
   // serial where it should not have.
-  constexpr bool kEventSamples = false;
-  Event e0(true), e1(true), e2(true);
-  double host_ms = 0;  // the last sample's host-clock span (enqueue to drained)
-  auto timed = [&](bool starts_on_side, auto&& enqueue) {
+  auto timed = [&](auto&& enqueue) {
     join_side();
     enqueue_block(cur_, nxt_, S);
     join_side();
     wait_idle("prepare: opening timing");
     device_barrier("prepare: opening timing");
-    const auto h0 = std::chrono::steady_clock::now();
-    if (kEventSamples) e0.record(starts_on_side ? side_.get() : main_.get());
-    enqueue();
-    if (kEventSamples) {
-      e1.record(main_.get());
-      e2.record(side_.get());
-    }
-    wait_idle("prepare: opening timing");
-    host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h0).count();
-    return kEventSamples ? std::max(double(e1.since(e0)), double(e2.since(e0))) : host_ms;
+    return host_span_ms(enqueue, "prepare: opening timing");
   };
   constexpr int kReps = 21;  // round 0 warms every shape (20 paired rounds: the notch is 1.58 IQR / sqrt(20))
   constexpr int nr = kReps - 1;
   // Per round: serial, then the three slots. v = [serial x nr, slot 0 x nr, slot 1 x nr, slot 2 x nr].
-  std::vector<double> v(size_t((1 + kCands) * nr), kMissingSample), vh(v.size(), 0.0);
+  std::vector<double> v(size_t((1 + kCands) * nr), kMissingSample);
   for (int rep = 0; rep < kReps; ++rep) {
-    const double serial = timed(false, [&] {
+    const double serial = timed([&] {
       prime_exchange();
       enqueue_bare_pass(cur_, nxt_, S);
     });
     if (rep > 0) v[size_t(rep - 1)] = serial;
-    if (rep > 0) vh[size_t(rep - 1)] = host_ms;
     for (int c = 0; c < kCands; ++c) {
-      const double ms = timed(cands[c] != nullptr, [&] {
+      const double ms = timed([&] {
         if (cands[c]) {
           enqueue_halo_last(cur_, nxt_, cands[c]);
         } else {
@@ -752,21 +741,15 @@ void StencilSolver<T>::choose_opening(int S) {
         }
       });
       if (rep > 0 && cands[c]) v[size_t((1 + c) * nr + rep - 1)] = ms;
-      if (rep > 0 && cands[c]) vh[size_t((1 + c) * nr + rep - 1)] = host_ms;
     }
   }
   // This rank's own paired ratios (diagnostics), then the agreed maxima.
   opening_local_ratio_samples_.clear();
-  opening_host_ratio_samples_.clear();
   for (int c = 0; c < kCands; ++c) {
     if (!cands[c]) continue;
-    std::vector<double> r(nr), rh(nr);
-    for (int i = 0; i < nr; ++i) {
-      r[size_t(i)] = v[size_t((1 + c) * nr + i)] / std::max(v[size_t(i)], 1e-12);
-      rh[size_t(i)] = vh[size_t((1 + c) * nr + i)] / std::max(vh[size_t(i)], 1e-12);
-    }
+    std::vector<double> r(nr);
+    for (int i = 0; i < nr; ++i) r[size_t(i)] = v[size_t((1 + c) * nr + i)] / std::max(v[size_t(i)], 1e-12);
     opening_local_ratio_samples_.emplace_back(cands[c]->sched.outer.blocks, std::move(r));
-    opening_host_ratio_samples_.emplace_back(cands[c]->sched.outer.blocks, std::move(rh));
   }
   agree_max(v, "prepare: opening agreement");
   std::vector<double> base(v.begin(), v.begin() + nr);
@@ -794,13 +777,89 @@ void StencilSolver<T>::choose_opening(int S) {
     std::snprintf(buf, sizeof(buf), "no rank-wide interior-first candidate (serial median %.4f ms)", d.baseline_ms);
   } else {
     std::snprintf(buf, sizeof(buf),
-                  "paired ratio of the per-round maxima over %d rank(s), interior-first / serial, %d rounds (GPU "
-                  "event spans): median %.3f, IQR %.3f, notch %.3f (switch at notch < %.3f); medians %.4f / %.4f "
+                  "paired ratio of the per-round maxima over %d rank(s), interior-first / serial, %d rounds (host "
+                  "clock, enqueue to drained): median %.3f, IQR %.3f, notch %.3f (switch at notch < %.3f); medians %.4f / %.4f "
                   "ms: %s; outer set %d workgroups from the measured exchange lead %.1f us of a %.1f us pass",
                   world_, nr, d.ratio, d.ratio_iqr, d.notch, 1.0 - cfg_.min_gain, d.candidate_ms, d.baseline_ms,
                   d.win ? "interior-first" : "serial kept", halo_last_outer_wgs(S), lead_us_, lead_pass_us_);
   }
   opening_reason_ = buf;
+}
+
+// SolverConfig::steady Auto, once (the first prepare() of a call with two or
+// more super-steps, after the opening chose interior-first): two back-to-back
+// super-steps from drained streams after a device barrier, the second one
+// serial (join, exchange of the first's output, pass) or interior-first again
+// (join, fork, inner chunks beside the exchange, outer chunks), host-timed as a
+// window, 20 paired rounds, per-round maxima over ranks (decision.hpp). The
+// samples advance the field (cur -> nxt -> cur): it is restored afterwards.
+template <typename T>
+void StencilSolver<T>::choose_steady(int S) {
+  if (cfg_.steady != Opening::Auto || !steady_choice_.empty() || !post_exchange()) return;
+  if (!halo_last_on_) {  // no interior-first opening: nothing to extend (config-level and agreed)
+    steady_choice_ = "serial";
+    steady_reason_ = "the opening is serial";
+    return;
+  }
+  HaloLastPass* hl = halo_last_pass(S, true);  // nullptr on a rank without the form: prime + pass instead
+  hipStream_t m = main_.get();
+  join_side();
+  wait_idle("prepare: steady timing");
+  const size_t bytes = size_t(tile_.alloc_elems()) * sizeof(T);
+  DeviceBuffer<T> snap(tile_.alloc_elems());
+  MXS_HIP_CHECK(hipMemcpyAsync(snap.get(), cur_, bytes, hipMemcpyDeviceToDevice, m));
+  T* const a = cur_;
+  T* const b = nxt_;
+  auto first = [&] {  // the call's interior-first opening, a -> b
+    if (hl) {
+      enqueue_halo_last(a, b, hl);
+    } else {
+      ex_->exchange(a, m);
+      core_pass(a, b, S, m);
+    }
+  };
+  auto sample = [&](bool steady) {
+    join_side();
+    wait_idle("prepare: steady timing");
+    device_barrier("prepare: steady timing");
+    return host_span_ms(
+        [&] {
+          first();
+          if (steady && hl) {
+            enqueue_halo_last(b, a, hl);
+          } else {
+            join_side();
+            ex_->exchange(b, m);
+            core_pass(b, a, S, m);
+          }
+        },
+        "prepare: steady timing");
+  };
+  constexpr int kReps = 21, nr = kReps - 1;  // round 0 warms both shapes
+  std::vector<double> v(size_t(2 * nr), 0.0);  // [serial x nr, steady x nr]
+  for (int rep = 0; rep < kReps; ++rep) {
+    const double ts = sample(false), ti = sample(true);
+    if (rep > 0) {
+      v[size_t(rep - 1)] = ts;
+      v[size_t(nr + rep - 1)] = ti;
+    }
+  }
+  join_side();
+  MXS_HIP_CHECK(hipMemcpyAsync(cur_, snap.get(), bytes, hipMemcpyDeviceToDevice, m));
+  wait_idle("prepare: steady timing");
+  ghost_fresh_ = false;
+  agree_max(v, "prepare: steady agreement");
+  const RoundDecision d = decide_on_maxima(std::vector<double>(v.begin(), v.begin() + nr),
+                                           {std::vector<double>(v.begin() + nr, v.end())}, cfg_.min_gain);
+  steady_on_ = d.win;
+  steady_choice_ = d.win ? "interior-first" : "serial";
+  char buf[320];
+  std::snprintf(buf, sizeof(buf),
+                "two super-steps, the second interior-first / serial, paired ratio of the per-round maxima over %d "
+                "rank(s), %d rounds (host clock): median %.3f, IQR %.3f, notch %.3f; medians %.4f / %.4f ms: %s",
+                world_, nr, d.ratio, d.ratio_iqr, d.notch, d.candidate_ms, d.baseline_ms,
+                d.win ? "interior-first" : "serial kept");
+  steady_reason_ = buf;
 }
 
 template <typename T>
@@ -891,21 +950,15 @@ void StencilSolver<T>::validate_direct(int S) {
     wait_idle("prepare: direct halo validation");
     return;
   }
-  // Timing (GPU events, as choose_opening), from drained streams after a
-  // barrier, each sample behind a state-preserving pass of its own path.
-  Event e0(true), e1(true), e2(true);
-  auto timed = [&](bool starts_on_side, auto&& warm, auto&& enqueue) {
+  // Timing as choose_opening (host clock, no events), from drained streams
+  // after a barrier, each sample behind a state-preserving pass of its own path.
+  auto timed = [&](auto&& warm, auto&& enqueue) {
     join_side();
     warm();
     join_side();
     wait_idle("prepare: direct halo timing");
     device_barrier("prepare: direct halo timing");
-    e0.record(starts_on_side ? side_.get() : m);
-    enqueue();
-    e1.record(m);  // both streams' ends, no join (choose_opening)
-    e2.record(side_.get());
-    wait_idle("prepare: direct halo timing");
-    return std::max(double(e1.since(e0)), double(e2.since(e0)));
+    return host_span_ms(enqueue, "prepare: direct halo timing");
   };
   auto direct_opening = [&] {  // the priming push, the wait for the neighbours' pushes, the pass
     direct_->push(cur_, m);
@@ -916,7 +969,7 @@ void StencilSolver<T>::validate_direct(int S) {
   std::vector<double> v(size_t(2 * nr), 0.0);  // [backend x nr, direct x nr]
   for (int rep = 0; rep < kReps; ++rep) {
     const double tb = timed(
-        halo_last_on_ && halo_last_pass(S, false), [&] { enqueue_block(cur_, nxt_, S); },
+        [&] { enqueue_block(cur_, nxt_, S); },
         [&] {
           if (halo_last_on_) {
             enqueue_opening(S, false);
@@ -925,7 +978,7 @@ void StencilSolver<T>::validate_direct(int S) {
             core_pass(cur_, nxt_, S, m);
           }
         });
-    const double td = timed(false, direct_opening, direct_opening);
+    const double td = timed(direct_opening, direct_opening);
     if (rep > 0) {
       v[size_t(rep - 1)] = tb;
       v[size_t(nr + rep - 1)] = td;
@@ -1122,6 +1175,7 @@ void StencilSolver<T>::prepare(int iters) {
   // Opening::Auto: decide the opening at the depth of the larger group.
   const Group& big = gr[0].count >= gr[1].count ? gr[0] : gr[1];
   if (big.count > 0) choose_opening(big.S);
+  if (gr[0].count + gr[1].count >= 2) choose_steady(big.S);
   if (big.count > 0) validate_direct(big.S);
   // Every collective below is issued the same number of times on every rank,
   // whatever this rank's forms and decisions: one priming exchange when the

@@ -89,10 +89,11 @@ class StencilConfig:
     # maxima is below 1 - min_gain with 95% confidence (runtime/decision.hpp).
     opening: str = "auto"
     min_gain: float = 0.0
-    # Super-steps after the opening: "serial" (pass, then the exchange of its
-    # output) or "interior-first" (each super-step like the opening, when the
-    # opening is interior-first).
-    steady: str = "serial"
+    # Super-steps after an interior-first opening: "serial" (pass, then the
+    # exchange of its output), "interior-first" (each super-step like the
+    # opening), or "auto" (prepare() of a call with >= 2 super-steps times both
+    # and all ranks adopt the faster).
+    steady: str = "auto"
     # Single GPU with loopback: follow the peers' schedule (every call primes,
     # the last pass of a call is bare, the opening is chosen as with peers), so
     # one GPU rehearses the window an N-GPU run executes.
@@ -214,7 +215,7 @@ class Stencil2D:
                                           self._direct_mode(backend),
                                           cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain,
                                           cfg.halo_max_ctas, cfg.main_priority, cfg.side_priority,
-                                          cfg.wire_delay_us, cfg.direct_engine, cfg.steady == "interior-first")
+                                          cfg.wire_delay_us, cfg.direct_engine, cfg.steady)
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()
@@ -418,7 +419,8 @@ class Stencil2D:
         wd = self.solver.wire_delay_us()
         if wd:
             text += f" (+ {wd:g} us of rehearsed wire time after each transfer)"
-        if opening == "interior-first" and self.cfg.steady == "interior-first" and passes > 1:
+        steady = self.solver.schedule_times().get("steady") == "interior-first"
+        if opening == "interior-first" and steady and passes > 1:
             text += ("; every super-step interior-first (its exchange ran under the chunks that read only core "
                      "cells, the ghost-ring chunks after it)")
         elif opening == "interior-first":
@@ -429,7 +431,7 @@ class Stencil2D:
         elif opening == "overlap":
             text += "; thin-strip overlap (interior on a second stream while each exchange runs)"
         if (self.solver.multi_rank() and not self.solver.direct_halo() and not self.solver.overlapped()
-                and not (self.cfg.steady == "interior-first" and opening == "interior-first")):
+                and not (steady and opening == "interior-first")):
             text += "; the call's last pass is bare (the next call primes)"
         return text
 

@@ -316,6 +316,34 @@ def test_steady_interior_first_bitwise_vs_serial(gpu, runs):
     assert torch.equal(a.core_view(), b.core_view())
 
 
+def test_steady_auto_decision_keeps_the_state(gpu):
+    """steady = auto (default): prepare() of a call with two or more super-steps
+    times two back-to-back super-steps with the second serial or interior-first
+    (paired rounds, host clock) and keeps the faster; the samples advance the
+    field twice and it is restored, so the run that follows is bitwise the
+    serial schedule's. One super-step or a serial opening: nothing is timed."""
+    a = _loopback(16384, 8192, seed=84, opening="interior-first", rehearse_peers=True, time_block=20)
+    b = _loopback(16384, 8192, seed=84, opening="serial", rehearse_peers=True, time_block=20)
+    a.run(20)
+    a.prepare(20)
+    assert a.solver.schedule_times()["steady"] == ""  # one super-step: undecided
+    a.prepare(60)
+    t = a.solver.schedule_times()
+    assert t["steady"] in ("serial", "interior-first"), t
+    assert "paired ratio of the per-round maxima over 1 rank(s), 20 rounds" in t["steady_reason"], t["steady_reason"]
+    a.run(60)
+    assert a.solver.last_run_exchanges() == 3
+    assert ("every super-step interior-first" in a.halo_mode()) == (t["steady"] == "interior-first")
+    b.run(80)
+    a.synchronize()
+    b.synchronize()
+    assert torch.equal(a.core_view(), b.core_view())
+    s = _loopback(4096, 2048, seed=84, opening="serial", rehearse_peers=True, time_block=24)
+    s.prepare(48)
+    assert s.solver.schedule_times()["steady"] == "serial"
+    assert s.solver.schedule_times()["steady_reason"] == "the opening is serial"
+
+
 def test_interior_first_warm_prepare_keep_the_state(gpu):
     """prepare() launches the interior-first opening into the scratch buffer
     (cur -> nxt, cur's ring re-exchanged with the same values), warm() the
