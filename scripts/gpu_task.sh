@@ -18,7 +18,8 @@
 #                          interior-first), fused; suffixes: -wNN adds NN us of rehearsed wire time per
 #                          transfer (--wire-delay-us), -cNN --halo-max-ctas NN, -ssync / -psync / -tsync
 #                          --window-sync solver / poll / torch, -p00 / -p11 stream priorities
-#                          -st --steady interior-first (in that order, e.g. ifirst-c16-w40-st)
+#                          -st / -ss --steady interior-first / serial (default auto) (in that order,
+#                          e.g. ifirst-c16-w40-st)
 #                          -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
 #   final                  tests + smoke + the driver's bench command + its kernel-trace profile
@@ -98,6 +99,7 @@ task_window() {
       case $base in *-ssync) args+=(--window-sync solver); base=${base%-ssync} ;; esac
       case $base in *-psync) args+=(--window-sync poll); base=${base%-psync} ;; esac
       case $base in *-st) args+=(--steady interior-first); base=${base%-st} ;; esac
+      case $base in *-ss) args+=(--steady serial); base=${base%-ss} ;; esac
       if [[ $base =~ ^(.*)-w([0-9]+)$ ]]; then args+=(--wire-delay-us "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi
       if [[ $base =~ ^(.*)-c([0-9]+)$ ]]; then args+=(--halo-max-ctas "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi
       case $base in
@@ -123,7 +125,7 @@ print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["
                   "choice": {k: (e.get("schedule_choice") or {}).get(k) for k in ("opening", "ratio", "ratio_iqr",
                                                                                    "outer_wgs", "serial_ms",
                                                                                    "interior_first_ms", "lead_us",
-                                                                                   "lead_pass_us")},
+                                                                                   "lead_pass_us", "steady")},
                   "phases": e.get("window_phases")}))
 PY
     done
