@@ -100,6 +100,7 @@
 
 #include <chrono>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 #include <tuple>
@@ -109,6 +110,7 @@
 #include "mxs/halo/exchange.hpp"
 #include "mxs/halo/ipc_direct.hpp"
 #include "mxs/kernels/kernels.hpp"
+#include "mxs/runtime/decision.hpp"
 #include "mxs/runtime/hip_utils.hpp"
 
 namespace mxs {
@@ -444,6 +446,8 @@ class StencilSolver {
   std::string opening_reason_;
   void choose_opening(int S);                // Opening::Auto: time both, agree, keep the faster
   void choose_steady(int S);                 // SolverConfig::steady Auto: the same for two super-steps
+  RoundDecision paired_rounds(int rounds, const std::vector<std::function<double()>>& kinds,
+                              const std::vector<bool>& have, const char* phase, std::vector<double>* local = nullptr);
   bool steady_on_ = false;                   // every super-step interior-first (with the opening)
   std::string steady_choice_, steady_reason_;
   bool side_pending_ = false;                // side-stream work not yet joined to main

@@ -721,18 +721,16 @@ void StencilSolver<T>::choose_opening(int S) {
     device_barrier("prepare: opening timing");
     return host_span_ms(enqueue, "prepare: opening timing");
   };
-  constexpr int kReps = 21;  // round 0 warms every shape (20 paired rounds: the notch is 1.58 IQR / sqrt(20))
-  constexpr int nr = kReps - 1;
-  // Per round: serial, then the three slots. v = [serial x nr, slot 0 x nr, slot 1 x nr, slot 2 x nr].
-  std::vector<double> v(size_t((1 + kCands) * nr), kMissingSample);
-  for (int rep = 0; rep < kReps; ++rep) {
-    const double serial = timed([&] {
+  constexpr int nr = 20;  // paired rounds: the notch is 1.58 IQR / sqrt(20)
+  std::vector<std::function<double()>> kinds{[&] {
+    return timed([&] {
       prime_exchange();
       enqueue_bare_pass(cur_, nxt_, S);
     });
-    if (rep > 0) v[size_t(rep - 1)] = serial;
-    for (int c = 0; c < kCands; ++c) {
-      const double ms = timed([&] {
+  }};
+  for (int c = 0; c < kCands; ++c)
+    kinds.emplace_back([&, c] {
+      return timed([&] {
         if (cands[c]) {
           enqueue_halo_last(cur_, nxt_, cands[c]);
         } else {
@@ -740,22 +738,17 @@ void StencilSolver<T>::choose_opening(int S) {
           enqueue_bare_pass(cur_, nxt_, S);
         }
       });
-      if (rep > 0 && cands[c]) v[size_t((1 + c) * nr + rep - 1)] = ms;
-    }
-  }
-  // This rank's own paired ratios (diagnostics), then the agreed maxima.
-  opening_local_ratio_samples_.clear();
+    });
+  std::vector<double> local;
+  const RoundDecision d = paired_rounds(nr, kinds, {true, !!cands[0], !!cands[1], !!cands[2]},
+                                        "prepare: opening agreement", &local);
+  opening_local_ratio_samples_.clear();  // this rank's own paired ratios (diagnostics)
   for (int c = 0; c < kCands; ++c) {
     if (!cands[c]) continue;
     std::vector<double> r(nr);
-    for (int i = 0; i < nr; ++i) r[size_t(i)] = v[size_t((1 + c) * nr + i)] / std::max(v[size_t(i)], 1e-12);
+    for (int i = 0; i < nr; ++i) r[size_t(i)] = local[size_t((1 + c) * nr + i)] / std::max(local[size_t(i)], 1e-12);
     opening_local_ratio_samples_.emplace_back(cands[c]->sched.outer.blocks, std::move(r));
   }
-  agree_max(v, "prepare: opening agreement");
-  std::vector<double> base(v.begin(), v.begin() + nr);
-  std::vector<std::vector<double>> cand(kCands);
-  for (int c = 0; c < kCands; ++c) cand[size_t(c)].assign(v.begin() + (1 + c) * nr, v.begin() + (2 + c) * nr);
-  const RoundDecision d = decide_on_maxima(base, cand, cfg_.min_gain);
   opening_ms_[0] = d.baseline_ms;
   opening_ms_[1] = d.best >= 0 ? d.candidate_ms : 0.0;
   opening_spread_[0] = d.baseline_iqr;
@@ -819,38 +812,30 @@ void StencilSolver<T>::choose_steady(int S) {
     }
   };
   auto sample = [&](bool steady) {
-    join_side();
-    wait_idle("prepare: steady timing");
-    device_barrier("prepare: steady timing");
-    return host_span_ms(
-        [&] {
-          first();
-          if (steady && hl) {
-            enqueue_halo_last(b, a, hl);
-          } else {
-            join_side();
-            ex_->exchange(b, m);
-            core_pass(b, a, S, m);
-          }
-        },
-        "prepare: steady timing");
+    return [&, steady] {
+      join_side();
+      wait_idle("prepare: steady timing");
+      device_barrier("prepare: steady timing");
+      return host_span_ms(
+          [&] {
+            first();
+            if (steady && hl) {
+              enqueue_halo_last(b, a, hl);
+            } else {
+              join_side();
+              ex_->exchange(b, m);
+              core_pass(b, a, S, m);
+            }
+          },
+          "prepare: steady timing");
+    };
   };
-  constexpr int kReps = 21, nr = kReps - 1;  // round 0 warms both shapes
-  std::vector<double> v(size_t(2 * nr), 0.0);  // [serial x nr, steady x nr]
-  for (int rep = 0; rep < kReps; ++rep) {
-    const double ts = sample(false), ti = sample(true);
-    if (rep > 0) {
-      v[size_t(rep - 1)] = ts;
-      v[size_t(nr + rep - 1)] = ti;
-    }
-  }
+  constexpr int nr = 20;
+  const RoundDecision d = paired_rounds(nr, {sample(false), sample(true)}, {true, true}, "prepare: steady agreement");
   join_side();
   MXS_HIP_CHECK(hipMemcpyAsync(cur_, snap.get(), bytes, hipMemcpyDeviceToDevice, m));
   wait_idle("prepare: steady timing");
   ghost_fresh_ = false;
-  agree_max(v, "prepare: steady agreement");
-  const RoundDecision d = decide_on_maxima(std::vector<double>(v.begin(), v.begin() + nr),
-                                           {std::vector<double>(v.begin() + nr, v.end())}, cfg_.min_gain);
   steady_on_ = d.win;
   steady_choice_ = d.win ? "interior-first" : "serial";
   char buf[320];
@@ -860,6 +845,29 @@ void StencilSolver<T>::choose_steady(int S) {
                 world_, nr, d.ratio, d.ratio_iqr, d.notch, d.candidate_ms, d.baseline_ms,
                 d.win ? "interior-first" : "serial kept");
   steady_reason_ = buf;
+}
+
+// Collective: rounds + 1 rounds, each sampling every kind once in order
+// (kinds[0] the baseline); round 0 warms every shape and is dropped. A kind a
+// rank lacks (have[k] false) still runs its sampler, which issues the same
+// collectives as the others, and is marked missing. The ranks agree on the
+// per-round maxima (one element-wise max) and decide on their paired ratios.
+template <typename T>
+RoundDecision StencilSolver<T>::paired_rounds(int rounds, const std::vector<std::function<double()>>& kinds,
+                                              const std::vector<bool>& have, const char* phase,
+                                              std::vector<double>* local) {
+  const size_t nk = kinds.size(), nr = size_t(rounds);
+  std::vector<double> v(nk * nr, kMissingSample);  // [kind 0 x rounds, kind 1 x rounds, ...]
+  for (size_t rep = 0; rep <= nr; ++rep)
+    for (size_t k = 0; k < nk; ++k) {
+      const double ms = kinds[k]();
+      if (rep > 0 && have[k]) v[k * nr + rep - 1] = ms;
+    }
+  if (local) *local = v;
+  agree_max(v, phase);
+  std::vector<std::vector<double>> cand(nk - 1);
+  for (size_t k = 1; k < nk; ++k) cand[k - 1].assign(v.begin() + long(k * nr), v.begin() + long((k + 1) * nr));
+  return decide_on_maxima(std::vector<double>(v.begin(), v.begin() + long(nr)), cand, cfg_.min_gain);
 }
 
 template <typename T>
@@ -965,28 +973,20 @@ void StencilSolver<T>::validate_direct(int S) {
     direct_->wait(m);
     update(cur_, nxt_, S, 0, w, 0, h, m);
   };
-  constexpr int kReps = 13, nr = kReps - 1;
-  std::vector<double> v(size_t(2 * nr), 0.0);  // [backend x nr, direct x nr]
-  for (int rep = 0; rep < kReps; ++rep) {
-    const double tb = timed(
-        [&] { enqueue_block(cur_, nxt_, S); },
-        [&] {
-          if (halo_last_on_) {
-            enqueue_opening(S, false);
-          } else {
-            prime_exchange();
-            core_pass(cur_, nxt_, S, m);
-          }
-        });
-    const double td = timed(direct_opening, direct_opening);
-    if (rep > 0) {
-      v[size_t(rep - 1)] = tb;
-      v[size_t(nr + rep - 1)] = td;
-    }
-  }
-  agree_max(v, "prepare: direct halo timing");
-  const RoundDecision d = decide_on_maxima(std::vector<double>(v.begin(), v.begin() + nr),
-                                           {std::vector<double>(v.begin() + nr, v.end())}, cfg_.min_gain);
+  constexpr int nr = 12;
+  auto backend = [&] {
+    return timed([&] { enqueue_block(cur_, nxt_, S); },
+                 [&] {
+                   if (halo_last_on_) {
+                     enqueue_opening(S, false);
+                   } else {
+                     prime_exchange();
+                     core_pass(cur_, nxt_, S, m);
+                   }
+                 });
+  };
+  const RoundDecision d = paired_rounds(nr, {backend, [&] { return timed(direct_opening, direct_opening); }},
+                                        {true, true}, "prepare: direct halo timing");
   direct_ms_[0] = d.baseline_ms;
   direct_ms_[1] = d.candidate_ms;
   char buf[320];
