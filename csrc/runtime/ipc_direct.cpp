@@ -112,18 +112,27 @@ __global__ void signal_kernel(FlagSet f, u64* epoch) {
 }
 
 // Spin (one lane per neighbour) until its counter reaches the local epoch.
+// Launched as kWaitWgs workgroups, which the dispatcher deals round-robin over
+// the 8 XCDs: every XCD observes the flags and then takes a system-scope
+// acquire itself, so no XCD's L2 keeps a stale line of the ghost ring for
+// the pass that follows (the ring is read by workgroups on all 8 XCDs; one
+// waiting workgroup would invalidate only its own XCD's L2).
+constexpr int kWaitWgs = 64;
 __global__ void wait_kernel(FlagSet f, const u64* epoch, u64* status, u64 timeout_ticks) {
   const u64 e = *epoch;
-  if (int(threadIdx.x) >= f.n) return;
-  const u64 t0 = wall_clock64();
-  while (ld_acquire_sys(f.flag[threadIdx.x]) < e) {
-    if (wall_clock64() - t0 > timeout_ticks) {
-      atomicCAS(status, 0ull, 1ull);
-      return;
+  if (int(threadIdx.x) < f.n) {
+    const u64 t0 = wall_clock64();
+    while (ld_acquire_sys(f.flag[threadIdx.x]) < e) {
+      if (wall_clock64() - t0 > timeout_ticks) {
+        atomicCAS(status, 0ull, 1ull);
+        break;
+      }
+      if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) break;
+      __builtin_amdgcn_s_sleep(1);
     }
-    if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
-    __builtin_amdgcn_s_sleep(1);
   }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, on this workgroup's XCD
 }
 
 // ------------------------------------------------------------------ setup
@@ -327,7 +336,7 @@ void IpcDirectHalo<T>::wait(hipStream_t s) {
   Impl& I = *impl_;
   if (I.wait.n == 0) return;
   MXS_TRACE_RANGE("halo.ipc_direct_wait");
-  wait_kernel<<<1, 64, 0, s>>>(I.wait, I.epoch(), I.status(), I.timeout_ticks);
+  wait_kernel<<<kWaitWgs, 64, 0, s>>>(I.wait, I.epoch(), I.status(), I.timeout_ticks);
   MXS_HIP_CHECK_LAUNCH();
 }
 

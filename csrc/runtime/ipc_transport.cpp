@@ -118,10 +118,16 @@ __global__ void ipc_free_wait_kernel(const PutDesc<T>* __restrict__ descs, int n
   if (int(threadIdx.x) < n) spin_ge(descs[threadIdx.x].local_free, k - 1, timeout_ticks, status, 1);
 }
 
+// kWaitWgs workgroups, dealt round-robin over the 8 XCDs: each observes the
+// ready counters and takes a system-scope acquire, so the unpack that follows
+// (workgroups on every XCD) finds no stale line of a receive slot in any L2.
+constexpr int kWaitWgs = 64;
 __global__ void ipc_wait_kernel(const WaitDesc* __restrict__ descs, int n, const u64* epoch, u64* status,
                                 u64 timeout_ticks) {
   const u64 k = *epoch + 1;
   if (int(threadIdx.x) < n) spin_ge(descs[threadIdx.x].ready, k, timeout_ticks, status, 2);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope, on this workgroup's XCD
 }
 
 __global__ void ipc_release_kernel(const ReleaseDesc* __restrict__ descs, int n, u64* epoch) {
@@ -359,7 +365,7 @@ void IpcHaloTransport<T>::wait(hipStream_t s) {
   Impl& I = *impl_;
   if (!I.nwait) return;
   MXS_TRACE_RANGE("halo.ipc_wait");
-  ipc_wait_kernel<<<1, 64, 0, s>>>(I.wait_d.get(), I.nwait, I.ctrl + I.L.epoch(), I.ctrl + I.L.status(),
+  ipc_wait_kernel<<<kWaitWgs, 64, 0, s>>>(I.wait_d.get(), I.nwait, I.ctrl + I.L.epoch(), I.ctrl + I.L.status(),
                                    I.timeout_ticks);
   MXS_HIP_CHECK_LAUNCH();
 }

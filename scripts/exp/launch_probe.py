@@ -1,18 +1,25 @@
-"""Host cost of one timed window's enqueue on the fused 8-GPU tile and the 1-GPU
-tile: Stencil2D.run(20) (Python -> solver.run -> one pipeline launch), the bare
-pybind stencil5_tb launch of the same pass, and an empty torch kernel, each
-timed on the host from call to return (the GPU drained before each call), and
-the GPU's idle gap from the call to the kernel's start (an event recorded just
-before the call on the same stream is not possible from Python for the solver's
-own stream, so the gap is estimated as window - event-timed pass).
+"""Where the fixed per-window host cost goes (round-4 verdict, Weak 6). One
+process, interleaved rounds of four windows, each from a drained device and
+timed on the host clock like the bench's window (t0, enqueue, device sync):
 
-usage: python scripts/exp/launch_probe.py [REPS]"""
+  empty    one spin_delay(0) launch (a one-wave kernel that returns at once):
+           the floor of launch + completion + sync on this box;
+  fused    run(20) of the fused-periodic 8-GPU tile (one 20-level pass);
+  pass     the same pass launched directly (stencil5_tb, no solver);
+  span     the fused pass's GPU time alone (events around it, median).
+
+Prints per-kind medians of the window and of the enqueue (t0 to the launch
+call's return); fused - span is the window's fixed cost, empty is the part of
+it any single launch pays.
+
+usage: python scripts/exp/launch_probe.py [TILE] [ROUNDS]"""
 import json
-import os
+import statistics
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.dirname(
+    __import__("os").path.abspath(__file__)))))
 
 import torch  # noqa: E402
 
@@ -20,50 +27,53 @@ from cuda_mpi_scratch_amd import hip  # noqa: E402
 from cuda_mpi_scratch_amd.models.stencil2d import Stencil2D, StencilConfig  # noqa: E402
 
 
-def med(v):
-    v = sorted(v)
-    return round(v[len(v) // 2], 2)
-
-
 def main() -> int:
-    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 50
+    tile = sys.argv[1] if len(sys.argv) > 1 else "16384x8192"
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 60
+    w, h = (int(x) for x in tile.split("x"))
     H = hip()
-    out = {}
-    for tile in ("16384x8192", "32768x32768"):
-        w, h = (int(x) for x in tile.split("x"))
-        st = Stencil2D(StencilConfig(global_width=w, global_height=h, dims="1x1", dtype="f32", seed=3))
-        st.run(20)
-        st.prepare(20)
-        st.synchronize()
-        a = st.current()
-        b = st.b if a.data_ptr() == st.a.data_ptr() else st.a
-        s = torch.cuda.current_stream()
-        t_run, t_launch, t_empty, t_window = [], [], [], []
-        x = torch.zeros(1, device="cuda")
-        for _ in range(reps):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            st.run(20)
-            t1 = time.perf_counter()
-            torch.cuda.synchronize()
-            t2 = time.perf_counter()
-            t_run.append((t1 - t0) * 1e6)
-            t_window.append((t2 - t0) * 1e6)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            H.stencil5_tb(a.data_ptr(), b.data_ptr(), st.geom, 20, 0, w, 0, h, 0.2, 0.2, True, stream=s.cuda_stream)
-            t1 = time.perf_counter()
-            t_launch.append((t1 - t0) * 1e6)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            x.add_(1.0)
-            t1 = time.perf_counter()
-            t_empty.append((t1 - t0) * 1e6)
-        out[tile] = {"run20_host_us": med(t_run), "pybind_stencil5_tb_host_us": med(t_launch),
-                     "torch_add_host_us": med(t_empty), "run20_window_us": med(t_window)}
-        print(json.dumps({tile: out[tile]}), flush=True)
-        del st
-        torch.cuda.empty_cache()
+    st = Stencil2D(StencilConfig(global_width=w, global_height=h, dims="1x1", dtype="f32", seed=5))
+    st.run(20)
+    st.prepare(20)
+    st.warm(20, 0.2)
+    st.synchronize()
+    s = torch.cuda.current_stream()
+    a, b = st.a, st.b
+    g = st.geom
+    rows = {"empty": ([], []), "fused": ([], []), "pass": ([], []), "span": ([], [])}
+
+    def window(kind, fn):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        tr = time.perf_counter()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        rows[kind][0].append((t1 - t0) * 1e6)
+        rows[kind][1].append((tr - t0) * 1e6)
+
+    def direct_pass():
+        H.stencil5_tb(a.data_ptr(), b.data_ptr(), g, 20, 0, w, 0, h, 0.2, 0.2, True, dtype="f32",
+                      stream=s.cuda_stream, variant="auto", sum_form=True)
+
+    for _ in range(rounds):
+        window("empty", lambda: H.spin_delay(0.0, s.cuda_stream))
+        window("fused", lambda: st.run(20))
+        window("pass", direct_pass)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        e0.record(s)
+        direct_pass()
+        e1.record(s)
+        torch.cuda.synchronize()
+        rows["span"][0].append(e0.elapsed_time(e1) * 1e3)
+        rows["span"][1].append(0.0)
+    out = {"tile": tile, "rounds": rounds, "solver_stream_is_torch_current": False}
+    for k, (win, enq) in rows.items():
+        out[k] = {"window_us_median": round(statistics.median(win), 1), "window_us_p10": round(sorted(win)[len(win) // 10], 1),
+                  "enqueue_us_median": round(statistics.median(enq), 1)}
+    out["fixed_cost_us"] = round(out["fused"]["window_us_median"] - out["span"]["window_us_median"], 1)
+    print(json.dumps(out), flush=True)
     return 0
 
 
