@@ -74,6 +74,26 @@ def main() -> int:
                   "enqueue_us_median": round(statistics.median(enq), 1)}
     out["fixed_cost_us"] = round(out["fused"]["window_us_median"] - out["span"]["window_us_median"], 1)
     print(json.dumps(out), flush=True)
+    # B. The bench's shape: warm() (~200 ms of passes), drain, then three
+    # windows in a row; with --pre, an empty kernel + sync just before the
+    # first window's t0 (outside it). Is the first window after the burst the
+    # slow one, and does a pre-launch change that?
+    seq = {"after_warm": [[], [], []], "after_warm_pre": [[], [], []]}
+    for r in range(max(4, rounds // 6)):
+        for kind in seq:
+            st.warm(20, 0.2)
+            st.synchronize()
+            torch.cuda.synchronize()
+            for i in range(3):
+                if kind.endswith("_pre") and i == 0:
+                    H.spin_delay(0.0, s.cuda_stream)
+                    torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                st.run(20)
+                torch.cuda.synchronize()
+                seq[kind][i].append((time.perf_counter() - t0) * 1e6)
+    print(json.dumps({k: [round(statistics.median(v), 1) for v in vs] for k, vs in seq.items()}
+                     | {"raw_" + k: [[round(x, 1) for x in v] for v in vs] for k, vs in seq.items()}), flush=True)
     return 0
 
 
