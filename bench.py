@@ -78,7 +78,7 @@ PINGPONG_SIZES = [8 << i for i in range(26)]  # 8 B .. 256 MiB
 SUMMARY_SIZES = {"1MiB": 1 << 20, "16MiB": 16 << 20, "256MiB": 256 << 20}
 
 
-ENV_PREFIXES = ("MXS_", "NCCL_", "RCCL_", "HIP_", "HSA_", "GPU_", "ROCR_", "TORCH_NCCL_")
+ENV_PREFIXES = ("MXS_", "NCCL_", "RCCL_", "HIP_", "HSA_", "GPU_", "ROCR_", "ROC_", "TORCH_NCCL_")
 # MXS_* variables a release build reads (not tuning knobs): recorded, allowed.
 MXS_RUNTIME_ENV = {"MXS_IPC_CROSS_DEVICE", "MXS_BUILD_DIR"}
 

@@ -19,7 +19,8 @@
 #                          transfer (--wire-delay-us), -cNN --halo-max-ctas NN, -ssync / -psync / -tsync
 #                          --window-sync solver / poll / torch, -p00 / -p11 stream priorities
 #                          -st / -ss --steady interior-first / serial (default auto) (in that order,
-#                          e.g. ifirst-c16-w40-st)
+#                          e.g. ifirst-c16-w40-st); a final -aw runs it with ROC_ACTIVE_WAIT_TIMEOUT=2000
+#                          (the HIP runtime spins up to 2 ms on a wait before sleeping on an interrupt)
 #                          -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
 #   final                  tests + smoke + the driver's bench command + its kernel-trace profile
@@ -92,7 +93,8 @@ task_window() {
   for i in $(seq "$reps"); do
     for mode in $modes; do
       local args=(--global "$tile" --steps "${WINDOW_STEPS:-20}" --warmup 5 --no-extras)
-      local base=$mode
+      local base=$mode envs=()
+      case $base in *-aw) envs+=(ROC_ACTIVE_WAIT_TIMEOUT=2000); base=${base%-aw} ;; esac
       case $base in *-p00) args+=(--stream-priorities=0,0); base=${base%-p00} ;; esac
       case $base in *-p11) args+=(--stream-priorities=-1,-1); base=${base%-p11} ;; esac
       case $base in *-tsync) args+=(--window-sync torch); base=${base%-tsync} ;; esac
@@ -109,7 +111,7 @@ task_window() {
         fused) ;;
         *) echo "unknown window mode '$mode'"; exit 2 ;;
       esac
-      timeout -k 10 200 python bench.py "${args[@]}" > "$OUT/window_last.txt" 2>&1 || {
+      env "${envs[@]}" timeout -k 10 200 python bench.py "${args[@]}" > "$OUT/window_last.txt" 2>&1 || {
         echo "window run failed ($mode)"
         tail -30 "$OUT/window_last.txt"
         exit 1
