@@ -24,6 +24,8 @@
 // --iters N, --warmup N, --time-block S (default: measured per tile size and dtype), --no-overlap, --no-graph,
 // --opening auto|serial|interior-first (--halo-last = interior-first; default auto: prepare() times the
 // serial and interior-first openings, agrees the per-round maxima over all ranks and keeps the faster),
+// --steady auto|serial|interior-first (the super-steps after an interior-first opening; auto: prepare() of a
+// run with two or more super-steps times both the same way),
 // --no-direct-halo (IPC backend: pack -> put -> unpack instead of the device-initiated push),
 // --halo-max-ctas N (RCCL: the halo exchange on a communicator split off with at most N workgroups per kernel),
 // --direct-halo on|off|validate (validate: prepare() compares the push with the backend's exchange bitwise on
@@ -141,6 +143,10 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
   MXS_CHECK(opening == "auto" || opening == "serial" || opening == "interior-first",
             "--opening must be auto, serial or interior-first, got " << opening);
   cfg.opening = opening == "serial" ? Opening::Serial : opening == "interior-first" ? Opening::InteriorFirst : Opening::Auto;
+  const std::string steady = cli.get("steady", "auto");
+  MXS_CHECK(steady == "auto" || steady == "serial" || steady == "interior-first",
+            "--steady must be auto, serial or interior-first, got " << steady);
+  cfg.steady = steady == "serial" ? Opening::Serial : steady == "interior-first" ? Opening::InteriorFirst : Opening::Auto;
   cfg.halo_max_ctas = int(cli.get_int("halo-max-ctas", 0));  // RCCL: the halo on a CTA-capped communicator
   cfg.loopback_self = loopback;
   cfg.coeffs = {c_center, c_neighbor, sum_form};
@@ -264,6 +270,7 @@ int run(MpiEnv& env, const Cli& cli, const CartTopology& topo, const DeviceBindi
         js << ", \"interior_first_opening\": " << (solver->halo_last(solver->time_block()) ? "true" : "false");
         if (!solver->opening_choice().empty()) js << ", \"opening_choice\": \"" << solver->opening_choice() << "\"";
         js << ", \"last_opening\": \"" << solver->last_run_opening() << "\"";
+        if (!solver->steady_choice().empty()) js << ", \"steady_choice\": \"" << solver->steady_choice() << "\"";
         if (!solver->direct_state().empty()) js << ", \"direct_halo\": \"" << solver->direct_state() << "\"";
       }
       if (want_sum) js << ", \"checksum\": " << app::fmt(checksum);
