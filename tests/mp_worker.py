@@ -130,7 +130,8 @@ def task_gpu_solver(args):
             per_run.append([int(st.solver.last_run_exchanges()), sum(c for _, c in st.solver.last_run_blocks())])
             openings.append(st.solver.last_run_opening())
     st.synchronize()
-    g = st.gather_global()
+    want_grid = args.get("return_grid", True)  # the same on every rank: gather_global is collective
+    g = st.gather_global() if want_grid else None
     out = {"rank": ctx.rank, "backend": st.backend, "halo": st.halo_mode(), "graph": st.graph_status(),
            "native": st.solver is not None, "time_block": st.time_block}
     if st.solver is not None:
@@ -145,7 +146,7 @@ def task_gpu_solver(args):
         if st.comm is not None:
             out["rccl_ranks"] = int(st.comm.count())
             out["rccl_device"] = int(st.comm.device())
-    if ctx.rank == 0:
+    if ctx.rank == 0 and want_grid:
         out["grid"] = g.double().tolist()
     ctx.barrier()
     ctx.destroy()
