@@ -31,9 +31,10 @@ def test_solver_one_rank_per_gpu(gpu, n, dims, backend, time_block, overlap, mon
     assert (got - ref).abs().max().item() < 1e-5
 
 
-@pytest.mark.parametrize("transport,mode", [("rccl", "async"), ("rccl", "bidir"), ("ipc", "async")])
+@pytest.mark.parametrize("transport,mode", [("rccl", "async"), ("rccl", "bidir"), ("ipc", "async"),
+                                            ("peer-copy", "async"), ("peer-copy", "bidir")])
 def test_pingpong_two_gpus(gpu, transport, mode, monkeypatch):
-    if transport == "ipc":
+    if transport in ("ipc", "peer-copy"):
         monkeypatch.setenv("MXS_IPC_CROSS_DEVICE", "1")  # the device-initiated transport across xGMI, opt-in
     res = run_ranks("pingpong", 2, {"transport": transport, "mode": mode, "sizes": [8, 4099, 1 << 20, 64 << 20]},
                     gpu=True, timeout=600)
