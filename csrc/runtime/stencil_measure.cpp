@@ -327,6 +327,7 @@ template <typename T>
 RoundDecision StencilSolver<T>::paired_rounds(int rounds, const std::vector<std::function<double()>>& kinds,
                                               const std::vector<bool>& have, const char* phase,
                                               std::vector<double>* local) {
+  MXS_CHECK(!kinds.empty() && have.size() == kinds.size() && rounds > 0, "paired_rounds: one have-flag per kind");
   const size_t nk = kinds.size(), nr = size_t(rounds);
   std::vector<double> v(nk * nr, kMissingSample);  // [kind 0 x rounds, kind 1 x rounds, ...]
   for (size_t rep = 0; rep <= nr; ++rep)
