@@ -24,6 +24,7 @@
 #                          -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
 #   final                  tests + smoke + the driver's bench command + its kernel-trace profile
+#   warmsweep REPS TILE W...  the driver's 20-step window after W ms of clock warm-up, interleaved
 set -uo pipefail
 OUT="gpurun_out/${1:?usage: gpu_task.sh OUT TASK [ARGS...]}"
 TASK="${2:?usage: gpu_task.sh OUT TASK [ARGS...]}"
@@ -177,6 +178,32 @@ for w in (200, 1000):
 PY
 }
 
+task_warmsweep() {  # REPS TILE W...: the driver's window (--steps 20) after W ms of clock warm-up, interleaved
+  local reps=$1 tile=$2
+  shift 2
+  : > "$OUT/warmsweep_$tile.jsonl"
+  for i in $(seq "$reps"); do
+    for w in "$@"; do
+      timeout -k 10 300 python bench.py --global "$tile" --steps 20 --warmup 5 --no-extras --clock-warmup-ms "$w" \
+        > "$OUT/warm_last.txt" 2>&1 || { echo "bench failed"; tail -20 "$OUT/warm_last.txt"; exit 1; }
+      python - "$OUT/warm_last.txt" "$w" >> "$OUT/warmsweep_$tile.jsonl" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+p = d["extras"].get("window_phases") or {}
+print(json.dumps({"warm_ms": float(sys.argv[2]), "window_ms": round(d["ms_per_step"] * d["steps"], 4),
+                  "value": d["value"], "span_us": p.get("gpu_span_us")}))
+PY
+    done
+  done
+  python - "$OUT/warmsweep_$tile.jsonl" <<'PY'
+import json, sys
+rs = [json.loads(l) for l in open(sys.argv[1])]
+for w in sorted({r["warm_ms"] for r in rs}):
+    v = sorted(r["window_ms"] for r in rs if r["warm_ms"] == w)
+    print(w, "n", len(v), "median", v[len(v) // 2], "min", v[0], "max", v[-1])
+PY
+}
+
 case "$TASK" in
   tests) task_tests "$@" ;;
   smoke) task_smoke ;;
@@ -186,5 +213,6 @@ case "$TASK" in
   py) task_py "$@" ;;
   final) task_final ;;
   warmab) task_warmab "$@" ;;
+  warmsweep) task_warmsweep "$@" ;;
   *) echo "unknown task '$TASK'"; exit 2 ;;
 esac
