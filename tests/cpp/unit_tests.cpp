@@ -1,8 +1,13 @@
 // Host-only unit tests of the C++ core ("Unit tests"): region
 // algebra, accessor indexing, Cartesian neighbour tables, halo-plan
-// aggregation/ordering. Run by ctest and by tests/test_cpp_unit.py.
+// aggregation/ordering, the collective decision statistics and the
+// interior-first chunk schedule. Run by ctest and by tests/test_cpp_unit.py
+// (and under host ASan/UBSan by scripts/cpu_sanitize.sh).
+#include <cmath>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <vector>
 #include <set>
 #include <sstream>
 #include <string>
@@ -11,6 +16,8 @@
 #include "mxs/grid/print.hpp"
 #include "mxs/grid/regions.hpp"
 #include "mxs/halo/plan.hpp"
+#include "mxs/kernels/chunk_schedule.hpp"
+#include "mxs/runtime/decision.hpp"
 #include "mxs/topo/cart.hpp"
 
 using namespace mxs;
@@ -131,11 +138,57 @@ static void test_plan() {
   EXPECT(reference_tag(D_TOP) == TOP && reference_tag(D_BOTTOM_RIGHT) == BOTTOM_RIGHT);
 }
 
+static void test_decision() {
+  // 20 rounds; the baseline drifts between rounds, the candidate stays 5% faster in each.
+  std::vector<double> base, fast, slow, missing;
+  for (int r = 0; r < 20; ++r) {
+    const double clock = 1.0 + 0.1 * ((r * 7) % 5);
+    base.push_back(0.30 * clock);
+    fast.push_back(0.285 * clock);
+    slow.push_back(0.33 * clock);
+    missing.push_back(r == 3 ? kMissingSample : 0.2 * clock);
+  }
+  RoundDecision d = decide_on_maxima(base, {slow, fast, missing}, 0.0);
+  EXPECT(d.best == 1 && d.win && std::fabs(d.ratio - 0.95) < 1e-9 && d.ratio_iqr < 1e-9);
+  EXPECT(d.ratios[2].empty() && d.ratios[0].size() == 20);  // a missing sample drops the candidate
+  EXPECT(!decide_on_maxima(base, {slow}, 0.0).win);
+  EXPECT(!decide_on_maxima(base, {fast}, 0.06).win);  // a 5% gain does not meet a 6% margin
+  // Element-wise max over ranks: one rank in a fast-serial state does not veto.
+  const std::vector<double> r0{0.30, 0.30}, r1{0.25, 0.28};
+  const std::vector<double> m = elementwise_max({r0, r1});
+  EXPECT(m.size() == 2 && m[0] == 0.30 && m[1] == 0.30);
+  std::vector<double> v{3, 1, 2, 4};
+  const auto mi = median_iqr(v);
+  EXPECT(mi.first == 3 && mi.second == 4 - 2);
+  EXPECT(std::fabs(median_notch(1.0, 0.1, 25) - 1.0316) < 1e-9);
+}
+
+static void test_halo_last_schedule() {
+  // 8 column groups x 600 rows, the edge groups reading the ghost columns, 256
+  // workgroups, depth 20: both sets cover every row once, inner chunks stay in the core.
+  const std::vector<std::uint8_t> ghost{1, 0, 0, 0, 0, 0, 0, 1};
+  const auto h = kernels::make_halo_last_schedule(8, 600, 256, 60, 20, ghost, 0, 0.12, 0, 8, 32);
+  EXPECT(kernels::check_halo_last_schedule(h, 8, 600, 20, ghost).empty());
+  EXPECT(h.outer.blocks % 8 == 0 && h.outer.blocks >= 32 && h.inner.blocks + h.outer.blocks == 256);
+  EXPECT(h.band >= 20);
+  // A fixed outer set.
+  const auto f = kernels::make_halo_last_schedule(8, 600, 256, 60, 20, ghost, 48);
+  EXPECT(f.outer.blocks == 48 && kernels::check_halo_last_schedule(f, 8, 600, 20, ghost).empty());
+  // Balanced starts: monotone, cover the whole range.
+  const auto st = kernels::balanced_starts(9, 8192, 256, 47);
+  EXPECT(st.size() == 257 && st.front() == 0 && st.back() == 9 * 8192);
+  bool mono = true;
+  for (size_t i = 1; i < st.size(); ++i) mono = mono && st[i] >= st[i - 1];
+  EXPECT(mono);
+}
+
 int main() {
   test_regions();
   test_layout();
   test_cart();
   test_plan();
+  test_decision();
+  test_halo_last_schedule();
   if (g_failures) {
     std::fprintf(stderr, "%d failure(s)\n", g_failures);
     return 1;
