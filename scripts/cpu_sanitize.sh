@@ -6,13 +6,13 @@
 # 9-rank golden CPU stencil, the CPU stencil configs (non-square grids,
 # checkpoint/resume, watchdog + fault injection), the CPU dot path and the 11
 # MPI tutorials (tests/test_apps_cpu.py + the native tests of
-# tests/test_core_plan.py). Log: profiles/r04_sanitize/cpu_sanitize.log (earlier rounds: profiles/r03_sanitize, r02_sanitize)
+# tests/test_core_plan.py). Log: profiles/r05_sanitize/cpu_sanitize.log (earlier rounds: profiles/r04_sanitize, r03_sanitize, r02_sanitize)
 #
 #   scripts/cpu_sanitize.sh            # needs no GPU
 set -o pipefail
 cd "$(dirname "$0")/.."
 B=build-asan
-out=${SAN_OUT:-profiles/r04_sanitize}
+out=${SAN_OUT:-profiles/r05_sanitize}
 mkdir -p "$out"
 log="$out/cpu_sanitize.log"
 {
