@@ -113,6 +113,25 @@ class StencilConfig:
     # hipGraph (long passes: eager measured faster). 0 = always graphs.
     graph_max_superstep_us: float = 150.0
 
+    # The string options and their allowed values (checked at construction, so a
+    # typo fails here on every rank instead of deep in the native solver).
+    _CHOICES = {"prefer": ("wide", "mpi"), "dtype": tuple(_DTYPES), "kind": ("jacobi5", "box"),
+                "backend": ("auto", "rccl", "ipc", "local", "torch"), "variant": ("auto", "roll", "lds"),
+                "init": ("random", "rank"), "direct_engine": ("kernel", "copy-engine"),
+                "opening": ("auto", "serial", "interior-first"), "steady": ("auto", "serial", "interior-first")}
+
+    def __post_init__(self):
+        for name, allowed in self._CHOICES.items():
+            if getattr(self, name) not in allowed:
+                raise ValueError(f"StencilConfig.{name} must be one of {', '.join(allowed)}; got {getattr(self, name)!r}")
+        if self.direct_halo not in (None, True, False, "on", "off", "validate"):
+            raise ValueError(f"StencilConfig.direct_halo must be None, a bool, 'on', 'off' or 'validate'; "
+                             f"got {self.direct_halo!r}")
+        if self.global_width <= 0 or self.global_height <= 0:
+            raise ValueError("StencilConfig: the global grid must be non-empty")
+        if not 0.0 <= self.min_gain < 1.0 or self.wire_delay_us < 0 or self.halo_max_ctas < 0:
+            raise ValueError("StencilConfig: min_gain in [0, 1), wire_delay_us >= 0, halo_max_ctas >= 0")
+
     @property
     def halo(self) -> int:
         if self.kind == "box":

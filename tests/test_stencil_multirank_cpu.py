@@ -77,3 +77,17 @@ def test_halo_property_nonsquare(rows, cols, w, h, halo, periodic):
     res = run_ranks("halo_property", rows * cols,
                     {"rows": rows, "cols": cols, "w": w, "h": h, "halo": halo, "periodic": periodic})
     assert all(r["bad"] == 0 for r in res), res
+
+
+@pytest.mark.parametrize("field,value", [("steady", "interior_first"), ("opening", "fast"), ("dtype", "f16"),
+                                         ("backend", "nvlink"), ("direct_engine", "dma"), ("direct_halo", "maybe"),
+                                         ("min_gain", 1.5), ("global_width", 0)])
+def test_stencil_config_rejects_bad_options(field, value):
+    """A mistyped option fails at StencilConfig construction, on every rank
+    alike, naming the field, instead of deep inside the native solver."""
+    from cuda_mpi_scratch_amd.models.stencil2d import StencilConfig
+
+    with pytest.raises(ValueError, match=field if field not in ("min_gain", "global_width") else "StencilConfig"):
+        StencilConfig(**{field: value})
+    StencilConfig(steady="interior-first", opening="serial", direct_halo="validate", direct_engine="copy-engine",
+                  prefer="mpi")
