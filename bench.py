@@ -117,7 +117,9 @@ def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync
     rank's (t1 - t0) still covers every rank's K steps."""
     st.run(warmup)
     st.prepare(steps)  # graphs + first launches of the timed shapes, outside the window
-    st.warm(steps, warm_s)  # untimed, state-preserving: sustained clocks for a short window
+    # Untimed, state-preserving: sustained clocks for a short window. Each warm
+    # pass is one run(steps)'s kernel shapes (cur -> nxt, the field unchanged).
+    st.untimed_warm_passes = st.warm(steps, warm_s)
     st.synchronize()
     _sync()
     ctx.barrier()
@@ -500,6 +502,10 @@ def main(argv=None) -> int:
                                    "c_neighbor = 0.2; range-guarded: 5|c| <= 1, max|u| 5^S < FLT_MAX/4)"
                                    if sum_used else "per step: fma(c_n, (n+s)+(w+e), c_c*c)"),
                     "clock_warmup_ms": args.clock_warmup_ms,
+                    # Before the window, besides the W warm-up steps: prepare() (its
+                    # decisions' samples) and this many untimed warm passes of the
+                    # window's shapes, each K steps of work on scratch (state unchanged).
+                    "untimed_warm_passes": int(getattr(st, "untimed_warm_passes", 0) or 0),
                     "window_sync": window_sync,
                     "tile": f"{st.decomp.width}x{st.decomp.height}",
                     "process_grid": f"{rows} rows x {cols} cols of ranks",

@@ -30,6 +30,8 @@ def test_bench_single_rank_cpu():
     ex = d["extras"]
     # The environment is on record (the launcher's RANK etc. are not runtime knobs).
     assert isinstance(ex["env"], dict) and all(k.startswith(bench.ENV_PREFIXES) for k in ex["env"])
+    # The untimed work before the window is on record (no native solver on CPU: no warm passes).
+    assert ex["clock_warmup_ms"] == 200.0 and ex["untimed_warm_passes"] == 0
 
 
 def test_bench_env_record_and_refusal(monkeypatch):

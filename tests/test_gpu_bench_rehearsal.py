@@ -51,6 +51,8 @@ def test_bench_8gpu_tile_window_through_loopback(gpu):
     assert ex["agreement"] == "none (one rank)" and "rehearsed_wire_delay_us" not in ex
     assert ph["gpu_span_us"] > 0 and ph["wall_us"] > 0
     assert isinstance(ex["env"], dict) and ex["experiments_build"] is False
+    # The untimed warm passes before the window are counted in the record (50 ms of ~0.25 ms passes).
+    assert ex["clock_warmup_ms"] == 50.0 and ex["untimed_warm_passes"] >= 20
     # 16384 x 8192 x 20 cell-updates: one pass (~0.25 ms) + one loopback exchange.
     assert d["value"] > 5000, d
 
