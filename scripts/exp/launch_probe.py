@@ -94,6 +94,27 @@ def main() -> int:
                 seq[kind][i].append((time.perf_counter() - t0) * 1e6)
     print(json.dumps({k: [round(statistics.median(v), 1) for v in vs] for k, vs in seq.items()}
                      | {"raw_" + k: [[round(x, 1) for x in v] for v in vs] for k, vs in seq.items()}), flush=True)
+    # C. The same after-warm sequence with events on the solver's own stream
+    # around each run(20): is the first window's extra time GPU time (the pass
+    # runs slower) or host time (launch / completion)?
+    ms = torch.cuda.ExternalStream(st.solver.main_stream())
+    walls, spans = [[], [], []], [[], [], []]
+    for r in range(max(4, rounds // 6)):
+        st.warm(20, 0.2)
+        st.synchronize()
+        torch.cuda.synchronize()
+        for i in range(3):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record(ms)
+            st.run(20)
+            e1.record(ms)
+            torch.cuda.synchronize()
+            walls[i].append((time.perf_counter() - t0) * 1e6)
+            spans[i].append(e0.elapsed_time(e1) * 1e3)
+    print(json.dumps({"after_warm_events": {"wall_us": [round(statistics.median(v), 1) for v in walls],
+                                            "span_us": [round(statistics.median(v), 1) for v in spans],
+                                            "raw_span_us": [[round(x, 1) for x in v] for v in spans]}}), flush=True)
     return 0
 
 
