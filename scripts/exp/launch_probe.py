@@ -112,6 +112,32 @@ def main() -> int:
             torch.cuda.synchronize()
             walls[i].append((time.perf_counter() - t0) * 1e6)
             spans[i].append(e0.elapsed_time(e1) * 1e3)
+    # D. What ends the post-burst transient? After warm(): nothing, an empty
+    # launch + sync, one more warm pass + sync (the second-window state), or a
+    # 1 ms sleep; then one event-bracketed window.
+    variants = {"none": lambda: None,
+                "empty": lambda: (H.spin_delay(0.0, s.cuda_stream), torch.cuda.synchronize()),
+                "one_pass": lambda: (st.warm(20, 1e-9), st.synchronize()),
+                "sleep1ms": lambda: time.sleep(0.001)}
+    dres = {k: ([], []) for k in variants}
+    for r in range(max(6, rounds // 5)):
+        for k, act in variants.items():
+            st.warm(20, 0.2)
+            st.synchronize()
+            torch.cuda.synchronize()
+            act()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0 = time.perf_counter()
+            e0.record(ms)
+            st.run(20)
+            e1.record(ms)
+            torch.cuda.synchronize()
+            dres[k][0].append((time.perf_counter() - t0) * 1e6)
+            dres[k][1].append(e0.elapsed_time(e1) * 1e3)
+    print(json.dumps({"after_warm_variants": {k: {"wall_us": round(statistics.median(w), 1),
+                                                  "span_us": round(statistics.median(sp), 1),
+                                                  "host_us": round(statistics.median([a - b for a, b in zip(w, sp)]), 1)}
+                                              for k, (w, sp) in dres.items()}}), flush=True)
     print(json.dumps({"after_warm_events": {"wall_us": [round(statistics.median(v), 1) for v in walls],
                                             "span_us": [round(statistics.median(v), 1) for v in spans],
                                             "raw_span_us": [[round(x, 1) for x in v] for v in spans]}}), flush=True)
