@@ -108,7 +108,7 @@ def _sync():
 
 
 def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync: str = "torch",
-              comm_timeout: float = 300.0) -> float:
+              comm_timeout: float = 300.0, warm_tail: int = 0) -> float:
     """K steps bracketed by barrier + device synchronisation on both sides; the
     max over ranks. Each rank's clock stops when its own device work is done,
     before the closing barrier: a 20-step window at N = 8 is one ~0.3 ms pass,
@@ -119,7 +119,7 @@ def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync
     st.prepare(steps)  # graphs + first launches of the timed shapes, outside the window
     # Untimed, state-preserving: sustained clocks for a short window. Each warm
     # pass is one run(steps)'s kernel shapes (cur -> nxt, the field unchanged).
-    st.untimed_warm_passes = st.warm(steps, warm_s)
+    st.untimed_warm_passes = st.warm(steps, warm_s, warm_tail)
     st.synchronize()
     _sync()
     ctx.barrier()
@@ -424,6 +424,9 @@ def main(argv=None) -> int:
     p.add_argument("--clock-warmup-ms", type=float, default=200.0,
                    help="untimed, state-preserving passes of the timed kernel shapes before the window, so a "
                         "short window runs at sustained clocks (0 = off)")
+    p.add_argument("--warm-tail", type=int, default=0,
+                   help="single untimed passes after the clock warm-up burst has drained (each drained too), "
+                        "so the window is the next of back-to-back windows, not the first after the burst")
     p.add_argument("--dot-n", type=int, default=2**30, help="global dot-product length (extras)")
     p.add_argument("--pingpong-max", type=int, default=256 << 20, help="largest ping-pong message (extras)")
     p.add_argument("--pingpong-ipc", action="store_true",
@@ -484,7 +487,8 @@ def main(argv=None) -> int:
     window_sync = args.window_sync
     if window_sync == "auto":
         window_sync = "torch" if st.comm is None else "solver"
-    dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3, window_sync, args.comm_timeout)
+    dt = timed_run(st, ctx, args.steps, args.warmup, args.clock_warmup_ms / 1e3, window_sync, args.comm_timeout,
+                   args.warm_tail)
     timed_blocks = st.last_run_blocks()  # the super-steps the timed window executed
     value = st.cells_per_step * args.steps / dt / 1e9
     halo = st.halo_mode()  # what the timed run() executed
@@ -502,6 +506,7 @@ def main(argv=None) -> int:
                                    "c_neighbor = 0.2; range-guarded: 5|c| <= 1, max|u| 5^S < FLT_MAX/4)"
                                    if sum_used else "per step: fma(c_n, (n+s)+(w+e), c_c*c)"),
                     "clock_warmup_ms": args.clock_warmup_ms,
+                    "warm_tail_passes": args.warm_tail,
                     # Before the window, besides the W warm-up steps: prepare() (its
                     # decisions' samples) and this many untimed warm passes of the
                     # window's shapes, each K steps of work on scratch (state unchanged).

@@ -288,12 +288,15 @@ class Stencil2D:
         if self.solver is not None and iters > 0:
             self.solver.prepare(iters)
 
-    def warm(self, iters: int, seconds: float) -> int:
+    def warm(self, iters: int, seconds: float, tail: int = 0) -> int:
         """Collective: about ``seconds`` of untimed, state-preserving passes of
         ``run(iters)``'s kernel shapes, so a short timed window that follows runs
         at the device's sustained clocks instead of paying the DVFS ramp (a cold
         20-step window at 32768^2 is ~20% slower than a warm one). The pass count
-        is agreed across ranks (max of the per-rank estimates). Returns it."""
+        is agreed across ranks (max of the per-rank estimates). ``tail``: that
+        many more single passes after the burst has drained, each drained too, so
+        the window that follows is the next of back-to-back windows rather than
+        the first after the burst. Returns the passes run."""
         if self.solver is None or iters <= 0 or seconds <= 0:
             return 0
         self.solver.synchronize()
@@ -302,7 +305,9 @@ class Stencil2D:
         one = max(time.perf_counter() - t0, 1e-5)
         passes = int(self.ctx.allreduce_max(min(1000.0, math.ceil(seconds / one))))
         self.solver.warm(iters, passes)
-        return passes + 1
+        for _ in range(max(0, tail)):
+            self.solver.warm(iters, 1)
+        return passes + 1 + max(0, tail)
 
     def _python_step(self):
         cfg, g = self.cfg, self.geom

@@ -96,6 +96,8 @@ task_window() {
       local args=(--global "$tile" --steps "${WINDOW_STEPS:-20}" --warmup 5 --no-extras)
       local base=$mode envs=()
       case $base in *-aw) envs+=(ROC_ACTIVE_WAIT_TIMEOUT=2000); base=${base%-aw} ;; esac
+      case $base in *-t1) args+=(--warm-tail 1); base=${base%-t1} ;; esac
+      case $base in *-t0) args+=(--warm-tail 0); base=${base%-t0} ;; esac
       case $base in *-p00) args+=(--stream-priorities=0,0); base=${base%-p00} ;; esac
       case $base in *-p11) args+=(--stream-priorities=-1,-1); base=${base%-p11} ;; esac
       case $base in *-tsync) args+=(--window-sync torch); base=${base%-tsync} ;; esac
