@@ -33,7 +33,9 @@ and one launch of every kernel shape the timed window uses, state unchanged)
 and ``--clock-warmup-ms`` (default 200) of further untimed, state-preserving
 launches of those shapes — a short window (K = 20 is one ~2 ms pass) otherwise
 runs partly below the sustained clocks while DVFS ramps up (cold 3.27 ms vs
-2.6 ms warm, profiles/r02_deep/clock_ramp.txt) — then K timed steps
+2.6 ms warm, profiles/r02_deep/clock_ramp.txt), then ``--warm-tail`` (default
+1) more single passes, each drained (the first window after the burst runs
+3-5% slower than the next one, profiles/r05_launch) — then K timed steps
 bracketed by barrier + device synchronisation on both sides: each rank's
 clock starts after the opening barrier and stops once its device work has
 completed, before the closing barrier; the time is the max over ranks. Every
@@ -108,7 +110,7 @@ def _sync():
 
 
 def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync: str = "torch",
-              comm_timeout: float = 300.0, warm_tail: int = 0) -> float:
+              comm_timeout: float = 300.0, warm_tail: int = 1) -> float:
     """K steps bracketed by barrier + device synchronisation on both sides; the
     max over ranks. Each rank's clock stops when its own device work is done,
     before the closing barrier: a 20-step window at N = 8 is one ~0.3 ms pass,
@@ -424,9 +426,10 @@ def main(argv=None) -> int:
     p.add_argument("--clock-warmup-ms", type=float, default=200.0,
                    help="untimed, state-preserving passes of the timed kernel shapes before the window, so a "
                         "short window runs at sustained clocks (0 = off)")
-    p.add_argument("--warm-tail", type=int, default=0,
+    p.add_argument("--warm-tail", type=int, default=1,
                    help="single untimed passes after the clock warm-up burst has drained (each drained too), "
-                        "so the window is the next of back-to-back windows, not the first after the burst")
+                        "so the window is the next of back-to-back windows, not the first after the burst "
+                        "(measured: the first window after the burst is 3-5%% slower, profiles/r05_launch)")
     p.add_argument("--dot-n", type=int, default=2**30, help="global dot-product length (extras)")
     p.add_argument("--pingpong-max", type=int, default=256 << 20, help="largest ping-pong message (extras)")
     p.add_argument("--pingpong-ipc", action="store_true",
