@@ -598,6 +598,16 @@ def main(argv=None) -> int:
                 stencil_rate(ctx, 32768, 32768, "f32", args.steps, args.warmup, args.clock_warmup_ms / 1e3,
                              time_block=args.time_block, sum_form=False), 2)
             torch.cuda.empty_cache()
+            # Unequal coefficients (c_center 0.5, c_neighbor 0.125) in the scaled
+            # form: the fast path for any 5-point Jacobi weights (c_neighbor != 0).
+            extras["stencil_32768sq_f32_unequal_coeffs_gcells_per_s"] = round(
+                stencil_rate(ctx, 32768, 32768, "f32", args.steps, args.warmup, args.clock_warmup_ms / 1e3,
+                             time_block=args.time_block, c_center=0.5, c_neighbor=0.125), 2)
+            from cuda_mpi_scratch_amd import hip as _hip
+
+            extras["stencil_unequal_coeffs"] = ("c_center 0.5, c_neighbor 0.125: scaled form (fma(k, u, n + s + w + e), "
+                                                "c_neighbor^S once per pass); kernel " + _hip().last_stencil_dispatch())
+            torch.cuda.empty_cache()
         if n == 1 and gpu and args.pingpong_loopback:
             pingpong_extras(ctx, extras, args.pingpong_max, loopback=True)
         elif n == 1 and gpu:

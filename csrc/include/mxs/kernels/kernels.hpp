@@ -46,10 +46,18 @@ struct Stencil5Coeffs {
   // run the sum form: each pass accumulates plain 5-point sums and scales by
   // c^S once when it stores (8 instead of 11 VALU issue slots per 4 fp32 cells
   // and step; stencil_device.hpp). Equal to the per-step evaluation up to
-  // rounding (a few ulp), not bit for bit. false = always the per-step form.
+  // rounding (a few ulp), not bit for bit. With center != neighbor (neighbor
+  // != 0) the pipeline passes run the scaled form instead: v' = (n + s + w + e)
+  // + (center / neighbor) v per level, neighbor^S once per pass (9 instead of 11
+  // slots). false = always the per-step form.
   bool sum_form = true;
 };
 inline bool uses_sum_form(const Stencil5Coeffs& c) { return c.sum_form && c.center == c.neighbor; }
+// The scaled form (stencil_device.hpp): unequal coefficients, c_neighbor != 0,
+// at the pipeline depths (fp32 20 / 24, fp64 16; other depths run per step).
+inline bool uses_scaled_form(const Stencil5Coeffs& c) {
+  return c.sum_form && c.center != c.neighbor && c.neighbor != 0.0;
+}
 
 enum class StencilVariant : int {
   Auto = 0,        // tuned default
@@ -143,6 +151,7 @@ void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, 
 struct ChunkPassShape {
   int steps = 0;
   bool sum = false;   // sum form (c_center == c_neighbor and allowed)
+  bool scaled = false;  // scaled form (c_center != c_neighbor, c_neighbor != 0, allowed)
   int js0 = 0;        // stage-0 levels of the joint windows
   int lag1 = 0;       // level-order mask (stencil_pipe.hpp)
   int blocks = 0;     // resident workgroups (one per CU)

@@ -324,7 +324,11 @@ class StencilSolver {
   }
   // Whether the passes currently take the sum form (coefficients, user choice
   // and the measured range all allow it).
-  bool sum_form_active() const { return cfg_.coeffs.sum_form && kernels::uses_sum_form(cfg_.coeffs); }
+  // A fast form is on: the sum form (equal coefficients) or the scaled form.
+  bool sum_form_active() const {
+    return cfg_.coeffs.sum_form && (kernels::uses_sum_form(cfg_.coeffs) || kernels::uses_scaled_form(cfg_.coeffs));
+  }
+  bool scaled_form_active() const { return cfg_.coeffs.sum_form && kernels::uses_scaled_form(cfg_.coeffs); }
   // Why the sum form is off when the coefficients are equal ("" when on).
   const std::string& sum_form_note() const { return sum_note_; }
   // (S, count) of the super-steps the last run() enqueued.
@@ -472,7 +476,8 @@ class StencilSolver {
   bool range_agreed_ = false;               // the ranks agreed on a range at least once
   double local_absmax_ = 0;
   bool user_sum_ = true;                     // the caller allows the sum form
-  bool sum_coeffs_ok_ = false;               // 5|c| <= 1 and c^S normal
+  bool sum_coeffs_ok_ = false;               // |c0| + 4|c1| <= 1 and c1^S normal
+  double fast_growth_ = 5.0;                 // per-level growth bound of the fast forms: 4 + |c0 / c1|
   std::string sum_note_;
   DeviceBuffer<T> absmax_;
   DeviceBuffer<double> agree_buf_;

@@ -37,6 +37,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <limits>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -237,7 +238,9 @@ void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
 // boundary strips are only S rows or S columns thin; a bulk tile or a 256-column
 // wave strip would recompute 8-32x the strip, so thin strips get a matching thin
 // LDS tile (32 x 128 for column strips, 128 x 16 for row strips).
-template <typename T, int S, bool WRAP, bool SUM>
+// XB = kScaledBody (with SUM): the scaled form, on the fp64 wide pipeline at
+// S = 16 only; the thin-strip tiles and the stream kernels then run per step.
+template <typename T, int S, bool WRAP, bool SUM, int XB = 0>
 void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
                T sc, StencilVariant v, hipStream_t s) {
   constexpr int TW = sizeof(T) == 4 ? 128 : 64;
@@ -251,33 +254,42 @@ void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, i
     if (v == StencilVariant::LdsTile)
       return launch_tb_tile<T, S, TW, 32, WRAP>(in, out, g, x0, x1, y0, y1, c0, c1, s);
   }
-  if constexpr (sizeof(T) == 8 && S >= kPipeMinF64) {
+  if constexpr (sizeof(T) == 8 && S >= kPipeMinF64 && (XB == 0 || S == 16)) {
     if (wide_pipe_ok<T, S, WRAP>(g, x0, x1, y0, y1))
-      return launch_pipe<T, S, WRAP, SUM>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+      return launch_pipe<T, S, WRAP, SUM, XB>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
   }
-  launch_stream<T, S, WRAP, SUM && sizeof(T) == 4>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+  launch_stream<T, S, WRAP, SUM && XB == 0 && sizeof(T) == 4>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
 }
 
-// sum: c_center == c_neighbor and the caller allows the sum form (the fast
-// bodies then take sc = c^S); S = 1 always keeps the per-step form.
+// form: 1 = sum form (c_center == c_neighbor, allowed by the caller: the fast
+// bodies take sc = c^S), 2 = scaled form (c_center != c_neighbor: sc = c1^S and
+// k = c0 / c1, at the pipeline depths fp32 20 / 24 and fp64 16; elsewhere per
+// step), 0 = per step. S = 1 always keeps the per-step form.
 template <typename T, bool WRAP, int S = 1>
-void dispatch_tb(int steps, bool sum, const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0,
+void dispatch_tb(int steps, int form, const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0,
                  index_t y1, T c0, T c1, StencilVariant v, hipStream_t s) {
   const T sc = T(std::pow(double(c1), double(S)));
   if constexpr (S <= kMaxTimeBlock) {
     if (steps == S) {
       if constexpr (S > 1) {
-        if (sum) return launch_tb<T, S, WRAP, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s);
+        if (form == 1) return launch_tb<T, S, WRAP, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s);
+      }
+      if constexpr (sizeof(T) == 8 && S == 16) {
+        if (form == 2)
+          return launch_tb<T, S, WRAP, true, kScaledBody>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s);
       }
       return launch_tb<T, S, WRAP, false>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s);
     }
-    return dispatch_tb<T, WRAP, S + 1>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+    return dispatch_tb<T, WRAP, S + 1>(steps, form, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   } else if constexpr (S <= kMaxTimeBlockDeep && sizeof(T) == 4) {
     if (steps == S) {
-      if (sum) return launch_pipe<T, S, WRAP, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+      if (form == 1) return launch_pipe<T, S, WRAP, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+      if constexpr (S == 20 || S == 24) {
+        if (form == 2) return launch_pipe<T, S, WRAP, true, kScaledBody>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+      }
       return launch_pipe<T, S, WRAP, false>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
     }
-    return dispatch_tb<T, WRAP, S + 1>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+    return dispatch_tb<T, WRAP, S + 1>(steps, form, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   } else {
     MXS_CHECK(false, "stencil5_tb: steps must be in [1, " << (sizeof(T) == 4 ? kMaxTimeBlockDeep : kMaxTimeBlock)
                                                           << "], got " << steps);
@@ -307,9 +319,14 @@ void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, 
               "stencil5_tb: row padding too small for the x apron");
   }
   const T c0 = T(c.center), c1 = T(c.neighbor);
-  const bool sum = uses_sum_form(c) && v != StencilVariant::LdsTile;
-  if (wrap) dispatch_tb<T, true>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
-  else dispatch_tb<T, false>(steps, sum, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+  // The scaled form needs c1^S in the normal range of T (it scales the stored result).
+  const bool scale_ok = std::fabs(double(T(std::pow(double(c1), double(steps))))) >= double(std::numeric_limits<T>::min());
+  const int form = v == StencilVariant::LdsTile ? 0
+                   : uses_sum_form(c)                ? 1
+                   : uses_scaled_form(c) && scale_ok ? 2
+                                                     : 0;
+  if (wrap) dispatch_tb<T, true>(steps, form, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
+  else dispatch_tb<T, false>(steps, form, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   MXS_HIP_CHECK_LAUNCH();
 }
 

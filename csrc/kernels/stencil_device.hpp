@@ -695,10 +695,71 @@ struct BodySumF64 : BodyWideF64 {
   }
 };
 
-// XB: alternative bodies of the tuner (bench/tune_kernels.hpp specialises
-// FastBody<T, SUM, 1>); the library instantiates only XB = 0.
+// Scaled form (any c_center, c_neighbor != 0; the pipeline passes of the
+// production depths): u' = c1 (N + S + W + E + k u) with k = c0 / c1, so a pass
+// carries v_l = u_l / c1^l, v' = (N + S + W + E) + k v — one packed FMA per
+// cell pair in place of the per-step form's multiply and FMA — and applies c1^S
+// once when it stores (the kernels' c0 argument holds c1^S, their c1 argument
+// k). Rotated fp32: 9 VALU issue slots per 4 cells and level instead of 11;
+// wide fp64: 16 fp64 ops + 4 moves instead of 20 + 4. The sum form is the
+// k = 1 case with the centre folded into the horizontal pair sums (8 slots).
+// Equal to the per-step evaluation up to rounding; magnitudes grow as
+// (4 + |k|)^S inside a pass (the solver's range guard).
+__device__ __forceinline__ f32x4 scaled_rot4f(const f32x4& up, const f32x4& mid, const f32x4& dn, float k) {
+  const f32x2 am = mid.xy, bm = mid.zw;  // (c1, c2), (c3, c0)
+  const f32x2 ns_a = up.xy + dn.xy, ns_b = up.zw + dn.zw;
+  const f32x2 we = am + bm;                 // (c1 + c3, c2 + c0): the in-lane neighbour pairs, swapped
+  const f32x2 t_a = pk_add_swap(ns_a, we);  // (ns(c1) + c0 + c2, ns(c2) + c1 + c3)
+  f32x2 we_b;                               // c3: c2 + c0[lane + 1], c0: c1 + c3[lane - 1]
+  we_b.x = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bm.y), kDppWaveShl1, 0xf, 0xf, true)) + am.y;
+  we_b.y = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(bm.x), kDppWaveShr1, 0xf, 0xf, true)) + am.x;
+  const f32x2 kv = f32x2(k);
+  f32x4 o;
+  o.xy = __builtin_elementwise_fma(kv, am, t_a);
+  o.zw = __builtin_elementwise_fma(kv, bm, ns_b + we_b);
+  return o;
+}
+__device__ __forceinline__ f64x4 scaled_w4d(const f64x4& up, const f64x4& mid, const f64x4& dn, double k) {
+  const double left = lane_shift<double, kDppWaveShr1>(mid.w);
+  const double right = lane_shift<double, kDppWaveShl1>(mid.x);
+  f64x4 o;
+  o.x = __builtin_fma(k, mid.x, (up.x + dn.x) + (left + mid.y));
+  o.y = __builtin_fma(k, mid.y, (up.y + dn.y) + (mid.x + mid.z));
+  o.z = __builtin_fma(k, mid.z, (up.z + dn.z) + (mid.y + mid.w));
+  o.w = __builtin_fma(k, mid.w, (up.w + dn.w) + (mid.z + right));
+  return o;
+}
+struct BodyScaledF32 : BodyRotF32 {
+  static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, float, float k) {
+    return scaled_rot4f(u, m, d, k);
+  }
+  static __device__ __forceinline__ void store(const V& top, __amdgpu_buffer_rsrc_t r, unsigned off, float scale) {
+    BodyRotF32::store(top * scale, r, off, scale);
+  }
+};
+struct BodyScaledF64 : BodyWideF64 {
+  static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, double, double k) {
+    return scaled_w4d(u, m, d, k);
+  }
+  static __device__ __forceinline__ void store(const V& top, __amdgpu_buffer_rsrc_t r, unsigned off, double scale) {
+    BodyWideF64::store(top * scale, r, off, scale);
+  }
+};
+
+// XB: alternative bodies. The tuner specialises FastBody<T, SUM, 1>
+// (bench/tune_kernels.hpp); the library uses XB = 0 and, with SUM, the scaled
+// form as XB = kScaledBody.
+constexpr int kScaledBody = 2;
 template <typename T, bool SUM = false, int XB = 0>
 struct FastBody;
+template <>
+struct FastBody<float, true, kScaledBody> {
+  using type = BodyScaledF32;
+};
+template <>
+struct FastBody<double, true, kScaledBody> {
+  using type = BodyScaledF64;
+};
 template <>
 struct FastBody<float, false, 0> {
   using type = BodyRotF32;
@@ -1458,13 +1519,13 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
 // it 32 of the 512 VGPRs in the sum forms (fp32 12 + 8 / 12 + 12: 238, 8 + 12:
 // 225, 8-VGPR granules); the per-step 8 + 12 and fp64 8 + 8 forms (244) leave
 // 16, and their copies take the CUs the inner launch leaves free.
-template <int S0, int S1, int PF, typename T, bool SUM, int LAG1>
+template <int S0, int S1, int PF, typename T, bool SUM, int LAG1, int XB = 0>
 __global__ __launch_bounds__(2 * kWavesPerBlock * kWaveSize) void stencil5_pipe_chunks_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, const PassChunk* __restrict__ table, int entries, T c0, T c1) {
   constexpr int G = kWavesPerBlock;
   using P = PipeShape<S0, S1, PF>;
-  using B = typename FastBody<T, SUM>::type;
+  using B = typename FastBody<T, SUM, XB>::type;
   constexpr int OWG = JointShape<S0, S1, G>::OWG;
   __shared__ typename B::V ring[G * P::RING * kWaveSize];
   const int wave = threadIdx.x / kWaveSize;

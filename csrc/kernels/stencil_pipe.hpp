@@ -80,11 +80,12 @@ constexpr index_t kLag1MaxChunkF64 = 384;
 constexpr index_t kJointWide = 12288;
 
 // JS0: 0 = per-strip layout (pipe_s0 split), else joint windows with S0 = JS0.
-template <typename T, int S, bool WRAP, bool SUM, int JS0 = 0, int LAG1 = 0>
+// XB = kScaledBody (with SUM): the scaled form's body (stencil_device.hpp).
+template <typename T, int S, bool WRAP, bool SUM, int JS0 = 0, int LAG1 = 0, int XB = 0>
 constexpr auto pipe_kernel() {
   if constexpr (JS0 > 0)
     return stencil5_stream_pipe_kernel<JS0, S - JS0, pipe_pf<T, S>(), WRAP, 0, T, SUM, kWavesPerBlock, false, true,
-                                       LAG1>;
+                                       LAG1, XB>;
   else
     return stencil5_stream_pipe_kernel<pipe_s0<T, S, SUM>(), S - pipe_s0<T, S, SUM>(), pipe_pf<T, S>(), WRAP, 0, T,
                                        SUM>;
@@ -131,9 +132,10 @@ void pipe_starts(index_t groups, index_t rows, int blocks, index_t fill, PipeSha
 // MXS_PIPE_BALANCED=0: equal row shares (the round-2 rule), for comparison.
 bool pipe_balanced();
 
-template <typename T, int S, bool WRAP, bool SUM, int JS0, int LAG1 = 0>
+template <typename T, int S, bool WRAP, bool SUM, int JS0, int LAG1 = 0, int XB = 0>
 void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0,
                       T c1, T sc, hipStream_t s) {
+  static_assert(XB == 0 || (SUM && XB == kScaledBody && JS0 > 0), "the scaled form runs the joint pipeline");
   const index_t share = pipe_share<T, S, WRAP, SUM, JS0>(x0, x1, y0, y1);
   const int blocks = pipe_blocks<T, S, WRAP, SUM, JS0>();
   PipeShares shares = PipeShares::equal(share);
@@ -149,13 +151,15 @@ void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_
   }
   MXS_CHECK(chunk * g.pitch * index_t(sizeof(T)) <= kMaxChunkBytes,
             "stencil5_tb: a pipeline chunk must stay within kMaxChunkBytes (buffer-descriptor stores)");
-  pipe_kernel<T, S, WRAP, SUM, JS0, LAG1>()<<<blocks, 2 * kBlock, 0, s>>>(
-      in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, shares, SUM ? sc : c0, c1);
-  note_dispatch(SUM ? "stream_pipe_sum" : "stream_pipe");
+  // Sum form: (c^S, c); scaled form: (c1^S, c0 / c1); per step: (c0, c1).
+  const T kc = XB == kScaledBody ? T(double(c0) / double(c1)) : c1;
+  pipe_kernel<T, S, WRAP, SUM, JS0, LAG1, XB>()<<<blocks, 2 * kBlock, 0, s>>>(
+      in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, shares, SUM ? sc : c0, kc);
+  note_dispatch(XB == kScaledBody ? "stream_pipe_scaled" : SUM ? "stream_pipe_sum" : "stream_pipe");
   note_pipe_lag1(LAG1 != 0);
 }
 
-template <typename T, int S, bool WRAP, bool SUM>
+template <typename T, int S, bool WRAP, bool SUM, int XB = 0>
 void launch_pipe_impl(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
                  T sc, hipStream_t s) {
   if constexpr (pipe_joint_ok<T, S>()) {
@@ -163,19 +167,24 @@ void launch_pipe_impl(const T* in, T* out, const TileGeom& g, index_t x0, index_
       if constexpr (sizeof(T) == 4 && S == 20) {
         if (pipe_lag1() && pipe_share<T, S, WRAP, SUM, 12>(x0, x1, y0, y1) <= kLag1MaxChunk) {
           if (x1 - x0 < kJointWide)
-            return launch_pipe_form<T, S, WRAP, SUM, 8, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
-          return launch_pipe_form<T, S, WRAP, SUM, 12, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+            return launch_pipe_form<T, S, WRAP, SUM, 8, kLagBoth, XB>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+          return launch_pipe_form<T, S, WRAP, SUM, 12, kLagBoth, XB>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
         }
       } else if constexpr (sizeof(T) == 4 && S == 24) {
-        if (pipe_lag1()) return launch_pipe_form<T, S, WRAP, SUM, 12, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+        if (pipe_lag1())
+          return launch_pipe_form<T, S, WRAP, SUM, 12, kLagBoth, XB>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
       } else if constexpr (sizeof(T) == 8 && S == 16) {
         if (pipe_lag1() && pipe_share<T, S, WRAP, SUM, 8>(x0, x1, y0, y1) <= kLag1MaxChunkF64)
-          return launch_pipe_form<T, S, WRAP, SUM, 8, kLagBoth>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+          return launch_pipe_form<T, S, WRAP, SUM, 8, kLagBoth, XB>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
       }
-      return launch_pipe_form<T, S, WRAP, SUM, joint_s0<T, S>()>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+      return launch_pipe_form<T, S, WRAP, SUM, joint_s0<T, S>(), 0, XB>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
     }
   }
-  launch_pipe_form<T, S, WRAP, SUM, 0>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+  if constexpr (XB == 0) {
+    launch_pipe_form<T, S, WRAP, SUM, 0>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+  } else {
+    MXS_CHECK(false, "stencil5_tb: the scaled form needs the joint pipeline windows (MXS_PIPE_JOINT=0 set?)");
+  }
 }
 
 // Whether the fp64 wide-lane pipeline can take [x0, x1) x [y0, y1) at depth S:
@@ -193,8 +202,9 @@ bool wide_pipe_ok_impl(const TileGeom& g, index_t x0, index_t x1, index_t y0, in
 }
 
 
-// Explicitly instantiated in the pipeline TUs.
-template <typename T, int S, bool WRAP, bool SUM>
+// Explicitly instantiated in the pipeline TUs (XB = kScaledBody: the scaled
+// form, instantiated at the solver's depths only: fp32 20 / 24, fp64 16).
+template <typename T, int S, bool WRAP, bool SUM, int XB = 0>
 void launch_pipe(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
                  T sc, hipStream_t s);
 template <typename T, int S, bool WRAP>

@@ -7,6 +7,7 @@
 // and S = 24 (12 + 12), fp64 S = 16 (8 + 8), each in the sum and the per-step
 // form. Other depths keep the one-launch pass.
 #include <cmath>
+#include <limits>
 
 #include "stencil_pipe.hpp"
 
@@ -15,9 +16,9 @@ namespace kernels {
 namespace detail {
 namespace {
 
-template <typename T, int S, bool SUM, int JS0, int LAG1>
+template <typename T, int S, bool SUM, int JS0, int LAG1, int XB = 0>
 constexpr auto chunks_kernel() {
-  return stencil5_pipe_chunks_kernel<JS0, S - JS0, pipe_pf<T, S>(), T, SUM, LAG1>;
+  return stencil5_pipe_chunks_kernel<JS0, S - JS0, pipe_pf<T, S>(), T, SUM, LAG1, XB>;
 }
 
 template <typename T, int S, bool SUM, int JS0, int LAG1>
@@ -70,29 +71,29 @@ bool shape_for(const TileGeom& g, ChunkPassShape* out) {
   return false;
 }
 
-template <typename T, int S, bool SUM, int JS0, int LAG1>
+template <typename T, int S, bool SUM, int JS0, int LAG1, int XB>
 void launch_chunks(const T* in, T* out, const TileGeom& g, T c0, T c1, const ChunkPassShape& sh,
                    const PassChunk* table, int entries, hipStream_t s) {
-  chunks_kernel<T, S, SUM, JS0, LAG1>()<<<sh.blocks, 2 * kBlock, 0, s>>>(
+  chunks_kernel<T, S, SUM, JS0, LAG1, XB>()<<<sh.blocks, 2 * kBlock, 0, s>>>(
       in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, table, entries, c0, c1);
-  note_dispatch(SUM ? "stream_pipe_sum_chunks" : "stream_pipe_chunks");
+  note_dispatch(XB == kScaledBody ? "stream_pipe_scaled_chunks" : SUM ? "stream_pipe_sum_chunks" : "stream_pipe_chunks");
   note_pipe_lag1(LAG1 != 0);
 }
 
-template <typename T, int S, bool SUM>
+template <typename T, int S, bool SUM, int XB = 0>
 void launch_for(const T* in, T* out, const TileGeom& g, T c0, T c1, const ChunkPassShape& sh, const PassChunk* table,
                 int entries, hipStream_t s) {
   const bool lag = sh.lag1 != 0;
   if constexpr (sizeof(T) == 4 && S == 20) {
-    if (sh.js0 == 8 && lag) return launch_chunks<T, S, SUM, 8, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s);
-    if (sh.js0 == 12 && lag) return launch_chunks<T, S, SUM, 12, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s);
-    if (sh.js0 == 12) return launch_chunks<T, S, SUM, 12, 0>(in, out, g, c0, c1, sh, table, entries, s);
+    if (sh.js0 == 8 && lag) return launch_chunks<T, S, SUM, 8, kLagBoth, XB>(in, out, g, c0, c1, sh, table, entries, s);
+    if (sh.js0 == 12 && lag) return launch_chunks<T, S, SUM, 12, kLagBoth, XB>(in, out, g, c0, c1, sh, table, entries, s);
+    if (sh.js0 == 12) return launch_chunks<T, S, SUM, 12, 0, XB>(in, out, g, c0, c1, sh, table, entries, s);
   } else if constexpr (sizeof(T) == 4 && S == 24) {
-    if (sh.js0 == 12 && lag) return launch_chunks<T, S, SUM, 12, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s);
-    if (sh.js0 == 12) return launch_chunks<T, S, SUM, 12, 0>(in, out, g, c0, c1, sh, table, entries, s);
+    if (sh.js0 == 12 && lag) return launch_chunks<T, S, SUM, 12, kLagBoth, XB>(in, out, g, c0, c1, sh, table, entries, s);
+    if (sh.js0 == 12) return launch_chunks<T, S, SUM, 12, 0, XB>(in, out, g, c0, c1, sh, table, entries, s);
   } else if constexpr (sizeof(T) == 8 && S == 16) {
-    if (sh.js0 == 8 && lag) return launch_chunks<T, S, SUM, 8, kLagBoth>(in, out, g, c0, c1, sh, table, entries, s);
-    if (sh.js0 == 8) return launch_chunks<T, S, SUM, 8, 0>(in, out, g, c0, c1, sh, table, entries, s);
+    if (sh.js0 == 8 && lag) return launch_chunks<T, S, SUM, 8, kLagBoth, XB>(in, out, g, c0, c1, sh, table, entries, s);
+    if (sh.js0 == 8) return launch_chunks<T, S, SUM, 8, 0, XB>(in, out, g, c0, c1, sh, table, entries, s);
   }
   MXS_CHECK(false, "stencil5_chunk_pass: no kernel for S = " << S << ", js0 = " << sh.js0 << ", lag1 = " << sh.lag1);
 }
@@ -109,7 +110,10 @@ bool chunk_pass_shape(const TileGeom& g, int steps, const Stencil5Coeffs& c, Chu
   if ((g.pitch % N) != 0 || ((g.x_origin + g.halo_x) % N) != 0) return false;
   const index_t sa = (steps + 3) / 4 * 4;  // the joint read reach A0 + A1
   if (g.x_origin + g.halo_x < sa || g.pitch < g.x_origin + g.halo_x + (g.width + 3) / 4 * 4 + sa) return false;
-  const bool sum = uses_sum_form(c);
+  // The scaled form scales the stored result by c_neighbor^S: it must be a normal number.
+  const bool scaled = uses_scaled_form(c) &&
+                      std::fabs(double(T(std::pow(c.neighbor, double(steps))))) >= double(std::numeric_limits<T>::min());
+  const bool sum = uses_sum_form(c) || scaled;  // both fast forms share the sum-form shape
   ChunkPassShape sh;
   bool ok = false;
   if constexpr (sizeof(T) == 4) {
@@ -118,6 +122,7 @@ bool chunk_pass_shape(const TileGeom& g, int steps, const Stencil5Coeffs& c, Chu
   } else {
     if (steps == 16) ok = sum ? shape_for<T, 16, true>(g, &sh) : shape_for<T, 16, false>(g, &sh);
   }
+  sh.scaled = scaled;
   if (ok && out) *out = sh;
   return ok;
 }
@@ -127,24 +132,31 @@ void stencil5_chunk_pass(const T* in, T* out, const TileGeom& g, const Stencil5C
                          const PassChunk* table, int entries, hipStream_t s) {
   using namespace detail;
   MXS_CHECK(table != nullptr && entries > 0 && sh.blocks > 0, "stencil5_chunk_pass: no schedule");
-  MXS_CHECK(sh.sum == uses_sum_form(c), "stencil5_chunk_pass: shape built for the other evaluation form");
+  ChunkPassShape now;
+  MXS_CHECK(chunk_pass_shape<T>(g, sh.steps, c, &now) && now.sum == sh.sum && now.scaled == sh.scaled,
+            "stencil5_chunk_pass: shape built for the other evaluation form");
   const T c0 = T(c.center), c1 = T(c.neighbor);
   const T sc = T(std::pow(double(c1), double(sh.steps)));
+  // Kernel coefficients: sum form (c^S, c), scaled form (c1^S, c0 / c1), per step (c0, c1).
   const T k0 = sh.sum ? sc : c0;
+  const T k1 = sh.scaled ? T(double(c.center) / double(c.neighbor)) : c1;
   if constexpr (sizeof(T) == 4) {
     if (sh.steps == 20) {
-      if (sh.sum) launch_for<T, 20, true>(in, out, g, k0, c1, sh, table, entries, s);
-      else launch_for<T, 20, false>(in, out, g, k0, c1, sh, table, entries, s);
+      if (sh.scaled) launch_for<T, 20, true, kScaledBody>(in, out, g, k0, k1, sh, table, entries, s);
+      else if (sh.sum) launch_for<T, 20, true>(in, out, g, k0, k1, sh, table, entries, s);
+      else launch_for<T, 20, false>(in, out, g, k0, k1, sh, table, entries, s);
     } else if (sh.steps == 24) {
-      if (sh.sum) launch_for<T, 24, true>(in, out, g, k0, c1, sh, table, entries, s);
-      else launch_for<T, 24, false>(in, out, g, k0, c1, sh, table, entries, s);
+      if (sh.scaled) launch_for<T, 24, true, kScaledBody>(in, out, g, k0, k1, sh, table, entries, s);
+      else if (sh.sum) launch_for<T, 24, true>(in, out, g, k0, k1, sh, table, entries, s);
+      else launch_for<T, 24, false>(in, out, g, k0, k1, sh, table, entries, s);
     } else {
       MXS_CHECK(false, "stencil5_chunk_pass: fp32 depth " << sh.steps);
     }
   } else {
     MXS_CHECK(sh.steps == 16, "stencil5_chunk_pass: fp64 depth " << sh.steps);
-    if (sh.sum) launch_for<T, 16, true>(in, out, g, k0, c1, sh, table, entries, s);
-    else launch_for<T, 16, false>(in, out, g, k0, c1, sh, table, entries, s);
+    if (sh.scaled) launch_for<T, 16, true, kScaledBody>(in, out, g, k0, k1, sh, table, entries, s);
+    else if (sh.sum) launch_for<T, 16, true>(in, out, g, k0, k1, sh, table, entries, s);
+    else launch_for<T, 16, false>(in, out, g, k0, k1, sh, table, entries, s);
   }
   MXS_HIP_CHECK_LAUNCH();
 }

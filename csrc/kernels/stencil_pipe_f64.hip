@@ -6,10 +6,10 @@ namespace mxs {
 namespace kernels {
 namespace detail {
 
-template <typename T, int S, bool WRAP, bool SUM>
+template <typename T, int S, bool WRAP, bool SUM, int XB>
 void launch_pipe(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
                  T sc, hipStream_t s) {
-  launch_pipe_impl<T, S, WRAP, SUM>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+  launch_pipe_impl<T, S, WRAP, SUM, XB>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
 }
 
 template <typename T, int S, bool WRAP>
@@ -39,6 +39,13 @@ MXS_INST_PIPE(16)
 
 #undef MXS_INST_PIPE
 #undef MXS_INST_LAUNCH
+
+// The scaled form (any c_center, c_neighbor != 0) at the solver's depths.
+template void launch_pipe<double, 16, true, true, kScaledBody>(const double*, double*, const TileGeom&, index_t, index_t,
+                                                           index_t, index_t, double, double, double, hipStream_t);
+template void launch_pipe<double, 16, false, true, kScaledBody>(const double*, double*, const TileGeom&, index_t, index_t,
+                                                           index_t, index_t, double, double, double, hipStream_t);
+
 
 }  // namespace detail
 }  // namespace kernels

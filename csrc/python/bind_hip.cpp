@@ -590,6 +590,8 @@ PYBIND11_MODULE(_mxs_hip, m) {
           "collective, state-preserving: one event-timed replica of run(iters)'s opening super-step "
           "(phases: (stream:phase, start us, end us))")
       .def("sum_form_active", [](SolverHandle& h) { return h.visit([](auto& s) { return s.sum_form_active(); }); })
+      .def("scaled_form_active",
+           [](SolverHandle& h) { return h.visit([](auto& s) { return s.scaled_form_active(); }); })
       .def("sum_form_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.sum_form_note(); }); })
       .def("last_run_blocks", [](SolverHandle& h) { return h.visit([](auto& s) { return s.last_run_blocks(); }); },
            "(S, count) super-steps the last run() enqueued")

@@ -159,15 +159,21 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
     opening_choice_ = "serial";
     opening_reason_ = "forced (opening = serial)";
   }
-  // Sum-form guard, coefficient part (the range part runs before the first pass).
+  // Fast-form guard, coefficient part (the range part runs before the first
+  // pass): the sum form (c_center == c_neighbor) or the scaled form (unequal,
+  // c_neighbor != 0). Both carry v_l = u_l / c_neighbor^l through a pass, which
+  // grows by at most (4 + |c_center / c_neighbor|) per level, and need the
+  // operator bounded by the field (|c_center| + 4 |c_neighbor| <= 1) and
+  // c_neighbor^S in the normal range (it scales the stored result).
   user_sum_ = cfg_.coeffs.sum_form;
-  if (user_sum_ && cfg_.coeffs.center == cfg_.coeffs.neighbor && cfg_.kind == StencilKind::Jacobi5) {
-    const double c = std::fabs(cfg_.coeffs.neighbor);
-    const T cs = T(std::pow(c, double(block_)));
-    if (!(5.0 * c <= 1.0 + 1e-6)) {
-      sum_note_ = "sum form off: 5 |c| > 1 (the S-level sums would not be bounded by the field)";
+  const double cc = cfg_.coeffs.center, cn = cfg_.coeffs.neighbor;
+  if (user_sum_ && cfg_.kind == StencilKind::Jacobi5 && cn != 0.0) {
+    const T cs = T(std::pow(std::fabs(cn), double(block_)));
+    fast_growth_ = 4.0 + std::fabs(cc / cn);
+    if (!(std::fabs(cc) + 4.0 * std::fabs(cn) <= 1.0 + 1e-6)) {
+      sum_note_ = "fast form off: |c_center| + 4 |c_neighbor| > 1 (the S-level sums would not be bounded by the field)";
     } else if (!(cs >= std::numeric_limits<T>::min())) {
-      sum_note_ = "sum form off: c^S is below the normal range of the element type";
+      sum_note_ = "fast form off: c_neighbor^S is below the normal range of the element type";
     } else {
       sum_coeffs_ok_ = true;
     }
@@ -486,11 +492,11 @@ void StencilSolver<T>::ensure_range(bool collective) {
     range_agreed_ = true;
     agreed = true;
   }
-  const double bound = double(std::numeric_limits<T>::max()) / 4.0 / std::pow(5.0, double(block_));
+  const double bound = double(std::numeric_limits<T>::max()) / 4.0 / std::pow(fast_growth_, double(block_));
   const bool ok = std::isfinite(md) && md < bound && (agreed || cfg_.coeffs.sum_form);
   if (ok == cfg_.coeffs.sum_form) return;
   cfg_.coeffs.sum_form = ok;
-  sum_note_ = ok ? "" : "sum form off: max|u| * 5^S would overflow the element type (per-step form)";
+  sum_note_ = ok ? "" : "fast form off: max|u| * (4 + |c_center / c_neighbor|)^S would overflow the element type (per-step form)";
   // Captured graphs and chunk-pass shapes were built for the other form.
   wait_idle("sum-form switch");
   graphs_.clear();

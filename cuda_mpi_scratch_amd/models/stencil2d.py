@@ -156,7 +156,9 @@ class Stencil2D:
         # exchange-only run (its dumps show a stencil_width/2 ghost ring).
         # A ghost ring deeper than a neighbour's tile would need cells two tiles away.
         tb = cfg.time_block
-        self.sum_form = bool(cfg.sum_form and cfg.c_center == cfg.c_neighbor)
+        # A fast form may run: the sum form (equal coefficients) or the scaled
+        # form (unequal, c_neighbor != 0); both take the same time blocks.
+        self.sum_form = bool(cfg.sum_form and (cfg.c_center == cfg.c_neighbor or cfg.c_neighbor != 0.0))
         if tb <= 0 and dev.type == "cuda":
             tb = hip().auto_time_block(d.width, d.height, cfg.dtype, self.sum_form)
             # The time block sets the ghost depth and the exchanges per call: the
@@ -360,10 +362,18 @@ class Stencil2D:
 
     @property
     def sum_form_active(self) -> bool:
-        """Whether the passes run the sum form right now (coefficients, the
-        user's choice and the measured field range all allow it)."""
+        """Whether the passes run a fast form right now — the sum form (equal
+        coefficients) or the scaled form (unequal) — because the coefficients,
+        the user's choice and the measured field range all allow it."""
         if self.solver is not None:
             return bool(self.solver.sum_form_active())
+        return False
+
+    @property
+    def scaled_form_active(self) -> bool:
+        """Whether the fast form running is the scaled one (c_center != c_neighbor)."""
+        if self.solver is not None:
+            return bool(self.solver.scaled_form_active())
         return False
 
     def last_run_blocks(self) -> list[tuple[int, int]]:

@@ -161,7 +161,7 @@ def test_sum_form_guard_coefficients(gpu, c, active):
         b.run(20)
         b.synchronize()
         assert torch.equal(a.core_view(), b.core_view())
-        assert a.solver.sum_form_note().startswith("sum form off")
+        assert a.solver.sum_form_note().startswith("fast form off")
 
 
 def test_absmax_kernel(gpu):
