@@ -31,7 +31,8 @@
 // --direct-halo on|off|validate (validate: prepare() compares the push with the backend's exchange bitwise on
 // every rank, times both, and uses it only if equal everywhere and faster),
 // --c-center C --c-neighbor C (default 0.2 / 0.2), --no-sum-form (keep the per-step evaluation in the
-// time-blocked kernels: bitwise equal to the CPU app; default: sum form when the coefficients are equal),
+// time-blocked kernels: bitwise equal to the CPU app; default: sum form when the coefficients are equal,
+// scaled form when they differ),
 // --loopback, --bind bunch|rrobin,
 // --dump / --no-dump, --checksum, --non-periodic, --seed S, --json FILE,
 // --checkpoint FILE / --resume FILE (collective MPI-IO global grid file, any

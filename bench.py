@@ -591,9 +591,9 @@ def main(argv=None) -> int:
         if gpu:
             torch.cuda.empty_cache()
         if n == 1 and gpu and args.global_ == "32768x32768" and not args.no_sum_form:
-            # The general rate on record: the same 20-step window in the per-step
-            # form (valid for any coefficients; the headline's sum form needs
-            # c_center == c_neighbor).
+            # The same 20-step window in the per-step form (bitwise equal to S
+            # single steps, any coefficients), then at unequal coefficients in the
+            # scaled form (the headline's sum form needs c_center == c_neighbor).
             extras["stencil_32768sq_f32_per_step_gcells_per_s"] = round(
                 stencil_rate(ctx, 32768, 32768, "f32", args.steps, args.warmup, args.clock_warmup_ms / 1e3,
                              time_block=args.time_block, sum_form=False), 2)
