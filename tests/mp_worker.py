@@ -104,7 +104,8 @@ def task_gpu_solver(args):
                         overlap=args.get("overlap", True), graph=args.get("graph", True),
                         time_block=args.get("time_block", 12), direct_halo=args.get("direct", None),
                         sum_form=args.get("sum_form", True), opening=args.get("opening", "auto"),
-                        min_gain=args.get("min_gain", 0.0), direct_engine=args.get("direct_engine", "kernel"))
+                        min_gain=args.get("min_gain", 0.0), direct_engine=args.get("direct_engine", "kernel"),
+                        c_center=args.get("c_center", 0.2), c_neighbor=args.get("c_neighbor", 0.2))
     st = Stencil2D(cfg, ctx)
     if args.get("mismatch_rank") == ctx.rank:
         st.solver.inject_direct_mismatch(True)
@@ -143,6 +144,8 @@ def task_gpu_solver(args):
         out["phases"] = phases
         out["direct_state"] = st.solver.direct_state()
         out["direct"] = bool(st.solver.direct_halo())
+        out["fast_form"] = bool(st.sum_form_active)
+        out["scaled_form"] = bool(st.scaled_form_active)
         if st.comm is not None:
             out["rccl_ranks"] = int(st.comm.count())
             out["rccl_device"] = int(st.comm.device())

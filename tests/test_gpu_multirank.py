@@ -60,6 +60,21 @@ def test_ipc_direct_halo_matches_global_reference(gpu, n, dims, dtype, time_bloc
     assert (got - ref).abs().max().item() < (1e-5 if dtype == "f32" else 1e-12)
 
 
+@pytest.mark.parametrize("dtype,time_block", [("f32", 20), ("f64", 16)])
+def test_ipc_ranks_unequal_coefficients_scaled_form(gpu, dtype, time_block):
+    """Unequal coefficients across ranks (IPC, 2 x 2, direct halo): every rank
+    runs the scaled form and the field stays within rounding of the fp64
+    reference of the same weights."""
+    w, h, seed, runs = 272, 216, 17, [time_block, 2 * time_block]
+    res = run_ranks("gpu_solver", 4, {"w": w, "h": h, "dims": "2x2", "iters": sum(runs), "runs": runs, "seed": seed,
+                                      "dtype": dtype, "time_block": time_block, "direct": True,
+                                      "c_center": 0.5, "c_neighbor": 0.125}, gpu=True)
+    assert all(r["fast_form"] and r["scaled_form"] for r in res), res
+    got = torch.tensor(res[0]["grid"], dtype=torch.float64)
+    ref = jacobi_reference_global(random_values(0, 0, w, h, w, seed, dtype=torch.float64), sum(runs), 0.5, 0.125)
+    assert (got - ref).abs().max().item() < (2e-6 if dtype == "f32" else 1e-13)
+
+
 @pytest.mark.parametrize("engine", ["kernel", "copy-engine"])
 def test_ipc_direct_halo_bitwise_vs_classic_exchange(gpu, engine):
     """The push (by a CU kernel, or by the SDMA copy engines: one
