@@ -54,6 +54,21 @@ def test_scaled_pass_matches_reference(gpu, dtype, S, want):
         assert torch.equal(p, b)
 
 
+@pytest.mark.parametrize("c0,c1", [(0.0, 0.25), (-0.2, 0.2), (0.3, 0.1), (0.9, 0.025)])
+def test_scaled_pass_other_weights(gpu, c0, c1):
+    """k = c0 / c1 of 0 (the pure neighbour average), negative, 3 and 36:
+    the scaled form within fp32 rounding of the fp64 reference."""
+    w, h, S = 2048, 1024, 20
+    g, a, u = _periodic(w, h, S, torch.float32, seed=5)
+    b = torch.zeros_like(a)
+    s = torch.cuda.current_stream().cuda_stream
+    hip().stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, w, 0, h, c0, c1, True, "f32", s, "auto", True)
+    assert hip().last_stencil_dispatch() == "stream_pipe_scaled"
+    torch.cuda.synchronize()
+    err = (_core(b, g, w, h) - jacobi_reference_global(u, S, c0, c1)).abs().max().item()
+    assert err <= 2e-6, err
+
+
 @pytest.mark.parametrize("w,h,S,dtype", [(16384, 8192, 20, "f32"), (4000, 1536, 24, "f32"), (4096, 2048, 16, "f64")])
 def test_scaled_chunk_pass_bitwise_vs_one_launch(gpu, w, h, S, dtype):
     tdt = torch.float32 if dtype == "f32" else torch.float64
