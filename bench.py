@@ -147,12 +147,9 @@ def timed_run(st, ctx, steps: int, warmup: int, warm_s: float = 0.0, window_sync
         tp = time.perf_counter()
         _sync()
         t1 = time.perf_counter()
-        # "poll": the window ends when the solver's streams have drained — every
-        # one of the K steps' launches is on them — and the device-wide sync
-        # that follows (all streams idle: it only returns) is left outside it.
+        # The device-wide sync after the polled wait (all streams idle: it only
+        # returns) stays inside the window, as the contract's bracket asks.
         st.window_device_sync_us = (t1 - tp) * 1e6
-        if window_sync == "poll":
-            t1 = tp
     st.timed_host_us = (tr - t0) * 1e6  # the window's enqueue on this rank (diagnostics)
     ctx.barrier()
     return ctx.allreduce_max(t1 - t0)
@@ -403,18 +400,13 @@ def main(argv=None) -> int:
     p.add_argument("--wire-delay-us", type=float, default=0.0,
                    help="with --loopback --rehearse-peers: a single-wave kernel holds the stream this long after "
                         "every RCCL transfer, standing in for xGMI wire time (one-GPU rehearsal only)")
-    p.add_argument("--window-sync", default="auto", choices=["auto", "solver", "poll", "torch"],
+    p.add_argument("--window-sync", default="auto", choices=["auto", "solver", "torch"],
                    help="how the timed window ends: torch = torch.cuda.synchronize() alone, under a timer-thread "
                         "watchdog that aborts the halo's RCCL communicators past --comm-timeout; solver = "
                         "solver.synchronize() (polls the solver's streams, RCCL watchdog) then "
                         "torch.cuda.synchronize(); auto (default): torch for a solver without a communicator (the "
                         "1-GPU fused tile: 8-20 us less per window), solver otherwise (with two streams in flight "
-                        "the device sync alone returned ~0.2 ms late in 2-4 of 16 windows; profiles/r04_sync); "
-                        "poll = the solver's polled wait alone ends the window (its streams carry every launch of "
-                        "the K steps), torch.cuda.synchronize() follows outside it")
-    p.add_argument("--stream-priorities", default="-1,0",
-                   help="HIP priorities of the solver's main (exchange chain) and side streams, 'MAIN,SIDE' "
-                        "(lower = higher priority)")
+                        "the device sync alone returned ~0.2 ms late in 2-4 of 16 windows; profiles/r04_sync)")
     p.add_argument("--direct-halo", default="off", choices=["off", "validate"],
                    help="N > 1: validate: prepare() compares the device-initiated push of the edge bands into the "
                         "neighbours' tiles (HIP IPC over xGMI) bitwise with the RCCL exchange on every rank and times "
@@ -483,8 +475,6 @@ def main(argv=None) -> int:
                         direct_halo=("validate" if args.direct_halo == "validate" else None),
                         halo_max_ctas=args.halo_max_ctas, wire_delay_us=args.wire_delay_us,
                         direct_engine=args.direct_engine, steady=args.steady,
-                        main_priority=int(args.stream_priorities.split(",")[0]),
-                        side_priority=int(args.stream_priorities.split(",")[1]),
                         fuse_periodic=not args.no_fuse_periodic)
     st = Stencil2D(cfg, ctx)
     window_sync = args.window_sync

@@ -16,8 +16,8 @@
 #                          peers' schedule against the fused-periodic tile (no exchange). MODES (default
 #                          "auto fused"; --serial = "auto serial fused"): auto, serial, ifirst (forced
 #                          interior-first), fused; suffixes: -wNN adds NN us of rehearsed wire time per
-#                          transfer (--wire-delay-us), -cNN --halo-max-ctas NN, -ssync / -psync / -tsync
-#                          --window-sync solver / poll / torch, -p00 / -p11 stream priorities
+#                          transfer (--wire-delay-us), -cNN --halo-max-ctas NN, -ssync / -tsync
+#                          --window-sync solver / torch
 #                          -st / -ss --steady interior-first / serial (default auto) (in that order,
 #                          e.g. ifirst-c16-w40-st); a final -aw runs it with ROC_ACTIVE_WAIT_TIMEOUT=2000
 #                          (the HIP runtime spins up to 2 ms on a wait before sleeping on an interrupt)
@@ -98,11 +98,8 @@ task_window() {
       case $base in *-aw) envs+=(ROC_ACTIVE_WAIT_TIMEOUT=2000); base=${base%-aw} ;; esac
       case $base in *-t1) args+=(--warm-tail 1); base=${base%-t1} ;; esac
       case $base in *-t0) args+=(--warm-tail 0); base=${base%-t0} ;; esac
-      case $base in *-p00) args+=(--stream-priorities=0,0); base=${base%-p00} ;; esac
-      case $base in *-p11) args+=(--stream-priorities=-1,-1); base=${base%-p11} ;; esac
       case $base in *-tsync) args+=(--window-sync torch); base=${base%-tsync} ;; esac
       case $base in *-ssync) args+=(--window-sync solver); base=${base%-ssync} ;; esac
-      case $base in *-psync) args+=(--window-sync poll); base=${base%-psync} ;; esac
       case $base in *-st) args+=(--steady interior-first); base=${base%-st} ;; esac
       case $base in *-ss) args+=(--steady serial); base=${base%-ss} ;; esac
       if [[ $base =~ ^(.*)-w([0-9]+)$ ]]; then args+=(--wire-delay-us "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi

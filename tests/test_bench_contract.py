@@ -94,7 +94,7 @@ def test_bench_eight_ranks_cpu_walks_the_8gpu_path():
 def test_bench_tuning_flags_parse_on_cpu():
     """The GPU-only tuning flags parse everywhere and leave no GPU keys on CPU."""
     r = run_ranks("bench", 1, {"argv": ["--global", "64x48", "--steps", "2", "--warmup", "1", "--no-extras",
-                                        "--stream-priorities=0,0", "--halo-max-ctas", "8", "--window-sync", "torch"]})
+                                        "--halo-max-ctas", "8", "--window-sync", "torch"]})
     ex = _check(r[0]["line"], 1, 2, 1)["extras"]
     assert "halo_max_ctas" not in ex and ex["window_sync"] == "torch"
 
