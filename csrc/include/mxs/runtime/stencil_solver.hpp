@@ -127,6 +127,9 @@ struct WindowPhases {
   double host_enqueue_us = 0;  // host time to enqueue the super-step
   double gpu_span_us = 0;      // first to last GPU marker
   double wall_us = 0;          // host: start of enqueue to both streams drained
+  // The same replica once more without phase events (their records cost host
+  // time of their own): enqueue to drained, as the bench times a window.
+  double plain_wall_us = 0;
   // (phase, start us, end us) relative to the first GPU marker.
   std::vector<std::tuple<std::string, double, double>> phases;
 };

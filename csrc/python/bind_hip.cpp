@@ -581,6 +581,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
             d["host_enqueue_us"] = w.host_enqueue_us;
             d["gpu_span_us"] = w.gpu_span_us;
             d["wall_us"] = w.wall_us;
+            d["plain_wall_us"] = w.plain_wall_us;
             py::list ph;
             for (const auto& [name, t0, t1] : w.phases) ph.append(py::make_tuple(name, t0, t1));
             d["phases"] = ph;

@@ -507,6 +507,7 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
   const auto t0 = std::chrono::steady_clock::now();
   HaloLastPass* hl = nullptr;
   if (!fused_ && halo_last_on_ && !ghost_fresh_) hl = halo_last_pass(S, true);
+  const bool primed = !ghost_fresh_;  // the replica's opening exchanges cur's ring
   if (fused_) {  // the whole super-step is one wrap-around pass
     out.opening = "fused";
     marks.mark("main:start", m);
@@ -563,6 +564,27 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
     }
     out.gpu_span_us = std::max(out.gpu_span_us, t);
   }
+  // The unmarked replica: the same launches and exchanges on every rank, from
+  // drained streams after a device barrier (cur -> nxt again, state unchanged).
+  join_side();
+  wait_idle("profile_window");
+  device_barrier("profile_window");
+  out.plain_wall_us = 1e3 * host_span_ms(
+                                [&] {
+                                  if (fused_) {
+                                    enqueue_block(cur_, nxt_, S);
+                                    return;
+                                  }
+                                  if (hl) {
+                                    enqueue_halo_last(cur_, nxt_, hl);
+                                    join_side();
+                                  } else {
+                                    if (primed) ex_->exchange(cur_, m);
+                                    core_pass(cur_, nxt_, S, m);
+                                  }
+                                  if (!(multi_rank_ && supersteps == 1)) ex_->exchange(nxt_, m);
+                                },
+                                "profile_window");
   ghost_fresh_ = false;  // conservative: the next call re-primes
   return out;
 }

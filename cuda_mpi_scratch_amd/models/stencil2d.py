@@ -479,6 +479,9 @@ class Stencil2D:
                 "host_enqueue_us": round(p["host_enqueue_us"], 1), "gpu_span_us": round(p["gpu_span_us"], 1),
                 "wall_us": round(p["wall_us"], 1),
                 "host_overhead_us": round(p["wall_us"] - p["gpu_span_us"], 1),
+                # The same replica without phase events: its wall time over the GPU span.
+                "plain_wall_us": round(p["plain_wall_us"], 1),
+                "plain_wall_over_span": round(p["plain_wall_us"] / p["gpu_span_us"], 3) if p["gpu_span_us"] else None,
                 "phases_us": {name: [round(t0, 1), round(t1, 1)] for name, t0, t1 in p["phases"]}}
 
     # ----------------------------------------------------------------- dump

@@ -380,6 +380,8 @@ def test_profile_window_phases_and_state(gpu, opening, fused):
     assert torch.equal(a.core_view(), b.core_view())
     ph = p["phases_us"]
     assert p["gpu_span_us"] > 0 and p["wall_us"] >= p["gpu_span_us"] * 0.5 and p["host_enqueue_us"] > 0
+    # The unmarked replica of the same super-step (collective, state-preserving too).
+    assert p["plain_wall_us"] > 0.5 * p["gpu_span_us"] and p["plain_wall_over_span"] > 0.5
     for name, (t0, t1) in ph.items():
         assert 0 <= t0 <= t1 <= p["gpu_span_us"] + 1e-3, (name, t0, t1)
     if fused:
