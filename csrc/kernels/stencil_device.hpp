@@ -696,7 +696,9 @@ struct BodySumF64 : BodyWideF64 {
 };
 
 // Scaled form (any c_center, c_neighbor != 0; the pipeline passes of the
-// production depths): u' = c1 (N + S + W + E + k u) with k = c0 / c1, so a pass
+// production depths). The update is this framework's (the reference's
+// Compute() is empty: stencil2d/mpi-2d-stencil-subarray-cuda.cu:32-37; SURVEY
+// K10). u' = c1 (N + S + W + E + k u) with k = c0 / c1, so a pass
 // carries v_l = u_l / c1^l, v' = (N + S + W + E) + k v — one packed FMA per
 // cell pair in place of the per-step form's multiply and FMA — and applies c1^S
 // once when it stores (the kernels' c0 argument holds c1^S, their c1 argument

@@ -9,6 +9,9 @@
 // Every decision is timed as the bench times a window (host clock, drained
 // streams, a device barrier in front) and taken on the paired ratios of the
 // per-round maxima over ranks (runtime/decision.hpp), so every rank adopts it.
+// What they schedule is the reference's exchange-then-compute loop
+// (stencil2d/stencil2D.h:361-377, stencil2d/mpi-2d-stencil-subarray-cuda.cu:
+// 169-172) with the exchange hidden where the measurement says it pays.
 #include "mxs/runtime/stencil_solver.hpp"
 
 #include <algorithm>
