@@ -20,7 +20,8 @@
 #                          --window-sync solver / torch
 #                          -st / -ss --steady interior-first / serial (default auto) (in that order,
 #                          e.g. ifirst-c16-w40-st); a final -aw runs it with ROC_ACTIVE_WAIT_TIMEOUT=2000
-#                          (the HIP runtime spins up to 2 ms on a wait before sleeping on an interrupt)
+#                          (the HIP runtime spins up to 2 ms on a wait before sleeping on an interrupt);
+#                          -cwNN --clock-warmup-ms NN, -t0 / -t1 --warm-tail 0 / 1 (checked first)
 #                          -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
 #   final                  tests + smoke + the driver's bench command + its kernel-trace profile
@@ -96,6 +97,7 @@ task_window() {
       local args=(--global "$tile" --steps "${WINDOW_STEPS:-20}" --warmup 5 --no-extras)
       local base=$mode envs=()
       case $base in *-aw) envs+=(ROC_ACTIVE_WAIT_TIMEOUT=2000); base=${base%-aw} ;; esac
+      if [[ $base =~ ^(.*)-cw([0-9]+)$ ]]; then args+=(--clock-warmup-ms "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi
       case $base in *-t1) args+=(--warm-tail 1); base=${base%-t1} ;; esac
       case $base in *-t0) args+=(--warm-tail 0); base=${base%-t0} ;; esac
       case $base in *-tsync) args+=(--window-sync torch); base=${base%-tsync} ;; esac
