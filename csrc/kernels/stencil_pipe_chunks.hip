@@ -139,7 +139,9 @@ void stencil5_chunk_pass(const T* in, T* out, const TileGeom& g, const Stencil5C
   const T sc = T(std::pow(double(c1), double(sh.steps)));
   // Kernel coefficients: sum form (c^S, c), scaled form (c1^S, c0 / c1), per step (c0, c1).
   const T k0 = sh.sum ? sc : c0;
-  const T k1 = sh.scaled ? T(double(c.center) / double(c.neighbor)) : c1;
+  // k from the element-type coefficients, exactly as launch_pipe_form forms it:
+  // the one-launch and the chunk-list passes must run the same k to stay bitwise equal.
+  const T k1 = sh.scaled ? T(double(c0) / double(c1)) : c1;
   if constexpr (sizeof(T) == 4) {
     if (sh.steps == 20) {
       if (sh.scaled) launch_for<T, 20, true, kScaledBody>(in, out, g, k0, k1, sh, table, entries, s);

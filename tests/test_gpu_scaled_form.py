@@ -69,8 +69,10 @@ def test_scaled_pass_other_weights(gpu, c0, c1):
     assert err <= 2e-6, err
 
 
-@pytest.mark.parametrize("w,h,S,dtype", [(16384, 8192, 20, "f32"), (4000, 1536, 24, "f32"), (4096, 2048, 16, "f64")])
-def test_scaled_chunk_pass_bitwise_vs_one_launch(gpu, w, h, S, dtype):
+@pytest.mark.parametrize("w,h,S,dtype,c0,c1", [(16384, 8192, 20, "f32", C0, C1), (4000, 1536, 24, "f32", C0, C1),
+                                               (4096, 2048, 16, "f64", C0, C1), (4096, 2048, 20, "f32", 0.3, 0.1),
+                                               (4096, 2048, 16, "f64", 0.3, 0.1)])
+def test_scaled_chunk_pass_bitwise_vs_one_launch(gpu, w, h, S, dtype, c0, c1):
     tdt = torch.float32 if dtype == "f32" else torch.float64
     g = core().TileGeom.aligned(w, h, S, S, tdt.itemsize)
     gen = torch.Generator(device=gpu).manual_seed(w + S)
@@ -78,9 +80,9 @@ def test_scaled_chunk_pass_bitwise_vs_one_launch(gpu, w, h, S, dtype):
     ref = torch.full_like(src, -3.0)
     got = torch.full_like(src, -3.0)
     s = torch.cuda.current_stream().cuda_stream
-    hip().stencil5_tb(src.data_ptr(), ref.data_ptr(), g, S, 0, w, 0, h, C0, C1, False, dtype, s, "auto", True)
+    hip().stencil5_tb(src.data_ptr(), ref.data_ptr(), g, S, 0, w, 0, h, c0, c1, False, dtype, s, "auto", True)
     assert hip().last_stencil_dispatch() == "stream_pipe_scaled"
-    d = hip().stencil5_chunk_pass(src.data_ptr(), got.data_ptr(), g, S, C0, C1, dtype, 0, s, True)
+    d = hip().stencil5_chunk_pass(src.data_ptr(), got.data_ptr(), g, S, c0, c1, dtype, 0, s, True)
     assert d is not None and d["check"] == ""
     assert hip().last_stencil_dispatch() == "stream_pipe_scaled_chunks"
     torch.cuda.synchronize()
