@@ -18,6 +18,7 @@ pytestmark = pytest.mark.gpu
     (4, "2x2", 12, True, True),
     (4, "2x2", 1, True, False),
     (6, "2x3", 5, True, True),
+    (8, "4x2", 20, False, True),  # the 8-GPU grid at the production depth: 8 ranks' agreements
 ])
 def test_ipc_solver_matches_global_reference(gpu, n, dims, time_block, overlap, graph):
     w, h, iters, seed = 264, 200, 29, 7
