@@ -545,6 +545,11 @@ def main(argv=None) -> int:
     p.add_argument("--variant", default="auto", choices=["auto", "roll", "lds"])
     p.add_argument("--time-block", type=int, default=StencilConfig.time_block)
     p.add_argument("--opening", default="auto", choices=["auto", "serial", "interior-first"])
+    p.add_argument("--steady", default="auto", choices=["auto", "serial", "interior-first"])
+    p.add_argument("--c-center", type=float, default=StencilConfig.c_center)
+    p.add_argument("--c-neighbor", type=float, default=StencilConfig.c_neighbor)
+    p.add_argument("--no-sum-form", action="store_true",
+                   help="per-step evaluation (bitwise equal to S single steps) instead of the sum / scaled form")
     p.add_argument("--seed", type=int, default=StencilConfig.seed)
     p.add_argument("--checkpoint", default=None, help="write the final field to this grid file")
     p.add_argument("--resume", default=None, help="start from this grid file (any decomposition)")
@@ -560,7 +565,8 @@ def main(argv=None) -> int:
     cfg = StencilConfig(global_width=gw, global_height=gh, dims=f"{rows}x{cols}", dtype=args.dtype,
                         backend=args.backend, overlap=False if args.no_overlap else None, graph=not args.no_graph,
                         loopback=args.loopback, variant=args.variant, time_block=args.time_block,
-                        seed=args.seed, opening=args.opening)
+                        seed=args.seed, opening=args.opening, steady=args.steady, c_center=args.c_center,
+                        c_neighbor=args.c_neighbor, sum_form=not args.no_sum_form)
     st = Stencil2D(cfg, ctx)
     if args.resume:
         hdr = st.load_checkpoint(args.resume)
@@ -578,7 +584,9 @@ def main(argv=None) -> int:
     gcells = st.cells_per_step * args.iters / dt / 1e9
     rec = {"metric": "stencil2d_gcells_per_s", "value": gcells, "ms_per_iter": dt / args.iters * 1e3,
            "ranks": ctx.world_size, "dims": f"{rows}x{cols}", "config": asdict(cfg), "backend": st.backend,
-           "graph": st.graph_status(), "iteration": st.iteration}
+           "graph": st.graph_status(), "iteration": st.iteration,
+           "evaluation": ("scaled form" if st.scaled_form_active else "sum form" if st.sum_form_active
+                          else "per step")}
     if args.checkpoint:
         st.save_checkpoint(args.checkpoint)
     if ctx.is_root:

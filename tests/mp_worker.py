@@ -78,6 +78,20 @@ def task_bench(args):
     return {"rank": int(os.environ["RANK"]), "rc": rc, "line": lines[-1] if lines else None}
 
 
+def task_stencil_cli(args):
+    """python -m cuda_mpi_scratch_amd.models.stencil2d main() on every rank (CPU / gloo)."""
+    import contextlib
+    import io
+
+    from cuda_mpi_scratch_amd.models import stencil2d
+
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        rc = stencil2d.main(args["argv"])
+    lines = [ln for ln in buf.getvalue().splitlines() if ln.startswith("{")]
+    return {"rank": int(os.environ["RANK"]), "rc": rc, "line": lines[-1] if lines else None}
+
+
 def task_ipc_pingpong_isolated(args):
     """bench.py's isolated IPC ping-pong (child processes) from two ranks."""
     sys.path.insert(0, ROOT)

@@ -91,3 +91,17 @@ def test_stencil_config_rejects_bad_options(field, value):
         StencilConfig(**{field: value})
     StencilConfig(steady="interior-first", opening="serial", direct_halo="validate", direct_engine="copy-engine",
                   prefer="mpi")
+
+
+def test_stencil_cli_weights_two_ranks_cpu():
+    """The package CLI with unequal weights on 2 gloo ranks: the record carries
+    the weights and the evaluation form (per step on CPU)."""
+    import json
+
+    r = run_ranks("stencil_cli", 2, {"argv": ["--global", "64x48", "--iters", "4", "--warmup", "1", "--backend",
+                                              "torch", "--c-center", "0.5", "--c-neighbor", "0.125",
+                                              "--steady", "serial"]})
+    assert all(x["rc"] == 0 for x in r)
+    d = json.loads(r[0]["line"])
+    assert d["config"]["c_center"] == 0.5 and d["config"]["c_neighbor"] == 0.125 and d["ranks"] == 2
+    assert d["evaluation"] == "per step" and d["iteration"] == 5
