@@ -195,8 +195,9 @@ bool rot_ok(const TileGeom& g, index_t x1, index_t chunk_rows) {
 }
 
 // SUM: the balanced rotated kernel runs the sum form (sc = c^S, see
-// stencil_device.hpp); every other form keeps the per-step coefficients.
-template <typename T, int S, bool WRAP, bool SUM = false>
+// stencil_device.hpp), with XB = kScaledBody the scaled form (sc = c1^S,
+// k = c0 / c1); every other form keeps the per-step coefficients.
+template <typename T, int S, bool WRAP, bool SUM = false, int XB = 0>
 void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
                    T sc, hipStream_t s) {
   constexpr int OW = StreamShape<T, S>::OW;
@@ -208,9 +209,10 @@ void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
   if (groups * rows >= index_t(blocks) * 64) {
     const index_t share = (groups * rows + blocks - 1) / blocks;
     if (kF32 && rot_ok<T>(g, x1, std::min(share, rows))) {
-      stencil5_stream_balanced_kernel<T, S, stream_pf<T, S>(), WRAP, true, kF32, SUM><<<blocks, kBlock, 0, s>>>(
-          in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, SUM ? sc : c0, c1);
-      note(SUM ? "stream_balanced_rot_sum" : "stream_balanced_rot");
+      const T kc = XB == kScaledBody ? T(double(c0) / double(c1)) : c1;
+      stencil5_stream_balanced_kernel<T, S, stream_pf<T, S>(), WRAP, true, kF32, SUM, XB><<<blocks, kBlock, 0, s>>>(
+          in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, SUM ? sc : c0, kc);
+      note(XB == kScaledBody ? "stream_balanced_rot_scaled" : SUM ? "stream_balanced_rot_sum" : "stream_balanced_rot");
     } else {
       stencil5_stream_balanced_kernel<T, S, 3, WRAP><<<blocks, kBlock, 0, s>>>(
           in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, c0, c1);
@@ -258,7 +260,9 @@ void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, i
     if (wide_pipe_ok<T, S, WRAP>(g, x0, x1, y0, y1))
       return launch_pipe<T, S, WRAP, SUM, XB>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
   }
-  launch_stream<T, S, WRAP, SUM && XB == 0 && sizeof(T) == 4>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
+  // fp32: the balanced rotated kernel takes the sum or the scaled form; fp64's
+  // stream kernels run per step.
+  launch_stream<T, S, WRAP, SUM && sizeof(T) == 4, sizeof(T) == 4 ? XB : 0>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
 }
 
 // form: 1 = sum form (c_center == c_neighbor, allowed by the caller: the fast
@@ -274,7 +278,7 @@ void dispatch_tb(int steps, int form, const T* in, T* out, const TileGeom& g, in
       if constexpr (S > 1) {
         if (form == 1) return launch_tb<T, S, WRAP, true>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s);
       }
-      if constexpr (sizeof(T) == 8 && S == 16) {
+      if constexpr ((sizeof(T) == 8 && S == 16) || (sizeof(T) == 4 && S > 1)) {
         if (form == 2)
           return launch_tb<T, S, WRAP, true, kScaledBody>(in, out, g, x0, x1, y0, y1, c0, c1, sc, v, s);
       }

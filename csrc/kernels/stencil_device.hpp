@@ -1073,7 +1073,7 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_kernel(const T* __rest
 // so the apron columns two neighbouring waves both read are L2 hits — and a
 // share that crosses a group boundary restarts there. No tail round, and
 // (3S-1)/share redundant rows instead of (3S-1)/CH per chunk.
-template <typename T, int S, int PF, bool WRAP, bool DPP = true, bool ROT = false, bool SUM = false>
+template <typename T, int S, int PF, bool WRAP, bool DPP = true, bool ROT = false, bool SUM = false, int XB = 0>
 __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
     const T* __restrict__ in, T* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
     index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, index_t share, T c0, T c1) {
@@ -1096,7 +1096,7 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
     if (xw < x_end) {
       wp.done = a - a0;
       if constexpr (ROT)
-        stream_chunk_fast<typename FastBody<T, SUM>::type, S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end,
+        stream_chunk_fast<typename FastBody<T, SUM, XB>::type, S, PF, WRAP>(in, out, pitch, core_off, W, H, xw, x_end,
                                                                         y_begin + r0, y_begin + r1, c0, c1, &wp);
       else
         stream_chunk<T, S, PF, WRAP, DPP>(in, out, pitch, core_off, W, H, xw, x_end, y_begin + r0, y_begin + r1, c0,

@@ -34,7 +34,10 @@ def _core(buf, g, w, h):
 
 
 @pytest.mark.parametrize("dtype,S,want", [("f32", 20, "stream_pipe_scaled"), ("f32", 24, "stream_pipe_scaled"),
-                                          ("f64", 16, "stream_pipe_scaled"), ("f32", 18, "stream_pipe")])
+                                          ("f64", 16, "stream_pipe_scaled"), ("f32", 18, "stream_pipe"),
+                                          ("f32", 12, "stream_balanced_rot_scaled"),
+                                          ("f32", 5, "stream_balanced_rot_scaled"),
+                                          ("f64", 12, "stream_pipe")])
 def test_scaled_pass_matches_reference(gpu, dtype, S, want):
     tdt = torch.float32 if dtype == "f32" else torch.float64
     w, h = 4096, 2048
@@ -47,7 +50,7 @@ def test_scaled_pass_matches_reference(gpu, dtype, S, want):
     ref = jacobi_reference_global(u, S, C0, C1)
     err = (_core(b, g, w, h) - ref).abs().max().item()
     assert err <= (2e-6 if dtype == "f32" else 1e-14), err
-    if want == "stream_pipe":  # no scaled instantiation at this depth: exactly the per-step form
+    if want == "stream_pipe":  # no scaled form at this depth: exactly the per-step form
         p = torch.zeros_like(a)
         hip().stencil5_tb(a.data_ptr(), p.data_ptr(), g, S, 0, w, 0, h, C0, C1, True, dtype, s, "auto", False)
         torch.cuda.synchronize()
