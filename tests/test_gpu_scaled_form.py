@@ -40,7 +40,9 @@ def _core(buf, g, w, h):
                                           ("f64", 12, "stream_pipe")])
 def test_scaled_pass_matches_reference(gpu, dtype, S, want):
     tdt = torch.float32 if dtype == "f32" else torch.float64
-    w, h = 4096, 2048
+    # The balanced stream kernel needs >= 64 rows per workgroup (smaller rectangles
+    # take the per-step grid form, as in the sum form): 8192^2 for those depths.
+    w, h = (8192, 8192) if want.startswith("stream_balanced") else (4096, 2048)
     g, a, u = _periodic(w, h, S, tdt, seed=S)
     b = torch.zeros_like(a)
     s = torch.cuda.current_stream().cuda_stream
