@@ -54,7 +54,8 @@ struct Stencil5Coeffs {
 };
 inline bool uses_sum_form(const Stencil5Coeffs& c) { return c.sum_form && c.center == c.neighbor; }
 // The scaled form (stencil_device.hpp): unequal coefficients, c_neighbor != 0,
-// at the pipeline depths (fp32 20 / 24, fp64 16; other depths run per step).
+// in the fp32 pipeline (20 / 24) and balanced stream kernel (2-16) and the fp64
+// wide pipeline (16); other depths and kernel forms run per step.
 inline bool uses_scaled_form(const Stencil5Coeffs& c) {
   return c.sum_form && c.center != c.neighbor && c.neighbor != 0.0;
 }

@@ -695,8 +695,8 @@ struct BodySumF64 : BodyWideF64 {
   }
 };
 
-// Scaled form (any c_center, c_neighbor != 0; the pipeline passes of the
-// production depths). The update is this framework's (the reference's
+// Scaled form (any c_center, c_neighbor != 0; the fp32 pipeline and balanced
+// stream kernels, the fp64 wide pipeline at depth 16). The update is this framework's (the reference's
 // Compute() is empty: stencil2d/mpi-2d-stencil-subarray-cuda.cu:32-37; SURVEY
 // K10). u' = c1 (N + S + W + E + k u) with k = c0 / c1, so a pass
 // carries v_l = u_l / c1^l, v' = (N + S + W + E) + k v — one packed FMA per
