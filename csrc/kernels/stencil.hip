@@ -241,7 +241,8 @@ void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
 // wave strip would recompute 8-32x the strip, so thin strips get a matching thin
 // LDS tile (32 x 128 for column strips, 128 x 16 for row strips).
 // XB = kScaledBody (with SUM): the scaled form, on the fp64 wide pipeline at
-// S = 16 only; the thin-strip tiles and the stream kernels then run per step.
+// S = 16 and the fp32 balanced stream kernel; the thin-strip tiles, the grid
+// form and the fp64 stream kernels run per step.
 template <typename T, int S, bool WRAP, bool SUM, int XB = 0>
 void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1, T c0, T c1,
                T sc, StencilVariant v, hipStream_t s) {
@@ -267,8 +268,8 @@ void launch_tb(const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, i
 
 // form: 1 = sum form (c_center == c_neighbor, allowed by the caller: the fast
 // bodies take sc = c^S), 2 = scaled form (c_center != c_neighbor: sc = c1^S and
-// k = c0 / c1, at the pipeline depths fp32 20 / 24 and fp64 16; elsewhere per
-// step), 0 = per step. S = 1 always keeps the per-step form.
+// k = c0 / c1; fp32 depths 2-16 and 20 / 24, fp64 16; elsewhere per step),
+// 0 = per step. S = 1 always keeps the per-step form.
 template <typename T, bool WRAP, int S = 1>
 void dispatch_tb(int steps, int form, const T* in, T* out, const TileGeom& g, index_t x0, index_t x1, index_t y0,
                  index_t y1, T c0, T c1, StencilVariant v, hipStream_t s) {
