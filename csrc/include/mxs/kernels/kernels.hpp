@@ -102,6 +102,10 @@ constexpr int kMaxTimeBlockDeep = 32;
 // stores through a single buffer descriptor: below 2^31 with room for the
 // drop offsets of stencil_device.hpp (a sum of two never wraps).
 constexpr index_t kMaxChunkBytes = 0x7F000000;
+// The wave pipelines walk a longer share in pieces of at most kMaxChunkBytes;
+// rows must be narrow enough that a piece holds at least this many (each piece
+// pays its own pipeline fill of S rows).
+constexpr index_t kMinChunkRows = 64;
 // Measured default S for a w x h tile of `elem_bytes`-byte cells
 // (profiles/stencil_tuning/tunes_*, profiles/r02_deep/pipe*_*, profiles/r02_f64,
 // profiles/r02_sum): fp32 takes the two-stage pipeline at S = 20 (sum form,

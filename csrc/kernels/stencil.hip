@@ -188,10 +188,12 @@ int balanced_blocks() {
 // >= 4096 waves.
 // The fp32 rotated-pair form (stream_chunk_rot: 11 VALU per level-row instead
 // of ~15, DPP shifts folded into the adds) stores through a buffer descriptor
-// over one chunk's rows: it needs whole output vectors and a chunk under 2 GiB.
+// over one chunk's rows: it needs whole output vectors and a chunk of at most
+// kMaxChunkBytes (the balanced kernel walks longer shares in pieces, so there
+// only kMinChunkRows rows have to fit).
 template <typename T>
 bool rot_ok(const TileGeom& g, index_t x1, index_t chunk_rows) {
-  return sizeof(T) == 4 && x1 % 4 == 0 && chunk_rows * g.pitch * index_t(sizeof(T)) < (index_t(1) << 31);
+  return sizeof(T) == 4 && x1 % 4 == 0 && chunk_rows * g.pitch * index_t(sizeof(T)) <= kMaxChunkBytes;
 }
 
 // SUM: the balanced rotated kernel runs the sum form (sc = c^S, see
@@ -208,7 +210,7 @@ void launch_stream(const T* in, T* out, const TileGeom& g, index_t x0, index_t x
   const int blocks = balanced_blocks<T, S, WRAP, SUM>();
   if (groups * rows >= index_t(blocks) * 64) {
     const index_t share = (groups * rows + blocks - 1) / blocks;
-    if (kF32 && rot_ok<T>(g, x1, std::min(share, rows))) {
+    if (kF32 && rot_ok<T>(g, x1, std::min<index_t>(kMinChunkRows, std::min(share, rows)))) {
       const T kc = XB == kScaledBody ? T(double(c0) / double(c1)) : c1;
       stencil5_stream_balanced_kernel<T, S, stream_pf<T, S>(), WRAP, true, kF32, SUM, XB><<<blocks, kBlock, 0, s>>>(
           in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, share, SUM ? sc : c0, kc);

@@ -1088,10 +1088,14 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
   const index_t b = a + share < total ? a + share : total;
   WavePrio wp;
   if (b > a) wp.quarters = 4.f / float(b - a);
+  // ROT stores go through one buffer descriptor per call: longer shares are
+  // walked in pieces of at most kMaxChunkBytes (see stencil5_stream_pipe_kernel).
+  const index_t max_rows = ROT ? kMaxChunkBytes / (pitch * index_t(sizeof(T))) : rows;
 #pragma unroll 1
   while (a < b) {  // workgroup-uniform
     const index_t grp = a / rows, r0 = a - grp * rows;
-    const index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
+    index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
+    r1 = r1 - r0 > max_rows ? r0 + max_rows : r1;
     const index_t xw = x_begin + (grp * kWavesPerBlock + wave) * OW;
     if (xw < x_end) {
       wp.done = a - a0;
@@ -1496,10 +1500,16 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
     a = slot * shares.share;
     b = a + shares.share < total ? a + shares.share : total;
   }
+  // Rows per pipe_chunk call: its output buffer descriptor spans at most
+  // kMaxChunkBytes (32-bit offsets), so on very wide tiles (rows of MiBs: a
+  // 65536^2 fp32 tile, 16 GiB per buffer) a share is walked in pieces, each
+  // paying its own pipeline fill (the launcher checks >= 64 rows fit).
+  const index_t max_rows = kMaxChunkBytes / (pitch * index_t(sizeof(T)));
 #pragma unroll 1
   while (a < b) {  // workgroup-uniform: all 8 waves take every chunk (barriers inside)
     const index_t grp = a / rows, r0 = a - grp * rows;
-    const index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
+    index_t r1 = rows < r0 + (b - a) ? rows : r0 + (b - a);
+    r1 = r1 - r0 > max_rows ? r0 + max_rows : r1;
     if constexpr (JOINT) {
       pipe_chunk<B, S0, S1, PF, WRAP, true, G, LAG1>(in, out, pitch, core_off, W, H, x_begin + grp * OWG, x_end,
                                                y_begin + r0, y_begin + r1, c0, c1, ring, stage, strip);

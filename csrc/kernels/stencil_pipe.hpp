@@ -139,7 +139,6 @@ void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_
   const index_t share = pipe_share<T, S, WRAP, SUM, JS0>(x0, x1, y0, y1);
   const int blocks = pipe_blocks<T, S, WRAP, SUM, JS0>();
   PipeShares shares = PipeShares::equal(share);
-  index_t chunk = std::min(share, y1 - y0);
   if (pipe_balanced() && blocks <= kMaxShareBlocks) {
     constexpr int S0 = JS0 > 0 ? JS0 : pipe_s0<T, S, SUM>();
     constexpr int OW = StripShape<T, S, true>::OW;
@@ -147,10 +146,12 @@ void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_
     const index_t groups =
         JS0 > 0 ? (x1 - x0 + OWG - 1) / OWG : ((x1 - x0 + OW - 1) / OW + kWavesPerBlock - 1) / kWavesPerBlock;
     pipe_starts(groups, y1 - y0, blocks, pipe_fill_rows<S0, S - S0, pipe_pf<T, S>(), LAG1>(), &shares);
-    for (int w = 0; w < shares.n; ++w) chunk = std::max<index_t>(chunk, std::min<index_t>(y1 - y0, shares.start[w + 1] - shares.start[w]));
   }
-  MXS_CHECK(chunk * g.pitch * index_t(sizeof(T)) <= kMaxChunkBytes,
-            "stencil5_tb: a pipeline chunk must stay within kMaxChunkBytes (buffer-descriptor stores)");
+  // Shares longer than kMaxChunkBytes are walked in pieces inside the kernel;
+  // a piece must still hold a useful number of rows.
+  MXS_CHECK(g.pitch * index_t(sizeof(T)) * kMinChunkRows <= kMaxChunkBytes,
+            "stencil5_tb: rows of " << g.pitch * index_t(sizeof(T)) << " bytes leave fewer than " << kMinChunkRows
+                                    << " rows per pipeline chunk (buffer-descriptor stores)");
   // Sum form: (c^S, c); scaled form: (c1^S, c0 / c1); per step: (c0, c1).
   const T kc = XB == kScaledBody ? T(double(c0) / double(c1)) : c1;
   pipe_kernel<T, S, WRAP, SUM, JS0, LAG1, XB>()<<<blocks, 2 * kBlock, 0, s>>>(
@@ -189,7 +190,8 @@ void launch_pipe_impl(const T* in, T* out, const TileGeom& g, index_t x0, index_
 
 // Whether the fp64 wide-lane pipeline can take [x0, x1) x [y0, y1) at depth S:
 // whole 4-cell lane vectors (x0, x1 and, wrapping, the width multiples of 4),
-// the apron inside the row padding, and a chunk of at most kMaxChunkBytes.
+// the apron inside the row padding, and rows narrow enough for kMinChunkRows
+// per descriptor-sized piece.
 template <typename T, int S, bool WRAP>
 bool wide_pipe_ok_impl(const TileGeom& g, index_t x0, index_t x1, index_t y0, index_t y1) {
   constexpr int SA = StripShape<T, S, true>::SA;
@@ -197,8 +199,9 @@ bool wide_pipe_ok_impl(const TileGeom& g, index_t x0, index_t x1, index_t y0, in
   if (WRAP && g.width % 4 != 0) return false;
   const index_t lead = g.x_origin + g.halo_x;
   if (!WRAP && (lead < SA || g.pitch < lead + (g.width + 3) / 4 * 4 + SA)) return false;
-  return std::min(pipe_share<T, S, WRAP, false>(x0, x1, y0, y1), y1 - y0) * g.pitch * index_t(sizeof(T)) <=
-         kMaxChunkBytes;
+  (void)y0;
+  (void)y1;
+  return g.pitch * index_t(sizeof(T)) * kMinChunkRows <= kMaxChunkBytes;  // longer chunks go in pieces
 }
 
 
