@@ -1543,12 +1543,17 @@ __global__ __launch_bounds__(2 * kWavesPerBlock * kWaveSize) void stencil5_pipe_
   const int wave = threadIdx.x / kWaveSize;
   const int strip = wave % G, stage = wave / G;
   const PassChunk* __restrict__ mine = table + index_t(blockIdx.x) * entries;
+  const index_t max_rows = kMaxChunkBytes / (pitch * index_t(sizeof(T)));  // pieces, as in stencil5_stream_pipe_kernel
 #pragma unroll 1
   for (int e = 0; e < entries; ++e) {  // workgroup-uniform
     const PassChunk c = mine[e];
     if (c.r1 <= c.r0) break;  // lists are packed from slot 0
-    pipe_chunk<B, S0, S1, PF, false, true, G, LAG1>(in, out, pitch, core_off, W, H, x_begin + index_t(c.group) * OWG,
-                                                   x_end, y_begin + c.r0, y_begin + c.r1, c0, c1, ring, stage, strip);
+#pragma unroll 1
+    for (index_t r0 = c.r0; r0 < c.r1; r0 += max_rows) {
+      const index_t r1 = c.r1 - r0 > max_rows ? r0 + max_rows : c.r1;
+      pipe_chunk<B, S0, S1, PF, false, true, G, LAG1>(in, out, pitch, core_off, W, H, x_begin + index_t(c.group) * OWG,
+                                                     x_end, y_begin + r0, y_begin + r1, c0, c1, ring, stage, strip);
+    }
   }
 }
 

@@ -110,6 +110,8 @@ bool chunk_pass_shape(const TileGeom& g, int steps, const Stencil5Coeffs& c, Chu
   if ((g.pitch % N) != 0 || ((g.x_origin + g.halo_x) % N) != 0) return false;
   const index_t sa = (steps + 3) / 4 * 4;  // the joint read reach A0 + A1
   if (g.x_origin + g.halo_x < sa || g.pitch < g.x_origin + g.halo_x + (g.width + 3) / 4 * 4 + sa) return false;
+  // Entries longer than kMaxChunkBytes run in pieces (stencil5_pipe_chunks_kernel).
+  if (g.pitch * index_t(sizeof(T)) * kMinChunkRows > kMaxChunkBytes) return false;
   // The scaled form scales the stored result by c_neighbor^S: it must be a normal number.
   const bool scaled = uses_scaled_form(c) &&
                       std::fabs(double(T(std::pow(c.neighbor, double(steps))))) >= double(std::numeric_limits<T>::min());

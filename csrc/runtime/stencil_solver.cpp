@@ -616,10 +616,9 @@ std::unique_ptr<typename StencilSolver<T>::HaloLastPass> StencilSolver<T>::build
   } catch (const std::invalid_argument&) {
     return nullptr;
   }
-  index_t longest = 0;
-  for (const auto* sc : {&hl->sched.inner, &hl->sched.outer})
-    for (const auto& c : sc->table) longest = std::max<index_t>(longest, c.r1 - c.r0);
-  if (longest * tile_.pitch * index_t(sizeof(T)) > kernels::kMaxChunkBytes) return nullptr;  // past the descriptor range
+  // Chunks longer than kMaxChunkBytes run in pieces inside the kernel; rows
+  // must leave kMinChunkRows per piece.
+  if (tile_.pitch * index_t(sizeof(T)) * kernels::kMinChunkRows > kernels::kMaxChunkBytes) return nullptr;
   hl->inner_shape = shape;
   hl->inner_shape.blocks = hl->sched.inner.blocks;
   hl->outer_shape = shape;

@@ -40,6 +40,7 @@ def _chunks_kernel(sum_form):
     (16384, 8192, 20, "f32"),   # the 8-GPU tile
     (4000, 1536, 24, "f32"),    # ragged last group, S = 24
     (4096, 2048, 16, "f64"),    # fp64 wide lanes, 8 + 8
+    (1 << 20, 1024, 20, "f32"),  # 4 MiB rows: entries run in descriptor-sized pieces
 ])
 @pytest.mark.parametrize("sum_form", [True, False])
 def test_chunk_pass_bitwise_vs_one_launch(gpu, w, h, S, dtype, sum_form):
@@ -269,6 +270,7 @@ def test_peer_schedule_bare_last_pass_bitwise(gpu, opening, runs):
     (4096, 2048, "f32", 24, (48,)),         # S = 24 (12 + 12)
     (4000, 1536, "f32", 24, (24, 24)),      # ragged last group
     (4096, 2048, "f64", 16, (32,)),         # fp64 wide lanes, 8 + 8
+    (1 << 20, 1024, "f32", 20, (20,)),      # 4 GiB tile of 4 MiB rows (descriptor-sized pieces)
 ])
 @pytest.mark.parametrize("sum_form", [True, False])
 def test_interior_first_bitwise_vs_serial(gpu, w, h, dtype, S, runs, sum_form):

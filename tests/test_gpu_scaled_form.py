@@ -76,7 +76,9 @@ def test_scaled_pass_other_weights(gpu, c0, c1):
 
 @pytest.mark.parametrize("w,h,S,dtype,c0,c1", [(16384, 8192, 20, "f32", C0, C1), (4000, 1536, 24, "f32", C0, C1),
                                                (4096, 2048, 16, "f64", C0, C1), (4096, 2048, 20, "f32", 0.3, 0.1),
-                                               (4096, 2048, 16, "f64", 0.3, 0.1)])
+                                               (4096, 2048, 16, "f64", 0.3, 0.1),
+                                               # 4 MiB rows: entries run in descriptor-sized pieces
+                                               (1 << 20, 1024, 20, "f32", C0, C1)])
 def test_scaled_chunk_pass_bitwise_vs_one_launch(gpu, w, h, S, dtype, c0, c1):
     tdt = torch.float32 if dtype == "f32" else torch.float64
     g = core().TileGeom.aligned(w, h, S, S, tdt.itemsize)
