@@ -562,9 +562,13 @@ def main(argv=None) -> int:
             extras["window_phases"] = st.profile_window(args.steps)
         except Exception as e:  # noqa: BLE001 - diagnostic only
             extras["window_phases_error"] = str(e)[:200]
+    # The tiles go back to torch's cache, not to the driver: freeing GPU memory
+    # (hipFree, e.g. through torch.cuda.empty_cache) starts the driver's
+    # background wipe of the freed VRAM, and HBM reads run ~4.5% slower while it
+    # lasts (a dot over tensors that stay allocated: 7.09 -> 6.77 TB/s, back to
+    # 7.09 about 2 s later; scripts/exp/dot_free_state.py, profiles/r05_free_state).
+    # The extras below would be measured inside that window.
     del st
-    if gpu:
-        torch.cuda.empty_cache()
     if ctx.is_root:
         # The headline is measured; the extras below (dot, ping-pong, 8192^2 tiles)
         # run after it. Log it now on stderr so a failure in an extra cannot lose it.
@@ -578,8 +582,6 @@ def main(argv=None) -> int:
             extras["dot_error"] = str(e)[:200]
         _sync()
         ctx.barrier()
-        if gpu:
-            torch.cuda.empty_cache()
         if n == 1 and gpu and args.global_ == "32768x32768" and not args.no_sum_form:
             # The same 20-step window in the per-step form (bitwise equal to S
             # single steps, any coefficients), then at unequal coefficients in the
@@ -587,7 +589,6 @@ def main(argv=None) -> int:
             extras["stencil_32768sq_f32_per_step_gcells_per_s"] = round(
                 stencil_rate(ctx, 32768, 32768, "f32", args.steps, args.warmup, args.clock_warmup_ms / 1e3,
                              time_block=args.time_block, sum_form=False), 2)
-            torch.cuda.empty_cache()
             # Unequal coefficients (c_center 0.5, c_neighbor 0.125) in the scaled
             # form: the fast path for any 5-point Jacobi weights (c_neighbor != 0).
             extras["stencil_32768sq_f32_unequal_coeffs_gcells_per_s"] = round(
@@ -597,7 +598,6 @@ def main(argv=None) -> int:
 
             extras["stencil_unequal_coeffs"] = ("c_center 0.5, c_neighbor 0.125: scaled form (fma(k, u, n + s + w + e), "
                                                 "c_neighbor^S once per pass); kernel " + _hip().last_stencil_dispatch())
-            torch.cuda.empty_cache()
         if n == 1 and gpu and args.pingpong_loopback:
             pingpong_extras(ctx, extras, args.pingpong_max, loopback=True)
         elif n == 1 and gpu:
