@@ -120,9 +120,13 @@ StencilSolver<T>::StencilSolver(const CartTopology& topo, int rank, const TileGe
   constexpr int N = 16 / int(sizeof(T));
   fused_ = cfg_.fuse_periodic_self && all_self && cfg_.kind == StencilKind::Jacobi5 && tile_.width % N == 0 &&
            kernels::stencil5_periodic_supported<T>(tile_);
-  // Interior-first opening: RCCL with a wire transfer, the tuned kernel forms,
-  // every edge a neighbour's (time blocking), the thin-strip overlap off.
-  halo_last_allowed_ = cfg_.opening != Opening::Serial && cfg_.backend == HaloBackend::Rccl && !plan.sends.empty() &&
+  // Interior-first opening: a wire transfer (RCCL, or the IPC exchange, which
+  // runs the same pack / transfer / unpack steps on the stream, so ranks
+  // sharing one GPU run this schedule and its multi-rank decisions too), the
+  // tuned kernel forms, every edge a neighbour's (time blocking), the
+  // thin-strip overlap off.
+  const bool wire = cfg_.backend == HaloBackend::Rccl || cfg_.backend == HaloBackend::Ipc;
+  halo_last_allowed_ = cfg_.opening != Opening::Serial && wire && !plan.sends.empty() &&
                        !fused_ && cfg_.kind == StencilKind::Jacobi5 &&
                        cfg_.variant == kernels::StencilVariant::Auto && block_ > 1 && !cfg_.overlap;
   if (world_ > 1) {  // one rank without it (thin-strip overlap on a small tile) rules it out everywhere

@@ -118,6 +118,7 @@ def task_gpu_solver(args):
                         overlap=args.get("overlap", True), graph=args.get("graph", True),
                         time_block=args.get("time_block", 12), direct_halo=args.get("direct", None),
                         sum_form=args.get("sum_form", True), opening=args.get("opening", "auto"),
+                        steady=args.get("steady", "auto"),
                         min_gain=args.get("min_gain", 0.0), direct_engine=args.get("direct_engine", "kernel"),
                         c_center=args.get("c_center", 0.2), c_neighbor=args.get("c_neighbor", 0.2))
     st = Stencil2D(cfg, ctx)
@@ -135,7 +136,7 @@ def task_gpu_solver(args):
     if args.get("warm"):
         assert st.warm(args["warm"], 0.01) >= 1  # untimed, state-preserving passes (collective)
     phases = st.profile_window(args["profile"]) if args.get("profile") else None
-    per_run, openings = [], []
+    per_run, openings, halo_modes = [], [], []
     for n in args.get("runs", [args["iters"]]):
         if args.get("rank0_reads") and ctx.rank == 0:
             st.synchronize()
@@ -144,6 +145,7 @@ def task_gpu_solver(args):
         if st.solver is not None:
             per_run.append([int(st.solver.last_run_exchanges()), sum(c for _, c in st.solver.last_run_blocks())])
             openings.append(st.solver.last_run_opening())
+            halo_modes.append(st.halo_mode())
     st.synchronize()
     want_grid = args.get("return_grid", True)  # the same on every rank: gather_global is collective
     g = st.gather_global() if want_grid else None
@@ -155,6 +157,7 @@ def task_gpu_solver(args):
         out["halo_last"] = bool(st.solver.halo_last(st.time_block))
         out["exchanges"] = per_run  # halo exchanges each run() enqueued, and its super-steps
         out["openings"] = openings
+        out["halo_modes"] = halo_modes
         out["phases"] = phases
         out["direct_state"] = st.solver.direct_state()
         out["direct"] = bool(st.solver.direct_halo())
@@ -164,7 +167,14 @@ def task_gpu_solver(args):
             out["rccl_ranks"] = int(st.comm.count())
             out["rccl_device"] = int(st.comm.device())
     if ctx.rank == 0 and want_grid:
-        out["grid"] = g.double().tolist()
+        if args.get("digest"):  # large grids: a hash and the global max|u| instead of the list
+            import hashlib
+
+            a = g.contiguous().cpu()
+            out["digest"] = hashlib.sha256(a.numpy().tobytes()).hexdigest()
+            out["absmax"] = float(a.abs().max())
+        else:
+            out["grid"] = g.double().tolist()
     ctx.barrier()
     ctx.destroy()
     return out

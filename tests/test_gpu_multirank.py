@@ -136,6 +136,69 @@ def test_peers_exchange_once_per_super_step(gpu, time_block):
     assert (got - ref).abs().max().item() < 1e-5
 
 
+@pytest.mark.parametrize("n,dims,w,h,steady", [(2, "1x2", 8192, 1024, "serial"),
+                                               (2, "2x1", 4096, 2048, "interior-first"),
+                                               (4, "2x2", 8192, 2048, "interior-first"),
+                                               (4, "2x2", 8192, 2048, "auto")])
+def test_ipc_interior_first_bitwise_vs_serial(gpu, n, dims, w, h, steady):
+    """The interior-first schedule on the IPC exchange (ranks sharing one GPU;
+    4096 x 1024 tiles, so the chunk-list form exists): the inner chunks run on
+    the side stream while pack, put, wait and unpack run on main, then the
+    ghost-ring chunks. Only the order of the work changes, so the global field
+    is bitwise the serial schedule's (compared by digest); with steady =
+    interior-first every super-step of a call runs that way; steady = auto
+    (prepare() of a 3-super-step window) runs the steady decision over the
+    ranks, which all adopt the same schedule."""
+    runs = [20, 60, 13]
+    args = {"w": w, "h": h, "dims": dims, "iters": sum(runs), "runs": runs, "seed": 31, "time_block": 20,
+            "overlap": False, "direct": False, "digest": True}
+    extra = {"prepare": 60, "comm_timeout": 120} if steady == "auto" else {}
+    first = run_ranks("gpu_solver", n, dict(args, opening="interior-first", steady=steady, **extra), gpu=True)
+    serial = run_ranks("gpu_solver", n, dict(args, opening="serial", steady="serial"), gpu=True)
+    chosen = {r["choice"]["steady"] for r in first}
+    assert len(chosen) == 1, chosen
+    took = chosen.pop()
+    assert took == steady or (steady == "auto" and took in ("serial", "interior-first")), took
+    for r in first:
+        assert r["backend"] == "ipc" and r["halo_last"], (r["halo_modes"], r["choice"]["opening"])
+        assert r["choice"]["opening"] == "interior-first", r["choice"]
+        if steady == "auto":
+            assert f"over {n} rank(s)" in r["choice"]["steady_reason"], r["choice"]["steady_reason"]
+        assert all(ex == steps for ex, steps in r["exchanges"]), r["exchanges"]  # one exchange per super-step
+        assert "interior-first" in r["halo_modes"][1], r["halo_modes"]
+        assert ("every super-step interior-first" in r["halo_modes"][1]) == (took == "interior-first")
+    assert all(not r["halo_last"] for r in serial)
+    assert first[0]["digest"] == serial[0]["digest"]
+    assert 0.0 < first[0]["absmax"] <= 1.0  # a bounded operator on a field in [0, 1)
+
+
+@pytest.mark.parametrize("n,dims,w,h", [(4, "2x2", 8192, 2048), (8, "4x2", 8192, 4096)])
+def test_ipc_ranks_agree_on_measured_schedules(gpu, n, dims, w, h):
+    """opening = auto, steady = auto with 4 or 8 ranks (4096 x 1024 tiles; 4 x 2
+    is the 8-GPU grid) on the IPC exchange: prepare() runs the multi-rank
+    decisions the 8-GPU bench runs (per-round maxima over ranks through the
+    host allgather, the same samples on every rank), every rank adopts the same
+    opening and steady schedule, and the field is bitwise the serial schedule's
+    whatever they chose."""
+    runs = [40, 20]
+    args = {"w": w, "h": h, "dims": dims, "iters": sum(runs), "runs": runs, "seed": 37, "time_block": 20,
+            "overlap": False, "direct": False, "digest": True, "comm_timeout": 120}
+    res = run_ranks("gpu_solver", n, dict(args, prepare=40), gpu=True)
+    serial = run_ranks("gpu_solver", n, dict(args, opening="serial", steady="serial"), gpu=True)
+    choices = [(r["choice"]["opening"], r["choice"]["steady"]) for r in res]
+    assert len(set(choices)) == 1, choices
+    opening, steady = choices[0]
+    assert opening in ("serial", "interior-first") and steady in ("serial", "interior-first"), choices
+    for r in res:
+        assert "host allgather" in r["agreement"], r["agreement"]
+        assert f"{n} rank" in r["choice"]["reason"] or r["choice"]["reason"].startswith("no rank"), r["choice"]["reason"]
+        if opening == "interior-first":
+            assert f"over {n} rank(s)" in r["choice"]["steady_reason"], r["choice"]
+        assert all(ex == steps for ex, steps in r["exchanges"]), r["exchanges"]
+    assert res[0]["digest"] == serial[0]["digest"]
+    print(f"{n} ranks chose opening {opening}, steady {steady}: {res[0]['choice']['reason']}")
+
+
 @pytest.mark.parametrize("direct", [True, False])
 def test_ipc_warm_and_prepare_leave_the_state_alone(gpu, direct):
     """bench.py's prepare() + warm() on the IPC paths (device-initiated pushes and
