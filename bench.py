@@ -609,6 +609,12 @@ def main(argv=None) -> int:
             extras["stencil_8192sq_f64_1gpu_gcells_per_s"] = round(
                 stencil_rate(ctx, 8192, 8192, "f64", 480, 48, args.clock_warmup_ms / 1e3, time_block=args.time_block,
                              sum_form=not args.no_sum_form), 2)
+            # One rank on a tile sized for the card's 288 GB: 65536^2 fp32 (16 GiB per
+            # buffer; shares longer than a buffer descriptor run in pieces). 40 steps
+            # as two 20-step passes.
+            extras["stencil_65536sq_f32_1gpu_gcells_per_s"] = round(
+                stencil_rate(ctx, 65536, 65536, "f32", 40, 20, args.clock_warmup_ms / 1e3, time_block=args.time_block,
+                             sum_form=not args.no_sum_form), 2)
         else:
             pingpong_extras(ctx, extras, args.pingpong_max, args.pingpong_ipc)
             if gpu and n >= 2 and not args.pingpong_ipc and not args.no_pingpong_ipc:
