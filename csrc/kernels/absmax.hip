@@ -29,22 +29,56 @@ struct Bits<double> {
 };
 
 constexpr int kAbsBlock = 256;
+constexpr int kAbsUnroll = 8;  // 16-byte loads in flight per lane (8 KiB per wave), as in dot.hip
 
+template <typename U>
+__device__ __forceinline__ U umax(U a, U b) {
+  return a > b ? a : b;
+}
+
+// Streams x once at the HBM read rate: 16-byte non-temporal loads of the bit
+// patterns, kAbsUnroll per lane issued before any compare, over workgroup
+// chunks of kAbsBlock x kAbsUnroll vectors (grid-stride); the elements before
+// the first 16-byte boundary and after the last whole vector go scalar.
 template <typename T>
 __global__ __launch_bounds__(kAbsBlock) void absmax_kernel(const T* __restrict__ x, index_t n,
                                                            typename Bits<T>::type* out) {
   using U = typename Bits<T>::type;
+  constexpr int N = 16 / int(sizeof(T));
+  using V = U __attribute__((ext_vector_type(N)));
+  constexpr U kMag = ~U(0) >> 1;  // clears the sign bit
+  const index_t mis = index_t(reinterpret_cast<std::uintptr_t>(x) & 15) / index_t(sizeof(T));
+  const index_t head = mis ? (N - mis < n ? N - mis : n) : 0;
+  const index_t nvec = (n - head) / N;
+  const V* __restrict__ xv = reinterpret_cast<const V*>(x + head);
+  constexpr index_t kChunk = index_t(kAbsBlock) * kAbsUnroll;
+  const index_t stride = index_t(gridDim.x) * kChunk;
   U m = 0;
-  const index_t stride = index_t(gridDim.x) * kAbsBlock;
-  for (index_t i = index_t(blockIdx.x) * kAbsBlock + threadIdx.x; i < n; i += stride) {
-    const U b = abs_bits(x[i]);
-    m = b > m ? b : m;
+  index_t base = index_t(blockIdx.x) * kChunk + threadIdx.x;
+  for (; base + (kAbsUnroll - 1) * kAbsBlock < nvec; base += stride) {  // whole chunks: no bounds checks
+    V v[kAbsUnroll];
+#pragma unroll
+    for (int u = 0; u < kAbsUnroll; ++u) v[u] = __builtin_nontemporal_load(xv + base + u * kAbsBlock);
+#pragma unroll
+    for (int u = 0; u < kAbsUnroll; ++u)
+#pragma unroll
+      for (int k = 0; k < N; ++k) m = umax<U>(m, v[u][k] & kMag);
   }
 #pragma unroll
-  for (int off = kWaveSize / 2; off > 0; off >>= 1) {
-    const U o = __shfl_xor(m, off);
-    m = o > m ? o : m;
+  for (int u = 0; u < kAbsUnroll; ++u) {  // the one ragged chunk
+    const index_t i = base + u * kAbsBlock;
+    if (i < nvec) {
+      const V v = xv[i];
+#pragma unroll
+      for (int k = 0; k < N; ++k) m = umax<U>(m, v[k] & kMag);
+    }
   }
+  const index_t tid = index_t(blockIdx.x) * kAbsBlock + threadIdx.x;
+  const index_t nthreads = index_t(gridDim.x) * kAbsBlock;
+  for (index_t j = tid; j < head; j += nthreads) m = umax<U>(m, abs_bits(x[j]));
+  for (index_t j = head + nvec * N + tid; j < n; j += nthreads) m = umax<U>(m, abs_bits(x[j]));
+#pragma unroll
+  for (int off = kWaveSize / 2; off > 0; off >>= 1) m = umax<U>(m, __shfl_xor(m, off));
   __shared__ U part[kAbsBlock / kWaveSize];
   const int lane = threadIdx.x & (kWaveSize - 1), wave = threadIdx.x / kWaveSize;
   if (lane == 0) part[wave] = m;
@@ -52,7 +86,7 @@ __global__ __launch_bounds__(kAbsBlock) void absmax_kernel(const T* __restrict__
   if (threadIdx.x == 0) {
     U r = 0;
 #pragma unroll
-    for (int w = 0; w < kAbsBlock / kWaveSize; ++w) r = part[w] > r ? part[w] : r;
+    for (int w = 0; w < kAbsBlock / kWaveSize; ++w) r = umax<U>(r, part[w]);
     atomicMax(out, r);
   }
 }
@@ -89,8 +123,12 @@ void absmax(const T* x, index_t n, T* out, hipStream_t s) {
   U* o = reinterpret_cast<U*>(out);
   MXS_HIP_CHECK(hipMemsetAsync(o, 0, sizeof(U), s));
   if (n <= 0) return;
-  const index_t want = (n + kAbsBlock * 4 - 1) / (kAbsBlock * 4);
-  const int grid = int(std::min<index_t>(want, index_t(4) * device_cu_count()));
+  MXS_CHECK(reinterpret_cast<std::uintptr_t>(x) % sizeof(T) == 0, "absmax: input must be element-aligned");
+  // Two workgroups per CU (one stream of 16-byte loads, kAbsUnroll deep), fewer
+  // for small inputs.
+  const index_t per_block = index_t(kAbsBlock) * kAbsUnroll * (16 / index_t(sizeof(T)));
+  const index_t want = (n + per_block - 1) / per_block;
+  const int grid = int(std::max<index_t>(1, std::min<index_t>(want, index_t(2) * device_cu_count())));
   absmax_kernel<T><<<grid, kAbsBlock, 0, s>>>(x, n, o);
   MXS_HIP_CHECK_LAUNCH();
 }

@@ -174,6 +174,24 @@ def test_absmax_kernel(gpu):
     assert math.isnan(hip().absmax(y.data_ptr(), y.numel(), "f64"))
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("off,n", [(0, 1), (1, 2), (3, 5), (1, 4097), (2, 1_000_003), (0, 2_000_000), (3, 65536 * 9)])
+def test_absmax_vector_head_body_tail(gpu, dtype, off, n):
+    """The 16-byte vector body with a scalar head (start not 16-byte aligned)
+    and tail: the maximum is found wherever it sits (head, body, tail), equal
+    to torch's, for both widths."""
+    base = torch.randn(n + 8, device=gpu, dtype=dtype)
+    tag = "f32" if dtype == torch.float32 else "f64"
+    for where in sorted({0, n // 2, n - 1}):
+        x = base[off:off + n]  # a view: starts `off` elements past a 256-byte boundary
+        keep = x[where].item()
+        x[where] = -1e30
+        got = hip().absmax(x.data_ptr(), n, tag)
+        assert got == abs(x).max().item() and got == pytest.approx(1e30, rel=1e-6), (where, got)
+        x[where] = keep
+        assert hip().absmax(x.data_ptr(), n, tag) == abs(x).max().item()
+
+
 @pytest.mark.parametrize("w,h,steps,wrap,dtype", [
     (8192, 8192, 20, True, "f32"),     # BASELINE config 2: 9 groups x 8192 rows over 256 workgroups
     (16384, 2048, 20, False, "f32"),   # ghost-ring tile
