@@ -117,6 +117,10 @@ constexpr index_t kMinChunkRows = 64;
 // below (the pass is VALU-bound beyond S ~ 8, so a deeper block only pays
 // where the chunk / strip aprons are small against the tile).
 inline int auto_time_block(index_t w, index_t h, int elem_bytes = 4, bool sum_form = true) {
+  // Rows too wide for kMinChunkRows per descriptor-sized piece (beyond ~8.3 M
+  // fp32 columns; the padded pitch is at most w + 256): the fp32 pipelines
+  // cannot take them, the single-wave kernels can (their non-descriptor body).
+  if (elem_bytes == 4 && (w + 256) * 4 * kMinChunkRows > kMaxChunkBytes) return kMaxTimeBlock;
   if (elem_bytes == 4 && w >= 1024 && h >= 1024) {
     // The pipeline runs workgroups of 4 strips; with joint stage-1 windows a
     // group stores 912 columns at S = 20 (12 + 8) and 904 at S = 24 (12 + 12),

@@ -26,6 +26,8 @@ def _hip():
         (8192, 8192, "f64", True, 16),     # wide-lane pipeline 8 + 8
         (8192, 8192, "f64", False, 12),    # per-step 6 + 6
         (512, 512, "f32", True, 12),       # small tiles: single-wave kernels
+        (1 << 20, 1024, "f32", True, 24),  # 4 MiB rows: the pipelines walk shares in descriptor-sized pieces
+        (9_000_000, 64, "f32", True, 16),  # rows beyond ~8.3 M fp32 columns: no 64-row piece fits the descriptor
     ],
 )
 def test_auto_time_block(w, h, dtype, sum_form, expected):
