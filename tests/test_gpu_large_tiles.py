@@ -60,3 +60,28 @@ def test_wide_tile_pieces_bitwise_vs_one_period(gpu, dtype, S, fast, want):
     ref = jacobi_reference_global(u, S, C0, C1)
     err = (first - ref).abs().max().item()
     assert err <= (2e-6 if dtype == "f32" else 1e-14), err
+
+
+def test_rows_beyond_the_descriptor_take_the_single_wave_kernel(gpu):
+    """Rows of 36 MiB (9,437,184 fp32 columns): not even kMinChunkRows = 64 rows
+    fit one buffer descriptor. auto_time_block picks S = 16 there, which runs on
+    the balanced single-wave kernel's plain-store body (no descriptor), periodic
+    in x as above; an S = 20 pipeline pass is refused before any launch."""
+    P, h, S = 4096, 64, 16
+    w = 2304 * P
+    assert hip().auto_time_block(w, h, "f32", True) == 16
+    s = torch.cuda.current_stream().cuda_stream
+    g, a, u = _tile(w, h, S, torch.float32, P)
+    b = torch.zeros_like(a)
+    hip().stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, w, 0, h, C0, C1, True, "f32", s, "auto", False)
+    assert hip().last_stencil_dispatch() == "stream_balanced"
+    torch.cuda.synchronize()
+    wide = _core(b, g, w, h).reshape(h, w // P, P)
+    assert torch.equal(wide, wide[:, :1, :].expand_as(wide))
+    first = wide[:, 0, :].cpu().double()
+    with pytest.raises(Exception, match="rows of"):
+        hip().stencil5_tb(a.data_ptr(), b.data_ptr(), g, 20, 0, w, 0, h, C0, C1, True, "f32", s, "auto", False)
+    del a, b, wide
+    torch.cuda.empty_cache()
+    err = (first - jacobi_reference_global(u, S, C0, C1)).abs().max().item()
+    assert err <= 2e-6, err
