@@ -1091,6 +1091,7 @@ __global__ __launch_bounds__(kBlock) void stencil5_stream_balanced_kernel(
   // ROT stores go through one buffer descriptor per call: longer shares are
   // walked in pieces of at most kMaxChunkBytes (see stencil5_stream_pipe_kernel).
   const index_t max_rows = ROT ? kMaxChunkBytes / (pitch * index_t(sizeof(T))) : rows;
+  if (max_rows < 1) return;  // workgroup-uniform (rot_ok keeps such rows on the plain body)
 #pragma unroll 1
   while (a < b) {  // workgroup-uniform
     const index_t grp = a / rows, r0 = a - grp * rows;
@@ -1505,6 +1506,7 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
   // 65536^2 fp32 tile, 16 GiB per buffer) a share is walked in pieces, each
   // paying its own pipeline fill (the launcher checks >= 64 rows fit).
   const index_t max_rows = kMaxChunkBytes / (pitch * index_t(sizeof(T)));
+  if (max_rows < 1) return;  // workgroup-uniform, before any barrier (never launched so: the host checks)
 #pragma unroll 1
   while (a < b) {  // workgroup-uniform: all 8 waves take every chunk (barriers inside)
     const index_t grp = a / rows, r0 = a - grp * rows;
@@ -1544,6 +1546,7 @@ __global__ __launch_bounds__(2 * kWavesPerBlock * kWaveSize) void stencil5_pipe_
   const int strip = wave % G, stage = wave / G;
   const PassChunk* __restrict__ mine = table + index_t(blockIdx.x) * entries;
   const index_t max_rows = kMaxChunkBytes / (pitch * index_t(sizeof(T)));  // pieces, as in stencil5_stream_pipe_kernel
+  if (max_rows < 1) return;  // workgroup-uniform, before any barrier (chunk_pass_shape refuses such rows)
 #pragma unroll 1
   for (int e = 0; e < entries; ++e) {  // workgroup-uniform
     const PassChunk c = mine[e];
