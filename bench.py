@@ -529,6 +529,7 @@ def main(argv=None) -> int:
             extras["opening"] = st.solver.last_run_opening()
             # How the ranks agreed on the time block, the opening and the sum-form range.
             extras["agreement"] = st.solver.agreement_path()
+            extras["barrier_path"] = st.solver.barrier_path()
             if args.wire_delay_us:
                 extras["rehearsed_wire_delay_us"] = args.wire_delay_us
             if args.halo_max_ctas:

@@ -13,7 +13,9 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include <cmath>
 #include <cstdint>
+#include <limits>
 
 #include "mxs/grid/layout.hpp"
 #include "mxs/kernels/chunk_schedule.hpp"
@@ -51,6 +53,9 @@ struct Stencil5Coeffs {
   // + (center / neighbor) v per level, neighbor^S once per pass (9 instead of 11
   // slots). false = always the per-step form.
   bool sum_form = true;
+  // Bound on max|u| of a pass's input field (the solver passes its measured,
+  // agreed absmax), or < 0: unknown. See fast_form_safe().
+  double range = -1.0;
 };
 inline bool uses_sum_form(const Stencil5Coeffs& c) { return c.sum_form && c.center == c.neighbor; }
 // The scaled form (stencil_device.hpp): unequal coefficients, c_neighbor != 0,
@@ -58,6 +63,27 @@ inline bool uses_sum_form(const Stencil5Coeffs& c) { return c.sum_form && c.cent
 // wide pipeline (16); other depths and kernel forms run per step.
 inline bool uses_scaled_form(const Stencil5Coeffs& c) {
   return c.sum_form && c.center != c.neighbor && c.neighbor != 0.0;
+}
+// The kernel layer's guard of both fast forms for an S-level pass in element
+// type T (stencil5_tb and the chunk pass choose their form through it; the
+// solver's range guard is the measured, collective version of the same bounds,
+// and passes its bound in `range`):
+//   * |c_center| + 4 |c_neighbor| <= 1: the operator is bounded by the field;
+//   * c_neighbor^S is a normal number of T (it scales the stored result);
+//   * inside a pass the carried values grow by up to (4 + |k|)^S (k =
+//     c_center / c_neighbor; 5^S for the sum form): range (4 + |k|)^S < max/4.
+// With the range unknown (range < 0) only a form that grows no faster than the
+// sum form (|k| <= 1) is taken, under the sum form's documented contract
+// (max|u| 5^S < max/4 is the caller's); a faster-growing scaled form runs per
+// step (c_center 0.9, c_neighbor 0.013 grows as 73^S: 2e37 at S = 20).
+template <typename T>
+inline bool fast_form_safe(const Stencil5Coeffs& c, int S) {
+  if (!(uses_sum_form(c) || uses_scaled_form(c))) return false;
+  if (!(std::fabs(c.center) + 4.0 * std::fabs(c.neighbor) <= 1.0 + 1e-6)) return false;
+  if (!(std::fabs(double(T(std::pow(c.neighbor, double(S))))) >= double(std::numeric_limits<T>::min()))) return false;
+  const double k = std::fabs(c.center / c.neighbor);
+  if (c.range < 0.0) return k <= 1.0;
+  return std::isfinite(c.range) && c.range * std::pow(4.0 + k, double(S)) < double(std::numeric_limits<T>::max()) / 4.0;
 }
 
 enum class StencilVariant : int {
@@ -278,8 +304,13 @@ struct Copy2DBatch {
 // block: threads per workgroup (0 = 256). One-wave (64) workgroups are the
 // ones the hardware places beside a running pipeline workgroup (the
 // interior-first super-step's copies); 256 is faster alone.
+// kind: which kernel symbol the launch uses (same body): halo_pack_kernel,
+// halo_unpack_kernel or copy2d_batch_kernel, so kernel traces separate the
+// exchange's two sides.
+enum class CopyKind : int { Copy = 0, Pack = 1, Unpack = 2 };
 template <typename T>
-void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x = 0, int block = 0);
+void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x = 0, int block = 0,
+                  CopyKind kind = CopyKind::Copy);
 
 // ---------------------------------------------------------------- dot (K2-K8)
 enum class DotReduce : int {

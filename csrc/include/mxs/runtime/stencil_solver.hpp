@@ -312,12 +312,23 @@ class StencilSolver {
   }
 
   // How collective agreements travel: "host allgather", "rccl all-reduce" or
-  // "none (one rank)"; the device barrier before timed samples uses RCCL when
-  // a communicator exists.
+  // "none (one rank)". The device barrier before timed samples has its own
+  // path (barrier_path()).
   std::string agreement_path() const {
     if (world_ <= 1) return "none (one rank)";
     return cfg_.bootstrap ? "host allgather" : "rccl all-reduce";
   }
+  // The device barrier's path, decided collectively at the first barrier:
+  // "" (none yet), "none (one rank)", "rccl all-reduce", "host allgather (no
+  // RCCL communicator)" or "host allgather (fallback: ...)" when the RCCL
+  // barrier failed or timed out on some rank — then every rank falls back to
+  // the host allgather instead of failing prepare().
+  const std::string& barrier_path() const { return barrier_path_; }
+  // Tests: the device barrier's own communicator (default: the halo's), e.g. a
+  // one-rank loopback communicator per IPC rank sharing one GPU.
+  void set_barrier_comm(const RcclComm* c) { barrier_comm_ = c; }
+  // Fault injection: this rank's first RCCL barrier fails (the fallback's test).
+  void inject_barrier_failure(bool on) { inject_barrier_fail_ = on; }
   // Workgroups of the outer (ghost-ring) launch of the interior-first opening
   // at depth S (0: none built).
   int halo_last_outer_wgs(int S) const {
@@ -466,6 +477,7 @@ class StencilSolver {
   // all-reduce waited under the watchdog (tight release skew, so timed samples
   // start together), or the agreement path without a communicator.
   void device_barrier(const char* phase);
+  void rccl_barrier(const RcclComm* c, const char* phase);  // one all-reduce on c, drained (throws on failure)
   // Both streams drained, polled under the communication watchdog when
   // collectives may be in flight; failures name `phase`.
   void wait_idle(const char* phase);
@@ -504,9 +516,14 @@ class StencilSolver {
   bool direct_on_ = false;                    // super-steps use the direct push
   std::string direct_state_;
   double direct_ms_[2] = {0, 0};              // agreed medians: backend opening, direct opening
+  const RcclComm* barrier_comm_ = nullptr;   // set_barrier_comm (tests); default comm_
+  std::string barrier_path_;
+  bool barrier_rccl_ = false;
+  bool inject_barrier_fail_ = false;
   bool inject_mismatch_ = false;
   bool inject_skip_wait_ = false;
   DeviceBuffer<T> ref_;                       // validation snapshots: the field before, the backend's result
+  T* scratch_tiles(int n);                    // ref_ with room for n tiles (persistent; nullptr: no room)
   DeviceBuffer<unsigned> diff_;
   void validate_direct(int S);                // DirectHalo::Validate, collective (prepare)
   void poison_ghost(T* tile);                 // sentinel into every received ghost cell

@@ -73,8 +73,8 @@ __device__ __forceinline__ void copy_2d(index_t width, index_t height, Src&& src
 }
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_vgpr(32))) void copy2d_batch_kernel(
-    T* __restrict__ s0, T* __restrict__ s1, T* __restrict__ s2, Copy2DBatch b) {
+__device__ __forceinline__ void copy2d_batch_body(T* __restrict__ s0, T* __restrict__ s1, T* __restrict__ s2,
+                                                  const Copy2DBatch& b) {
   // Highest wave priority: in the interior-first opening the pack / unpack run
   // while the inner chunk launch still fills most CUs (a copy wave fits beside a
   // pipeline workgroup: 20 VGPRs), and the pass's VALU-bound waves, which
@@ -105,10 +105,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_vgpr(32))) void c
       [&](index_t x, index_t y) { return dst + y * op.dst_stride + x; });
 }
 
+// Three symbols over one body, so a kernel trace names the exchange's sides
+// (halo_pack_kernel / halo_unpack_kernel) apart from other batched copies.
+template <typename T>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_vgpr(32))) void halo_pack_kernel(
+    T* __restrict__ s0, T* __restrict__ s1, T* __restrict__ s2, Copy2DBatch b) {
+  copy2d_batch_body<T>(s0, s1, s2, b);
+}
+template <typename T>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_vgpr(32))) void halo_unpack_kernel(
+    T* __restrict__ s0, T* __restrict__ s1, T* __restrict__ s2, Copy2DBatch b) {
+  copy2d_batch_body<T>(s0, s1, s2, b);
+}
+template <typename T>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_vgpr(32))) void copy2d_batch_kernel(
+    T* __restrict__ s0, T* __restrict__ s1, T* __restrict__ s2, Copy2DBatch b) {
+  copy2d_batch_body<T>(s0, s1, s2, b);
+}
+
 }  // namespace
 
 template <typename T>
-void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x, int block_req) {
+void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x, int block_req,
+                  CopyKind kind) {
   if (b.n <= 0) return;
   MXS_CHECK(b.n <= kMaxCopies, "copy2d_batch: too many copies " << b.n);
   index_t biggest = 0;
@@ -130,15 +149,19 @@ void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_
   const index_t want = (biggest + block * kVec - 1) / (block * kVec);
   const index_t cap = std::max<index_t>(64, index_t(4 * kBlock / block) * device_cu_count() / b.n);
   const int gx = grid_x > 0 ? grid_x : int(std::min<index_t>(want, cap));
-  copy2d_batch_kernel<T><<<dim3(gx, b.n), block, 0, s>>>(slot0, slot1, slot2, b);
+  switch (kind) {
+    case CopyKind::Pack: halo_pack_kernel<T><<<dim3(gx, b.n), block, 0, s>>>(slot0, slot1, slot2, b); break;
+    case CopyKind::Unpack: halo_unpack_kernel<T><<<dim3(gx, b.n), block, 0, s>>>(slot0, slot1, slot2, b); break;
+    default: copy2d_batch_kernel<T><<<dim3(gx, b.n), block, 0, s>>>(slot0, slot1, slot2, b); break;
+  }
   MXS_HIP_CHECK_LAUNCH();
 }
 
-template void copy2d_batch<float>(float*, float*, float*, const Copy2DBatch&, hipStream_t, int, int);
-template void copy2d_batch<double>(double*, double*, double*, const Copy2DBatch&, hipStream_t, int, int);
-template void copy2d_batch<int>(int*, int*, int*, const Copy2DBatch&, hipStream_t, int, int);
+template void copy2d_batch<float>(float*, float*, float*, const Copy2DBatch&, hipStream_t, int, int, CopyKind);
+template void copy2d_batch<double>(double*, double*, double*, const Copy2DBatch&, hipStream_t, int, int, CopyKind);
+template void copy2d_batch<int>(int*, int*, int*, const Copy2DBatch&, hipStream_t, int, int, CopyKind);
 template void copy2d_batch<unsigned char>(unsigned char*, unsigned char*, unsigned char*, const Copy2DBatch&,
-                                          hipStream_t, int, int);
+                                          hipStream_t, int, int, CopyKind);
 
 }  // namespace kernels
 }  // namespace mxs

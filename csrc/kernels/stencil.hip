@@ -326,12 +326,10 @@ void stencil5_tb(const T* in, T* out, const TileGeom& g, int steps, index_t x0, 
               "stencil5_tb: row padding too small for the x apron");
   }
   const T c0 = T(c.center), c1 = T(c.neighbor);
-  // The scaled form needs c1^S in the normal range of T (it scales the stored result).
-  const bool scale_ok = std::fabs(double(T(std::pow(double(c1), double(steps))))) >= double(std::numeric_limits<T>::min());
-  const int form = v == StencilVariant::LdsTile ? 0
-                   : uses_sum_form(c)                ? 1
-                   : uses_scaled_form(c) && scale_ok ? 2
-                                                     : 0;
+  // Fast forms only inside their bounds (fast_form_safe: coefficients, c1^S
+  // normal, growth x the caller's range); else the per-step form.
+  const bool fast = v != StencilVariant::LdsTile && fast_form_safe<T>(c, steps);
+  const int form = !fast ? 0 : uses_sum_form(c) ? 1 : uses_scaled_form(c) ? 2 : 0;
   if (wrap) dispatch_tb<T, true>(steps, form, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   else dispatch_tb<T, false>(steps, form, in, out, g, x0, x1, y0, y1, c0, c1, v, s);
   MXS_HIP_CHECK_LAUNCH();

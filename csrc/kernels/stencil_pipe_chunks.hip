@@ -112,10 +112,10 @@ bool chunk_pass_shape(const TileGeom& g, int steps, const Stencil5Coeffs& c, Chu
   if (g.x_origin + g.halo_x < sa || g.pitch < g.x_origin + g.halo_x + (g.width + 3) / 4 * 4 + sa) return false;
   // Entries longer than kMaxChunkBytes run in pieces (stencil5_pipe_chunks_kernel).
   if (g.pitch * index_t(sizeof(T)) * kMinChunkRows > kMaxChunkBytes) return false;
-  // The scaled form scales the stored result by c_neighbor^S: it must be a normal number.
-  const bool scaled = uses_scaled_form(c) &&
-                      std::fabs(double(T(std::pow(c.neighbor, double(steps))))) >= double(std::numeric_limits<T>::min());
-  const bool sum = uses_sum_form(c) || scaled;  // both fast forms share the sum-form shape
+  // Fast forms only inside their bounds (kernels.hpp: fast_form_safe).
+  const bool fast = fast_form_safe<T>(c, steps);
+  const bool scaled = fast && uses_scaled_form(c);
+  const bool sum = fast;  // both fast forms share the sum-form shape
   ChunkPassShape sh;
   bool ok = false;
   if constexpr (sizeof(T) == 4) {

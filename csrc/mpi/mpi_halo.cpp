@@ -22,7 +22,7 @@ MpiStagedHalo<T>::MpiStagedHalo(const HaloPlan& plan, MPI_Comm comm, bool page_l
 
 template <typename T>
 void MpiStagedHalo<T>::exchange(T* tile, hipStream_t stream) {
-  kernels::copy2d_batch<T>(tile, dsend_.get(), drecv_.get(), progs_.pack, stream);
+  kernels::copy2d_batch<T>(tile, dsend_.get(), drecv_.get(), progs_.pack, stream, 0, 0, kernels::CopyKind::Pack);
   if (plan_.sends.empty()) return;
   MXS_HIP_CHECK(hipMemcpyAsync(hsend_, dsend_.get(), size_t(plan_.send_elems) * sizeof(T), hipMemcpyDeviceToHost,
                                stream));
@@ -36,7 +36,7 @@ void MpiStagedHalo<T>::exchange(T* tile, hipStream_t stream) {
   mpi_wait_all(req, "halo exchange (MPI staged)");
   MXS_HIP_CHECK(hipMemcpyAsync(drecv_.get(), hrecv_, size_t(plan_.recv_elems) * sizeof(T), hipMemcpyHostToDevice,
                                stream));
-  kernels::copy2d_batch<T>(tile, dsend_.get(), drecv_.get(), progs_.unpack, stream);
+  kernels::copy2d_batch<T>(tile, dsend_.get(), drecv_.get(), progs_.unpack, stream, 0, 0, kernels::CopyKind::Unpack);
 }
 
 template class MpiStagedHalo<float>;

@@ -204,12 +204,12 @@ PYBIND11_MODULE(_mxs_hip, m) {
   m.def(
       "stencil5_chunk_pass",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, double c0, double c1,
-         const std::string& dt, int outer_wgs, std::uintptr_t s, bool sum_form) -> py::object {
+         const std::string& dt, int outer_wgs, std::uintptr_t s, bool sum_form, double range) -> py::object {
         // One interior-first pass (tests / tuning): the inner and the outer
         // chunk lists of kernels::make_halo_last_schedule as two launches of the
         // chunk-list kernel on one stream. The tables live for the call, so the
         // launches are synchronised before return.
-        kernels::Stencil5Coeffs c{c0, c1, sum_form};
+        kernels::Stencil5Coeffs c{c0, c1, sum_form, range};
         auto run = [&](auto tag) -> py::object {
           using T = decltype(tag);
           kernels::ChunkPassShape sh;
@@ -248,17 +248,17 @@ PYBIND11_MODULE(_mxs_hip, m) {
       },
       py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("steps"), py::arg("c_center") = 0.2,
       py::arg("c_neighbor") = 0.2, py::arg("dtype") = "f32", py::arg("outer_wgs") = 0, py::arg("stream") = 0,
-      py::arg("sum_form") = true,
+      py::arg("sum_form") = true, py::arg("range") = -1.0,
       "one interior-first pass (inner + outer chunk lists) over the core of a ghost-ring tile (None: no "
-      "chunk-list form for this depth)");
+      "chunk-list form for this depth); sum_form / range as for stencil5_tb");
   m.def("last_pipe_lag1", &kernels::last_pipe_lag1,
         "whether the most recent stencil launch was a pipeline pass in ascending level order");
   m.def(
       "stencil5_tb",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, index_t x0, index_t x1, index_t y0,
          index_t y1, double c0, double c1, bool wrap, const std::string& dt, std::uintptr_t s,
-         const std::string& variant, bool sum_form) {
-        kernels::Stencil5Coeffs c{c0, c1, sum_form};
+         const std::string& variant, bool sum_form, double range) {
+        kernels::Stencil5Coeffs c{c0, c1, sum_form, range};
         const kernels::StencilVariant v = parse_variant(variant);
         if (parse_dtype(dt) == DType::F32)
           kernels::stencil5_tb<float>(ptr<float>(in), ptr<float>(out), g, steps, x0, x1, y0, y1, c, wrap, strm(s), v);
@@ -269,7 +269,12 @@ PYBIND11_MODULE(_mxs_hip, m) {
       py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("steps"), py::arg("x0"), py::arg("x1"), py::arg("y0"),
       py::arg("y1"), py::arg("c_center") = 0.2, py::arg("c_neighbor") = 0.2, py::arg("wrap") = false,
       py::arg("dtype") = "f32", py::arg("stream") = 0, py::arg("variant") = "auto", py::arg("sum_form") = true,
-      "S Jacobi steps over [x0, x1) x [y0, y1); sum_form: allow the sum form when c_center == c_neighbor");
+      py::arg("range") = -1.0,
+      "S Jacobi steps over [x0, x1) x [y0, y1). sum_form: allow the fast forms — the sum form (c_center == "
+      "c_neighbor) or the scaled form (unequal, c_neighbor != 0) — within their bounds (kernels::fast_form_safe: "
+      "|c_center| + 4 |c_neighbor| <= 1, c_neighbor^S normal, range (4 + |c_center / c_neighbor|)^S < max / 4). "
+      "range: a bound on max|u| of the input (< 0: unknown; then only forms growing no faster than the sum form "
+      "run fast, under its contract max|u| 5^S < max / 4); otherwise the per-step form");
   m.def(
       "streams_concurrent",
       [](std::uintptr_t a, std::uintptr_t b) { return kernels::streams_concurrent(strm(a), strm(b)); },
@@ -547,6 +552,18 @@ PYBIND11_MODULE(_mxs_hip, m) {
           py::arg("on") = true, "fault injection: the validation's direct schedule skips its first wait on this rank")
       .def("agreement_path", [](SolverHandle& h) { return h.visit([](auto& s) { return s.agreement_path(); }); },
            "how collective agreements travel: host allgather, rccl all-reduce or none (one rank)")
+      .def("barrier_path", [](SolverHandle& h) { return h.visit([](auto& s) { return s.barrier_path(); }); },
+           "the device barrier's path ('' before the first barrier): rccl all-reduce, host allgather (...), "
+           "or the host allgather as the agreed fallback after an RCCL barrier failed on some rank")
+      .def(
+          "set_barrier_comm",
+          [](SolverHandle& h, const RcclComm* c) { h.visit([c](auto& s) { s.set_barrier_comm(c); }); },
+          py::arg("comm"), py::keep_alive<1, 2>(),
+          "tests: the device barrier's own RCCL communicator (default: the halo's)")
+      .def(
+          "inject_barrier_failure",
+          [](SolverHandle& h, bool on) { h.visit([on](auto& s) { s.inject_barrier_failure(on); }); },
+          py::arg("on") = true, "fault injection: this rank's RCCL barrier probe fails (tests of the fallback)")
       .def("wire_delay_us", [](SolverHandle& h) { return h.visit([](auto& s) { return s.wire_delay_us(); }); },
            "rehearsal wire time added after each RCCL transfer (us)")
       .def("halo_max_ctas", [](SolverHandle& h) { return h.visit([](auto& s) { return s.halo_max_ctas(); }); },

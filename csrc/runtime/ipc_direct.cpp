@@ -48,8 +48,10 @@ __device__ __forceinline__ void store_sys4(void* p, unsigned v) {
   asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
 }
 
-__device__ __forceinline__ u64 ld_acquire_sys(const u64* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+// Relaxed system-scope polls, one acquire fence after the loop (see
+// ipc_transport.cpp: an acquire load per poll invalidates the XCD's L2 each time).
+__device__ __forceinline__ u64 ld_relaxed_sys(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // gridDim.y = band; 16-byte vectors when the band's rows allow it (the
@@ -122,7 +124,7 @@ __global__ void wait_kernel(FlagSet f, const u64* epoch, u64* status, u64 timeou
   const u64 e = *epoch;
   if (int(threadIdx.x) < f.n) {
     const u64 t0 = wall_clock64();
-    while (ld_acquire_sys(f.flag[threadIdx.x]) < e) {
+    while (ld_relaxed_sys(f.flag[threadIdx.x]) < e) {
       if (wall_clock64() - t0 > timeout_ticks) {
         atomicCAS(status, 0ull, 1ull);
         break;

@@ -47,8 +47,12 @@ struct CtrlLayout {
   size_t words() const { return size_t(2 * world + 2 + kMaxMsgs); }
 };
 
-__device__ __forceinline__ u64 ld_acquire_sys(const u64* p) {
-  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+// Polls read the flag with a relaxed system-scope load (it bypasses the
+// non-coherent caches, so a peer's store is seen); the acquire is ONE fence
+// after the loop. An acquire load per poll would also invalidate this XCD's L2
+// on every iteration, while the inner chunk launch runs beside the wait.
+__device__ __forceinline__ u64 ld_relaxed_sys(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <typename T>
@@ -69,7 +73,7 @@ __device__ __forceinline__ void store_sys<double>(double* p, double v) {
 // Spin (thread 0) until *p >= target; false (and status set) on deadline.
 __device__ bool spin_ge(const u64* p, u64 target, u64 timeout_ticks, u64* status, u64 code) {
   const u64 t0 = wall_clock64();
-  while (ld_acquire_sys(p) < target) {
+  while (ld_relaxed_sys(p) < target) {
     if (wall_clock64() - t0 > timeout_ticks) {
       atomicCAS(status, 0ull, code);
       return false;
@@ -116,6 +120,8 @@ __global__ void ipc_free_wait_kernel(const PutDesc<T>* __restrict__ descs, int n
                                      u64 timeout_ticks) {
   const u64 k = *epoch + 1;
   if (int(threadIdx.x) < n) spin_ge(descs[threadIdx.x].local_free, k - 1, timeout_ticks, status, 1);
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the puts that follow come after the observation
 }
 
 // kWaitWgs workgroups, dealt round-robin over the 8 XCDs: each observes the

@@ -23,6 +23,7 @@
 #include <utility>
 #include <vector>
 
+#include "mxs/core/fault.hpp"
 #include "mxs/core/trace.hpp"
 #include "mxs/runtime/decision.hpp"
 
@@ -68,13 +69,68 @@ void StencilSolver<T>::agree_max(std::vector<double>& v, const char* phase) {
   wait_idle(phase);
 }
 
+// One all-reduce of a double on c, drained under the watchdog of c (throws on
+// an RCCL error or a timeout, which also aborts c).
+template <typename T>
+void StencilSolver<T>::rccl_barrier(const RcclComm* c, const char* phase) {
+  if (agree_buf_.size() < 1) agree_buf_.reset(1);
+  c->allreduce_max<double>(agree_buf_.get(), agree_buf_.get(), 1, main_.get());
+  if (comm_timeout() > 0) {
+    const hipStream_t both[2] = {main_.get(), side_.get()};
+    c->wait_all(both, 2, phase);
+  } else {
+    main_.spin_sync();
+    side_.spin_sync();
+  }
+  side_pending_ = false;
+}
+
+// The release in front of every timed sample. A device all-reduce releases
+// every rank within microseconds of each other; the host allgather is the
+// fallback. The path is decided once, collectively, at the first barrier: each
+// rank tries the RCCL barrier (bounded by the comm watchdog), the ranks agree
+// through the host allgather on whether it worked everywhere, and a failure on
+// any rank moves every rank to the host allgather (extras.barrier_path) rather
+// than failing prepare() and the headline with it. Without a host allgather
+// there is nothing to fall back on: the RCCL barrier's errors propagate.
 template <typename T>
 void StencilSolver<T>::device_barrier(const char* phase) {
-  if (world_ <= 1) return;
-  if (comm_) {  // a device all-reduce releases every rank within microseconds of each other
-    if (agree_buf_.size() < 1) agree_buf_.reset(1);
-    comm_->allreduce_max<double>(agree_buf_.get(), agree_buf_.get(), 1, main_.get());
-    wait_idle(phase);
+  if (world_ <= 1) {
+    if (barrier_path_.empty()) barrier_path_ = "none (one rank)";
+    return;
+  }
+  const RcclComm* bc = barrier_comm_ ? barrier_comm_ : comm_;
+  if (barrier_path_.empty()) {
+    if (!bc) {
+      barrier_path_ = "host allgather (no RCCL communicator)";
+    } else if (!cfg_.bootstrap) {
+      barrier_rccl_ = true;
+      barrier_path_ = "rccl all-reduce";
+    } else {
+      std::string why;
+      try {
+        if (inject_barrier_fail_) throw Error("injected RCCL barrier failure (fault injection)");
+        if (bc->aborted()) throw Error("the communicator was aborted");
+        rccl_barrier(bc, phase);
+      } catch (const std::exception& e) {
+        why = e.what();
+      }
+      std::vector<double> failed{why.empty() ? 0.0 : 1.0};
+      agree_max(failed, "device barrier agreement");  // host allgather (bootstrap)
+      barrier_rccl_ = failed[0] == 0.0;
+      if (barrier_rccl_) barrier_path_ = "rccl all-reduce";
+      else
+        barrier_path_ = "host allgather (fallback: the RCCL barrier failed on " +
+                        std::string(why.empty() ? "another rank" : "this rank: " + why) + ")";
+      if (!barrier_rccl_ && !why.empty()) {
+        std::fprintf(stderr, "[device barrier] %s\n", barrier_path_.c_str());
+        std::fflush(stderr);
+      }
+      return;  // the probe (or the agreement) was this barrier
+    }
+  }
+  if (barrier_rccl_) {
+    rccl_barrier(bc, phase);
     return;
   }
   std::vector<double> v{0.0};
@@ -253,6 +309,24 @@ void StencilSolver<T>::choose_opening(int S) {
   opening_reason_ = buf;
 }
 
+// The persistent snapshot scratch (ref_): n whole tiles (ghost rings included),
+// allocated once at the size every prepare()-time user will need — two tiles
+// when the direct halo still awaits validation, else n — and never freed before
+// the solver is. nullptr when the device has no room (the callers decide).
+template <typename T>
+T* StencilSolver<T>::scratch_tiles(int n) {
+  const index_t elems = tile_.alloc_elems();
+  const int want = std::max(n, direct_ && direct_state_ == "pending validation" ? 2 : 1);
+  if (ref_.size() >= index_t(n) * elems) return ref_.get();
+  try {
+    ref_.reset(index_t(want) * elems);
+  } catch (const std::exception&) {
+    (void)hipGetLastError();  // clear the failed allocation's sticky error
+    return nullptr;
+  }
+  return ref_.get();
+}
+
 // SolverConfig::steady Auto, once (the first prepare() of a call with two or
 // more super-steps, after the opening chose interior-first): two back-to-back
 // super-steps from drained streams after a device barrier, the second one
@@ -272,9 +346,21 @@ void StencilSolver<T>::choose_steady(int S) {
   hipStream_t m = main_.get();
   join_side();
   wait_idle("prepare: steady timing");
+  // The snapshot goes into the solver's persistent scratch (ref_, shared with
+  // validate_direct and sized for both when that runs too): nothing is freed
+  // between construction and a timed window, so no VRAM wipe runs under it
+  // (profiles/r05_free_state). A rank that cannot allocate it keeps serial, and
+  // so does every other rank (agreed).
   const size_t bytes = size_t(tile_.alloc_elems()) * sizeof(T);
-  DeviceBuffer<T> snap(tile_.alloc_elems());
-  MXS_HIP_CHECK(hipMemcpyAsync(snap.get(), cur_, bytes, hipMemcpyDeviceToDevice, m));
+  T* const snap = scratch_tiles(1);
+  std::vector<double> no_room{snap ? 0.0 : 1.0};
+  agree_max(no_room, "prepare: steady agreement");
+  if (no_room[0] != 0.0) {
+    steady_choice_ = "serial";
+    steady_reason_ = "no room for the steady decision's field snapshot on some rank: serial kept";
+    return;
+  }
+  MXS_HIP_CHECK(hipMemcpyAsync(snap, cur_, bytes, hipMemcpyDeviceToDevice, m));
   T* const a = cur_;
   T* const b = nxt_;
   auto first = [&] {  // the call's interior-first opening, a -> b
@@ -307,7 +393,7 @@ void StencilSolver<T>::choose_steady(int S) {
   constexpr int nr = 20;
   const RoundDecision d = paired_rounds(nr, {sample(false), sample(true)}, {true, true}, "prepare: steady agreement");
   join_side();
-  MXS_HIP_CHECK(hipMemcpyAsync(cur_, snap.get(), bytes, hipMemcpyDeviceToDevice, m));
+  MXS_HIP_CHECK(hipMemcpyAsync(cur_, snap, bytes, hipMemcpyDeviceToDevice, m));
   wait_idle("prepare: steady timing");
   ghost_fresh_ = false;
   steady_on_ = d.win;
@@ -376,10 +462,10 @@ void StencilSolver<T>::validate_direct(int S) {
   constexpr int kSteps = 3;
   const index_t elems = tile_.alloc_elems();
   const size_t bytes = size_t(elems) * sizeof(T);
-  if (!ref_.get()) ref_.reset(2 * elems);
+  T* const before = scratch_tiles(2);
+  MXS_CHECK(before != nullptr, "direct halo validation: cannot allocate two tile snapshots");
   if (!diff_.get()) diff_.reset(1);
-  T* const before = ref_.get();
-  T* const want = ref_.get() + elems;
+  T* const want = before + elems;
   const index_t w = tile_.width, h = tile_.height;
   MXS_HIP_CHECK(hipMemcpyAsync(before, cur_, bytes, hipMemcpyDeviceToDevice, m));
   T* a = cur_;
@@ -597,8 +683,10 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
 #define MXS_MEASURE_INSTANTIATE(T)                                                                            \
   template void StencilSolver<T>::agree_max(std::vector<double>&, const char*);                              \
   template void StencilSolver<T>::device_barrier(const char*);                                               \
+  template void StencilSolver<T>::rccl_barrier(const RcclComm*, const char*);                                \
   template void StencilSolver<T>::choose_opening(int);                                                       \
   template void StencilSolver<T>::choose_steady(int);                                                        \
+  template T* StencilSolver<T>::scratch_tiles(int);                                                          \
   template RoundDecision StencilSolver<T>::paired_rounds(int, const std::vector<std::function<double()>>&,   \
                                                          const std::vector<bool>&, const char*,              \
                                                          std::vector<double>*);                              \

@@ -498,6 +498,9 @@ void StencilSolver<T>::ensure_range(bool collective) {
   }
   const double bound = double(std::numeric_limits<T>::max()) / 4.0 / std::pow(fast_growth_, double(block_));
   const bool ok = std::isfinite(md) && md < bound && (agreed || cfg_.coeffs.sum_form);
+  // The kernels re-check the same bound per pass (kernels::fast_form_safe):
+  // whenever `ok` holds here it holds there (S <= block_).
+  cfg_.coeffs.range = md;
   if (ok == cfg_.coeffs.sum_form) return;
   cfg_.coeffs.sum_form = ok;
   sum_note_ = ok ? "" : "fast form off: max|u| * (4 + |c_center / c_neighbor|)^S would overflow the element type (per-step form)";

@@ -126,6 +126,14 @@ def task_gpu_solver(args):
         st.solver.inject_direct_mismatch(True)
     if args.get("skip_wait_rank") == ctx.rank:
         st.solver.inject_direct_skip_wait(True)
+    barrier_comm = None
+    if args.get("barrier_loopback"):  # a one-rank RCCL communicator per rank, for the device barrier only
+        from cuda_mpi_scratch_amd import hip
+
+        barrier_comm = hip().RcclComm(hip().RcclComm.make_unique_id(), 1, 0)
+        st.solver.set_barrier_comm(barrier_comm)
+    if args.get("barrier_fail_rank") == ctx.rank:
+        st.solver.inject_barrier_failure(True)
     stall = args.get("stall")
     if stall and ctx.rank == stall["rank"]:
         st.solver.inject_stall(stall["phase"], float(stall["seconds"]))
@@ -154,6 +162,7 @@ def task_gpu_solver(args):
     if st.solver is not None:
         out["choice"] = dict(st.solver.schedule_times())
         out["agreement"] = st.solver.agreement_path()
+        out["barrier_path"] = st.solver.barrier_path()
         out["halo_last"] = bool(st.solver.halo_last(st.time_block))
         out["exchanges"] = per_run  # halo exchanges each run() enqueued, and its super-steps
         out["openings"] = openings

@@ -49,7 +49,7 @@ def test_wide_tile_pieces_bitwise_vs_one_period(gpu, dtype, S, fast, want):
     g, a, u = _tile(w, h, S, tdt, P)
     assert g.pitch * tdt.itemsize * 600 > 0x7F000000  # shares really are split
     b = torch.zeros_like(a)
-    hip().stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, w, 0, h, C0, C1, True, dtype, s, "auto", fast)
+    hip().stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, w, 0, h, C0, C1, True, dtype, s, "auto", fast, range=1.0)
     assert hip().last_stencil_dispatch() == want
     torch.cuda.synchronize()
     wide = _core(b, g, w, h).reshape(h, w // P, P)

@@ -199,6 +199,34 @@ def test_ipc_ranks_agree_on_measured_schedules(gpu, n, dims, w, h):
     print(f"{n} ranks chose opening {opening}, steady {steady}: {res[0]['choice']['reason']}")
 
 
+@pytest.mark.parametrize("fail_rank", [None, 2])
+def test_device_barrier_falls_back_to_the_host_allgather(gpu, fail_rank):
+    """The device barrier in front of every timed decision sample (VERDICT r05
+    item 5). Four IPC ranks sharing the GPU, each given a one-rank RCCL
+    loopback communicator for the barrier only (RCCL refuses two ranks of one
+    communicator on one GPU). The first barrier probes RCCL on every rank and
+    the ranks agree through the host allgather: all good -> "rccl all-reduce"
+    everywhere; one rank's barrier failing (fault injection) -> every rank
+    takes the host allgather, prepare() completes, the decisions still agree,
+    and the field is bitwise the serial schedule's."""
+    runs = [20]
+    args = {"w": 8192, "h": 2048, "dims": "2x2", "iters": sum(runs), "runs": runs, "seed": 41, "time_block": 20,
+            "overlap": False, "direct": False, "digest": True, "comm_timeout": 60}
+    res = run_ranks("gpu_solver", 4, dict(args, prepare=20, barrier_loopback=True, barrier_fail_rank=fail_rank),
+                    gpu=True)
+    paths = [r["barrier_path"] for r in res]
+    if fail_rank is None:
+        assert paths == ["rccl all-reduce"] * 4, paths
+    else:
+        assert all(p.startswith("host allgather (fallback: the RCCL barrier failed on") for p in paths), paths
+        assert "injected RCCL barrier failure" in paths[fail_rank], paths
+        assert all("another rank" in p for i, p in enumerate(paths) if i != fail_rank), paths
+    assert len({r["choice"]["opening"] for r in res}) == 1, [r["choice"] for r in res]
+    assert all(r["choice"]["opening"] in ("serial", "interior-first") for r in res)
+    serial = run_ranks("gpu_solver", 4, dict(args, opening="serial", steady="serial"), gpu=True)
+    assert res[0]["digest"] == serial[0]["digest"]
+
+
 @pytest.mark.parametrize("direct", [True, False])
 def test_ipc_warm_and_prepare_leave_the_state_alone(gpu, direct):
     """bench.py's prepare() + warm() on the IPC paths (device-initiated pushes and

@@ -46,7 +46,7 @@ def test_scaled_pass_matches_reference(gpu, dtype, S, want):
     g, a, u = _periodic(w, h, S, tdt, seed=S)
     b = torch.zeros_like(a)
     s = torch.cuda.current_stream().cuda_stream
-    hip().stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, w, 0, h, C0, C1, True, dtype, s, "auto", True)
+    hip().stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, w, 0, h, C0, C1, True, dtype, s, "auto", True, range=1.0)
     assert hip().last_stencil_dispatch() == want
     torch.cuda.synchronize()
     ref = jacobi_reference_global(u, S, C0, C1)
@@ -67,7 +67,7 @@ def test_scaled_pass_other_weights(gpu, c0, c1):
     g, a, u = _periodic(w, h, S, torch.float32, seed=5)
     b = torch.zeros_like(a)
     s = torch.cuda.current_stream().cuda_stream
-    hip().stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, w, 0, h, c0, c1, True, "f32", s, "auto", True)
+    hip().stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, w, 0, h, c0, c1, True, "f32", s, "auto", True, range=1.0)
     assert hip().last_stencil_dispatch() == "stream_pipe_scaled"
     torch.cuda.synchronize()
     err = (_core(b, g, w, h) - jacobi_reference_global(u, S, c0, c1)).abs().max().item()
@@ -87,9 +87,9 @@ def test_scaled_chunk_pass_bitwise_vs_one_launch(gpu, w, h, S, dtype, c0, c1):
     ref = torch.full_like(src, -3.0)
     got = torch.full_like(src, -3.0)
     s = torch.cuda.current_stream().cuda_stream
-    hip().stencil5_tb(src.data_ptr(), ref.data_ptr(), g, S, 0, w, 0, h, c0, c1, False, dtype, s, "auto", True)
+    hip().stencil5_tb(src.data_ptr(), ref.data_ptr(), g, S, 0, w, 0, h, c0, c1, False, dtype, s, "auto", True, range=1.0)
     assert hip().last_stencil_dispatch() == "stream_pipe_scaled"
-    d = hip().stencil5_chunk_pass(src.data_ptr(), got.data_ptr(), g, S, c0, c1, dtype, 0, s, True)
+    d = hip().stencil5_chunk_pass(src.data_ptr(), got.data_ptr(), g, S, c0, c1, dtype, 0, s, True, range=1.0)
     assert d is not None and d["check"] == ""
     assert hip().last_stencil_dispatch() == "stream_pipe_scaled_chunks"
     torch.cuda.synchronize()
@@ -118,3 +118,36 @@ def test_solver_unequal_coefficients_interior_first_bitwise_vs_serial(gpu):
     # A coefficient pair whose operator grows with the field keeps the per-step form.
     c = Stencil2D(StencilConfig(**{**kw, "c_center": 0.6, "c_neighbor": 0.2}))
     assert not c.sum_form_active and "fast form off" in c.solver.sum_form_note()
+
+
+@pytest.mark.parametrize("rng,scale,want", [(None, 1.0, "stream_pipe"), (1.0, 1.0, "stream_pipe_scaled"),
+                                            (17.0, 17.0, "stream_pipe")])
+def test_scaled_form_kernel_layer_guard(gpu, rng, scale, want):
+    """The kernels' own guard (kernels::fast_form_safe; ADVICE r05): c_center 0.9,
+    c_neighbor 0.013 is a bounded operator (0.952) whose scaled-form sums grow as
+    73.2^S = 1.9e37 at S = 20. With the input's range unknown the direct call
+    runs per step; with max|u| <= 1 declared it runs the scaled form; with
+    max|u| = 17 declared (17 x 1.9e37 > FLT_MAX / 4) per step again. Every
+    result is finite and within fp32 rounding of the fp64 reference, and each
+    per-step result is bitwise the sum_form=False pass."""
+    c0, c1 = 0.9, 0.013
+    w, h, S = 2048, 1024, 20
+    g, a, u = _periodic(w, h, S, torch.float32, seed=11)
+    if scale != 1.0:
+        a.mul_(scale)
+        u = u * scale
+    b = torch.zeros_like(a)
+    s = torch.cuda.current_stream().cuda_stream
+    kw = {} if rng is None else {"range": rng}
+    hip().stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, w, 0, h, c0, c1, True, "f32", s, "auto", True, **kw)
+    assert hip().last_stencil_dispatch() == want
+    torch.cuda.synchronize()
+    got = _core(b, g, w, h)
+    assert torch.isfinite(got).all()
+    ref = jacobi_reference_global(u, S, c0, c1)
+    assert (got - ref).abs().max().item() <= 2e-6 * scale
+    if want == "stream_pipe":
+        p = torch.zeros_like(a)
+        hip().stencil5_tb(a.data_ptr(), p.data_ptr(), g, S, 0, w, 0, h, c0, c1, True, "f32", s, "auto", False)
+        torch.cuda.synchronize()
+        assert torch.equal(p, b)
