@@ -567,7 +567,7 @@ def main(argv=None) -> int:
     # (hipFree, e.g. through torch.cuda.empty_cache) starts the driver's
     # background wipe of the freed VRAM, and HBM reads run ~4.5% slower while it
     # lasts (a dot over tensors that stay allocated: 7.09 -> 6.77 TB/s, back to
-    # 7.09 about 2 s later; scripts/exp/dot_free_state.py, profiles/r05_free_state).
+    # 7.09 about 2 s later; profiles/r05_free_state).
     # The extras below would be measured inside that window.
     del st
     if ctx.is_root:

@@ -66,6 +66,142 @@ __global__ __launch_bounds__(256) void balanced_stamped(const float* __restrict_
   }
 }
 
+
+// The production pipeline pass (joint windows, sum form) with per-workgroup
+// clock stamps at entry and exit (TUNE_FOCUS=fillfit): the shader cycles each
+// workgroup spends on its share, against the share's rows, fitted to
+// cycles = fixed + per_row x rows over several tile heights (the fill per
+// share is the fixed part). stamps[6 b ..]: realtime in / out, s_memtime in /
+// out, share rows, chunks.
+template <int S0, int S1, int PF, bool WRAP, int LAG1>
+__global__ __launch_bounds__(2 * kWavesPerBlock * kWaveSize) void pipe_stamped(
+    const float* __restrict__ in, float* __restrict__ out, index_t pitch, index_t core_off, index_t W, index_t H,
+    index_t x_begin, index_t x_end, index_t y_begin, index_t y_end, const PipeShares shares, float c0, float c1,
+    unsigned long long* stamps) {
+  const unsigned long long r0 = __builtin_amdgcn_s_memrealtime(), t0 = __builtin_amdgcn_s_memtime();
+  constexpr int G = kWavesPerBlock;
+  using P = PipeShape<S0, S1, PF>;
+  using B = BodySumF32;
+  constexpr int OWG = JointShape<S0, S1, G>::OWG;
+  __shared__ B::V ring[G * P::RING * kWaveSize];
+  const index_t rows = y_end - y_begin;
+  const int wave = threadIdx.x / kWaveSize;
+  const int strip = wave % G, stage = wave / G;
+  index_t a = shares.start[blockIdx.x], b = shares.start[blockIdx.x + 1];
+  const index_t share_rows = b - a;
+  int chunks = 0;
+#pragma unroll 1
+  while (a < b) {
+    const index_t grp = a / rows, q0 = a - grp * rows;
+    const index_t q1 = rows < q0 + (b - a) ? rows : q0 + (b - a);
+    pipe_chunk<B, S0, S1, PF, WRAP, true, G, LAG1>(in, out, pitch, core_off, W, H, x_begin + grp * OWG, x_end,
+                                                   y_begin + q0, y_begin + q1, c0, c1, ring, stage, strip);
+    a += q1 - q0;
+    ++chunks;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long* p = stamps + size_t(blockIdx.x) * 6;
+    p[0] = r0;
+    p[1] = __builtin_amdgcn_s_memrealtime();
+    p[2] = t0;
+    p[3] = __builtin_amdgcn_s_memtime();
+    p[4] = (unsigned long long)share_rows;
+    p[5] = (unsigned long long)chunks | ((unsigned long long)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 16) |
+           ((unsigned long long)__builtin_amdgcn_s_getreg(4 | (31 << 11)) << 32);  // XCC_ID, HW_ID
+  }
+}
+
+// TUNE_FOCUS=fillfit: one pipeline form over rows [0, h) of the ghost-ring
+// tile for several h, `reps` stamped passes each; per h the median over passes
+// of the median / max workgroup cycles and of the pass's span.
+template <int S0, int S1, int PF, int LAG1>
+void fillfit(const char* name, const float* in, float* out, const TileGeom& g, const std::vector<index_t>& heights,
+             int reps) {
+  constexpr int OWG = JointShape<S0, S1, kWavesPerBlock>::OWG;
+  int cus = 0;
+  MXS_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const int blocks = cus;  // one 512-thread workgroup per CU (VGPR-bound)
+  DeviceBuffer<unsigned long long> st(index_t(blocks) * 6);
+  std::vector<unsigned long long> h(size_t(blocks) * 6);
+  const float c0 = float(std::pow(0.2, S0 + S1));
+  const index_t groups = (g.width + OWG - 1) / OWG;
+  for (index_t hh : heights) {
+    PipeShares shares = PipeShares::equal((groups * hh + blocks - 1) / blocks);
+    pipe_starts(groups, hh, blocks, pipe_fill_rows<S0, S1, PF, LAG1>(), &shares);
+    auto launch = [&](const float* I, float* O) {
+      pipe_stamped<S0, S1, PF, false, LAG1><<<blocks, 2 * kBlock>>>(I, O, g.pitch, g.core_offset(), g.width, g.height,
+                                                                     0, g.width, 0, hh, shares, c0, 0.2f, st.get());
+    };
+    std::vector<double> med_c, max_c, span, mhz, rows_mean, start_p50, start_max, end_min, end_p50, end_max;
+    std::vector<std::vector<double>> xcd_c(8), xcd_start(8), xcd_clk(8);
+    for (int r = 0; r < reps + 3; ++r) {
+      if (r & 1) launch(out, const_cast<float*>(in));
+      else launch(in, out);
+      MXS_HIP_CHECK(hipDeviceSynchronize());
+      if (r < 3) continue;
+      MXS_HIP_CHECK(hipMemcpy(h.data(), st.get(), h.size() * 8, hipMemcpyDeviceToHost));
+      std::vector<double> c, clk;
+      unsigned long long rmin = ~0ull, rmax = 0;
+      double rows = 0;
+      for (int b = 0; b < blocks; ++b) {
+        const unsigned long long* p = &h[size_t(b) * 6];
+        c.push_back(double(p[3] - p[2]));
+        clk.push_back(double(p[3] - p[2]) / double(std::max<unsigned long long>(p[1] - p[0], 1)) * 100.0);  // MHz
+        rmin = std::min(rmin, p[0]);
+        rmax = std::max(rmax, p[1]);
+        rows += double(p[4]);
+      }
+      std::vector<double> st0, en0;  // us after the first workgroup's start
+      for (int b = 0; b < blocks; ++b) {
+        const unsigned long long* p = &h[size_t(b) * 6];
+        st0.push_back(double(p[0] - rmin) / 100.0);
+        en0.push_back(double(p[1] - rmin) / 100.0);
+        const int x = int((p[5] >> 16) & 0xf) & 7;
+        xcd_c[size_t(x)].push_back(double(p[3] - p[2]));
+        xcd_start[size_t(x)].push_back(double(p[0] - rmin) / 100.0);
+        xcd_clk[size_t(x)].push_back(double(p[3] - p[2]) / double(std::max<unsigned long long>(p[1] - p[0], 1)) * 100.0);
+      }
+      std::sort(st0.begin(), st0.end());
+      std::sort(en0.begin(), en0.end());
+      start_p50.push_back(st0[st0.size() / 2]);
+      start_max.push_back(st0.back());
+      end_min.push_back(en0.front());
+      end_p50.push_back(en0[en0.size() / 2]);
+      end_max.push_back(en0.back());
+      std::sort(c.begin(), c.end());
+      std::sort(clk.begin(), clk.end());
+      med_c.push_back(c[c.size() / 2]);
+      max_c.push_back(c.back());
+      span.push_back(double(rmax - rmin) / 100.0);
+      mhz.push_back(clk[clk.size() / 2]);
+      rows_mean.push_back(rows / blocks);
+    }
+    auto med = [](std::vector<double> v) {
+      std::sort(v.begin(), v.end());
+      return v[v.size() / 2];
+    };
+    std::printf("{\"fillfit\": \"%s\", \"W\": %ld, \"h\": %ld, \"groups\": %ld, \"rows_per_wg\": %.1f, "
+                "\"model_fill_rows\": %ld, \"wg_kcycles_median\": %.2f, \"wg_kcycles_max\": %.2f, \"span_us\": %.2f, "
+                "\"mhz\": %.0f, \"pass_kcycles\": %.1f}\n",
+                name, long(g.width), long(hh), long(groups), med(rows_mean), long(pipe_fill_rows<S0, S1, PF, LAG1>()),
+                med(med_c) / 1e3, med(max_c) / 1e3, med(span), med(mhz), med(span) * med(mhz) / 1e3);
+    std::printf("{\"fillfit_skew\": \"%s\", \"h\": %ld, \"start_us_p50\": %.2f, \"start_us_max\": %.2f, "
+                "\"end_us_min\": %.2f, \"end_us_p50\": %.2f, \"end_us_max\": %.2f, \"xcd\": [",
+                name, long(hh), med(start_p50), med(start_max), med(end_min), med(end_p50), med(end_max));
+    for (int x = 0; x < 8; ++x)
+      std::printf("%s[%zu, %.1f, %.2f, %.0f]", x ? ", " : "", xcd_c[size_t(x)].size() / size_t(reps),
+                  xcd_c[size_t(x)].empty() ? 0.0 : med(xcd_c[size_t(x)]) / 1e3,
+                  xcd_start[size_t(x)].empty() ? 0.0 : med(xcd_start[size_t(x)]),
+                  xcd_clk[size_t(x)].empty() ? 0.0 : med(xcd_clk[size_t(x)]));
+    std::printf("]}\n");
+    for (auto& v : xcd_c) v.clear();
+    for (auto& v : xcd_start) v.clear();
+    for (auto& v : xcd_clk) v.clear();
+    std::fflush(stdout);
+  }
+}
+
 struct Variant {
   std::string name;
   std::function<void(hipStream_t)> launch;
@@ -302,6 +438,24 @@ int main(int argc, char** argv) {
   vs.push_back(tb1<6, 128, 32, false>(in, out, g));
   float* tmp = c.get();
   const char* focus = std::getenv("TUNE_FOCUS");
+  if (focus && std::string(focus) == "fillfit") {  // fill per share: workgroup cycles vs share rows (ghost tile)
+    const int reps = rounds;
+    std::vector<index_t> hs;
+    for (index_t hh = H; hh >= 1024 && hs.size() < 5; hh /= 2) hs.push_back(hh);
+    const char* set = std::getenv("TUNE_FILL_SET");
+    if (set && std::string(set) == "prod") {  // the forms the launcher picks: ascending <= 768-row shares, else descending
+      fillfit<12, 8, 6, 3>("12+8_pf6_asc", in, out, g, hs, reps);
+      fillfit<12, 8, 6, 0>("12+8_pf6_desc", in, out, g, hs, reps);
+      return 0;
+    }
+    fillfit<12, 8, 6, 3>("12+8_pf6_asc", in, out, g, hs, reps);
+    fillfit<12, 8, 3, 3>("12+8_pf3_asc", in, out, g, hs, reps);
+    fillfit<12, 8, 6, 0>("12+8_pf6_desc", in, out, g, hs, reps);
+    fillfit<8, 12, 6, 3>("8+12_pf6_asc", in, out, g, hs, reps);
+    fillfit<16, 4, 6, 3>("16+4_pf6_asc", in, out, g, hs, reps);
+    fillfit<12, 8, 9, 3>("12+8_pf9_asc", in, out, g, hs, reps);
+    return 0;
+  }
   if (focus && std::string(focus) == "stamp") {  // per-wave lifetimes of the default S = 16 rotated kernel
     int occ = 0, cus = 0;
     MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(

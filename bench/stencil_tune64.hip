@@ -190,6 +190,20 @@ int main(int argc, char** argv) {
     vs.push_back(c);
     vs.push_back(d);
   }
+  if (f == "spill") {  // the 8192^2 default (8 + 8 joint, ascending, sum form) vs its register-pressure variants
+    Variant a = pipe<8, 8, 3, true, true, true, 3>(g, tmp);
+    Variant b = pipe<8, 8, 3, true, true, true, 3, 5>(g, tmp);
+    Variant c = pipe<8, 8, 3, true, true, true, 3, 6>(g, tmp);
+    b.ref = c.ref = a.launch;
+    b.tol = c.tol = 0.0;
+    b.name += "_nocopy";
+    c.name += "_fence";
+    Variant d = pipe<8, 8, 3, true, true, true>(g, tmp);  // descending (no spill)
+    vs.push_back(a);
+    vs.push_back(b);
+    vs.push_back(c);
+    vs.push_back(d);
+  }
   if (f == "perm") {  // lane-crossing neighbours via ds_bpermute (LDS pipe) vs DPP moves, bitwise twins
     Variant a = pipe<8, 8, 3, true, true, true, 3>(g, tmp);
     Variant b = pipe<8, 8, 3, true, true, true, 3, 1>(g, tmp);

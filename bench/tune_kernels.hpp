@@ -431,6 +431,24 @@ struct BodySumF64Perm : BodySumF64 {
 };
 
 
+// fp64 register-pressure variants of the sum body (TUNE_FOCUS=spill in
+// stencil_tune64): XB = 5 enters loaded rows without the copy into fresh
+// registers, XB = 6 fences the fetching stage's row iterations.
+struct BodySumF64NoCopy : BodySumF64 {
+  static __device__ __forceinline__ V enter(const V& v) { return v; }
+};
+struct BodySumF64Fence : BodySumF64 {
+  static constexpr bool kStage0Fence = true;
+};
+template <>
+struct FastBody<double, true, 5> {
+  using type = BodySumF64NoCopy;
+};
+template <>
+struct FastBody<double, true, 6> {
+  using type = BodySumF64Fence;
+};
+
 template <>
 struct FastBody<float, true, 1> {
   using type = BodySumF32Perm;

@@ -606,6 +606,10 @@ struct BodyRotF32 {  // rotated-pair fp32 (jac_rot4f)
   using T = float;
   using V = f32x4;
   static constexpr int N = 4;
+  // A scheduling fence after each row iteration of the pipeline's fetching
+  // stage (pipe_chunk): keeps the scheduler from overlapping consecutive rows'
+  // level chains, which holds more rows live (see BodySumF64).
+  static constexpr bool kStage0Fence = false;
   static __device__ __forceinline__ V zero() { return f32x4(0.f); }
   static __device__ __forceinline__ V load(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
   static __device__ __forceinline__ V enter(const V& v) { return rot_in_copy(v); }
@@ -621,6 +625,7 @@ struct BodyWideF64 {  // 4 consecutive fp64 cells per lane (jac_w4d)
   using T = double;
   using V = f64x4;
   static constexpr int N = 4;
+  static constexpr bool kStage0Fence = false;  // see BodyRotF32
   static __device__ __forceinline__ V zero() { return f64x4(0.0); }
   static __device__ __forceinline__ V load(const double* p) {
     const f64x2 a = *reinterpret_cast<const f64x2*>(p), b = *reinterpret_cast<const f64x2*>(p + 2);
@@ -689,6 +694,10 @@ struct BodySumF32 : BodyRotF32 {
   }
 };
 struct BodySumF64 : BodyWideF64 {
+  // Without the fence the ascending 8 + 8 pass (fp64 8192^2) needs more than
+  // the 256 VGPRs two waves per SIMD allow and spills 44 B per lane to
+  // scratch; fenced: 231 VGPRs, no scratch, 1.5% faster (profiles/r06_fp64).
+  static constexpr bool kStage0Fence = true;
   static __device__ __forceinline__ V jac(const V& u, const V& m, const V& d, double, double) { return sum_w4d(u, m, d); }
   static __device__ __forceinline__ void store(const V& top, __amdgpu_buffer_rsrc_t r, unsigned off, double scale) {
     BodyWideF64::store(top * scale, r, off, scale);
@@ -1333,6 +1342,7 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
         // writes for k < 0 land in slots no reader touches before they are
         // rewritten. base + k < RING: blocks are ring-aligned.
         my[(base + k) * RSTRIDE] = top;
+        if constexpr (B::kStage0Fence) __builtin_amdgcn_sched_barrier(0);
       }
       base = base + PF < RING ? base + PF : 0;
       __syncthreads();

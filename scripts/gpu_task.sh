@@ -24,6 +24,7 @@
 #                          -cwNN --clock-warmup-ms NN, -t0 / -t1 --warm-tail 0 / 1 (checked first)
 #                          -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
+#   tune BIN FOCUS [ARGS]  an in-process tuner (build/bin/BIN with TUNE_FOCUS=FOCUS) -> OUT/tune_FOCUS.txt
 #   final                  tests + smoke + the driver's bench command + its kernel-trace profile
 #   warmsweep REPS TILE W...  the driver's 20-step window after W ms of clock warm-up, interleaved
 set -uo pipefail
@@ -149,6 +150,13 @@ task_py() {
   tail -20 "$OUT/py.txt"
 }
 
+task_tune() {  # BIN FOCUS [ARGS]: the in-process tuners (build/bin/stencil_tune, stencil_tune64) -> OUT/tune_FOCUS.txt
+  local bin=$1 focus=$2
+  shift 2
+  step 600 "$OUT/tune_$focus.txt" env TUNE_FOCUS="$focus" "build/bin/$bin" "$@"
+  grep -E "median_ms|mismatches|error|fillfit" "$OUT/tune_$focus.txt" | head -60 || true
+}
+
 task_final() {
   task_tests || exit $?
   task_smoke
@@ -213,6 +221,7 @@ case "$TASK" in
   window) task_window "$@" ;;
   py) task_py "$@" ;;
   final) task_final ;;
+  tune) task_tune "$@" ;;
   warmab) task_warmab "$@" ;;
   warmsweep) task_warmsweep "$@" ;;
   *) echo "unknown task '$TASK'"; exit 2 ;;
