@@ -686,6 +686,13 @@ int main(int argc, char** argv) {
     vs.push_back(c);
     vs.push_back(vs_plain(pipe<12, 12, 6, true, 0, true, 4, false, true, 2>(in, out, g), c));
     vs.push_back(vs_plain(pipe<12, 12, 6, true, 0, true, 4, false, true, 3>(in, out, g), c));
+  } else if (focus && std::string(focus) == "head20") {  // the headline pass: S = 20 12 + 8 descending vs ascending (r06)
+    const Variant a = pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g);
+    Variant b = pipe<12, 8, 6, true, 0, true, 4, false, true, 3>(in, out, g);
+    b.ref = a.launch;  // same arithmetic per cell: bitwise
+    b.tol = 0.f;
+    vs.push_back(a);
+    vs.push_back(b);
   } else if (focus && std::string(focus) == "lag2head") {  // long-chunk tiles: the S = 20 / 24 candidates
     const Variant a = pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g);
     Variant b = pipe<8, 12, 6, true, 0, true, 4, false, true, 2>(in, out, g);

@@ -674,6 +674,13 @@ __device__ __forceinline__ f32x4 sum_rot4f(const f32x4& up, const f32x4& mid, co
   f32x4 o;
   o.xy = ns_a + h_a;
   o.zw = ns_b + h_b;
+#ifdef MXS_TEST_VALU_PAD
+  // Test builds only (tests/test_gpu_cycles.py, profiles/r06_cycles): one more
+  // VALU slot per level-row (9 instead of 8, +12.5%), results unchanged (x * 1).
+  float pad = o.x;
+  asm volatile("v_mul_f32 %0, 1.0, %0" : "+v"(pad));
+  o.x = pad;
+#endif
   return o;
 }
 __device__ __forceinline__ f64x4 sum_w4d(const f64x4& up, const f64x4& mid, const f64x4& dn) {

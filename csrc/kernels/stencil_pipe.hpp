@@ -63,18 +63,21 @@ constexpr int joint_s0() {
 }
 // Level order (LAG1, stencil_device.hpp pipe_chunk): ascending levels lag one
 // row per level instead of three, so a chunk fills its pipeline S - 1 rows
-// sooner per stage, at the cost of a dependent chain of levels per row. It pays
-// on short chunks (tuner focus lag1, 21 interleaved rounds, profiles/r02_lag1):
-// S = 20 on 8192^2 (288-row chunks) 8 + 12: 8.88 -> 9.49 T cells/s, on the
-// 8-GPU tile 16384 x 8192 (576 rows) 12 + 8: 10.21 -> 10.52; with 1152-row
-// chunks (16384^2) and longer the descending order wins (12 + 8: 11.04 vs 10.58;
-// 32768^2: 10.84 vs 10.50). S = 24 (12 + 12) takes LAG1 everywhere (+1.3% on
-// 32768^2, +6-9% on the smaller tiles).
-constexpr index_t kLag1MaxChunk = 768;
+// sooner per stage, at the cost of a dependent chain of levels per row. Round 2
+// (wall-clock tuner, profiles/r02_lag1) found it paying on short chunks only
+// and kept the descending order past 768-row shares. Round 6 measured it in
+// shader cycles per workgroup (tuner focus fillfit, profiles/r06_fill): the two
+// orders cost the same per row (796 cycles per group-row at S = 20, 12 + 8) and
+// the ascending one less per share (38 k vs 51 k cycles of fill), so fp32 S = 20
+// ascends at every share length: 32768^2 -0.65%, 16384^2 -1.8%, the 8-GPU tile
+// -2.3% workgroup cycles. S = 24 (12 + 12) took LAG1 everywhere already.
+constexpr index_t kLag1MaxChunk = index_t(1) << 62;  // fp32 S = 20: every share length
 constexpr int kLagBoth = 3;  // LAG1 stage mask: both stages ascend
 // fp64 (S = 16 as 8 + 8, wide lanes): 8192^2 (288-row chunks) 3.88 -> 4.00 T
-// cells/s; 576- and 1152-row chunks within +-1.5% (profiles/r02_lag1/*64*).
-constexpr index_t kLag1MaxChunkF64 = 384;
+// cells/s (profiles/r02_lag1/*64*); on 2240-row shares (32768 x 16384) the two
+// orders tie (4,354 vs 4,346 G cells/s, profiles/r06_fp64), so fp64 ascends at
+// every share length too.
+constexpr index_t kLag1MaxChunkF64 = index_t(1) << 62;
 // With LAG1 (short chunks) S = 20 runs 8 + 12 below 12288 columns (8192^2:
 // 9.49 vs 9.36 for 12 + 8), else 12 + 8.
 constexpr index_t kJointWide = 12288;

@@ -28,12 +28,16 @@ from cuda_mpi_scratch_amd.utils.cycles import pass_cycles
 
 pytestmark = pytest.mark.gpu
 
-# name: (width, height, dtype, levels (0: auto_time_block), wrap, budget in k shader cycles per pass)
+# name: (width, height, dtype, levels (0: auto_time_block), wrap, budget). The VALU-bound
+# fp32 passes are held in k shader cycles per pass at the slowest XCD's clock (two boxes:
+# 3647 / 3652, 277.3 / 277.8, 505.6 / 506.1; budgets +5%). The fp64 pass is HBM-bound
+# (S = 16: 1 B per cell-level against a 19-slot VALU body): its cycles follow the clock
+# (433-477 k at 1.82-2.0 GHz) while its time does not (242-245 us), so it is held in us.
 CASES = {
-    "headline_32768sq_f32": (32768, 32768, "f32", 20, True, None),
-    "config2_8192sq_f32": (8192, 8192, "f32", 0, True, None),
-    "fp64_8192sq": (8192, 8192, "f64", 16, True, None),
-    "tile8_16384x8192_f32": (16384, 8192, "f32", 20, False, None),
+    "headline_32768sq_f32": (32768, 32768, "f32", 20, True, ("kcycles", 3830.0)),
+    "config2_8192sq_f32": (8192, 8192, "f32", 0, True, ("kcycles", 291.0)),
+    "fp64_8192sq": (8192, 8192, "f64", 16, True, ("us", 257.0)),
+    "tile8_16384x8192_f32": (16384, 8192, "f32", 20, False, ("kcycles", 531.0)),
 }
 
 
@@ -59,10 +63,14 @@ def test_pass_cycles_within_budget(gpu, name):
 
     r = pass_cycles(launch, s, passes=24, warm=40 if w * h >= 1 << 28 else 200)
     kernel = H.last_stencil_dispatch()
-    rec = {"case": name, "S": S, "kernel": kernel, "kcycles": round(r["cycles"] / 1e3, 1),
-           "kcycles_min": round(r["cycles_min"] / 1e3, 1), "kcycles_max": round(r["cycles_max"] / 1e3, 1),
-           "us": round(r["us"], 1), "mhz": round(r["mhz"]), "budget_kcycles": budget}
+    rec = {"case": name, "S": S, "kernel": kernel, "lag1": bool(H.last_pipe_lag1()),
+           "kcycles": round(r["cycles"] / 1e3, 1), "kcycles_min": round(r["cycles_min"] / 1e3, 1),
+           "kcycles_max": round(r["cycles_max"] / 1e3, 1),
+           "kcycles_median_clock": round(r["cycles_median_clock"] / 1e3, 1), "us": round(r["us"], 1),
+           "mhz": round(r["mhz"]), "mhz_slowest_xcd": round(r["mhz_slowest_xcd"]),
+           "xcd_spread": round(r["xcd_spread"], 3), "budget": budget}
     print(json.dumps(rec))
     assert kernel.startswith("stream_pipe_sum"), kernel
-    if budget is not None:
-        assert r["cycles"] / 1e3 <= budget, rec
+    unit, limit = budget
+    got = r["cycles"] / 1e3 if unit == "kcycles" else r["us"]
+    assert got <= limit, rec

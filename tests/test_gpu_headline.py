@@ -333,10 +333,10 @@ def test_pipe_joint_windows_bitwise_vs_per_strip(gpu, w, h, steps, wrap, rect, d
     (16384, 2048, 20, False, None, "f32", True),   # ghost-ring tile (multi-GPU schedule)
     (8192, 4096, 24, True, None, "f32", True),     # S = 24: ascending order at every chunk length
     (4096, 2048, 24, False, (8, 4088, 24, 2024), "f32", True),  # interior rectangle
-    (4096, 49152, 20, True, None, "f32", False),   # 960-row chunks: descending order
+    (4096, 49152, 20, True, None, "f32", True),    # 960-row chunks: fp32 S = 20 ascends at every length (r06)
     (4096, 2048, 16, True, None, "f64", True),     # fp64 wide lanes, 8 + 8, short chunks
     (2048, 1024, 16, False, (8, 2040, 16, 1008), "f64", True),
-    (2048, 40000, 16, True, None, "f64", False),   # 469-row chunks: descending order
+    (2048, 40000, 16, True, None, "f64", True),    # 469-row chunks: fp64 ascends at every length too (r06)
 ])
 @pytest.mark.parametrize("sum_form", [True, False])
 def test_pipe_level_order_bitwise(gpu, w, h, steps, wrap, rect, dtype, lag1, sum_form):
