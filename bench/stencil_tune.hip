@@ -443,6 +443,13 @@ int main(int argc, char** argv) {
     std::vector<index_t> hs;
     for (index_t hh = H; hh >= 1024 && hs.size() < 5; hh /= 2) hs.push_back(hh);
     const char* set = std::getenv("TUNE_FILL_SET");
+    if (set && std::string(set) == "split") {  // stage splits of S = 20, ascending (10 + 10, 11 + 9 need a 24-deep ring)
+      fillfit<12, 8, 6, 3>("12+8_pf6_asc", in, out, g, hs, reps);
+      fillfit<10, 10, 6, 3>("10+10_pf6_asc", in, out, g, hs, reps);
+      fillfit<11, 9, 6, 3>("11+9_pf6_asc", in, out, g, hs, reps);
+      fillfit<13, 7, 6, 3>("13+7_pf6_asc", in, out, g, hs, reps);
+      return 0;
+    }
     if (set && std::string(set) == "prod") {  // the forms the launcher picks: ascending <= 768-row shares, else descending
       fillfit<12, 8, 6, 3>("12+8_pf6_asc", in, out, g, hs, reps);
       fillfit<12, 8, 6, 0>("12+8_pf6_desc", in, out, g, hs, reps);
@@ -693,6 +700,14 @@ int main(int argc, char** argv) {
     b.tol = 0.f;
     vs.push_back(a);
     vs.push_back(b);
+    // Balanced stage splits (wrap only: their joint read reach A0 + A1 = 24 exceeds
+    // SA(20), so a ghost-ring tile would need a 24-deep ring).
+    for (auto v : {pipe<10, 10, 6, true, 0, true, 4, false, true, 3>(in, out, g),
+                   pipe<11, 9, 6, true, 0, true, 4, false, true, 3>(in, out, g)}) {
+      v.ref = a.launch;
+      v.tol = 0.f;
+      vs.push_back(v);
+    }
   } else if (focus && std::string(focus) == "lag2head") {  // long-chunk tiles: the S = 20 / 24 candidates
     const Variant a = pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g);
     Variant b = pipe<8, 12, 6, true, 0, true, 4, false, true, 2>(in, out, g);

@@ -282,6 +282,14 @@ class StencilSolver {
   // Whether the solver follows the peers' schedule (remote peers, or a
   // loopback rehearsal of them).
   bool multi_rank() const { return multi_rank_; }
+  // Paired measurements (scripts/exp/wire_paired.py): override the opening for
+  // the following calls on one solver — Serial, InteriorFirst (needs the
+  // form: interior-first allowed at construction) or Auto (back to the
+  // opening construction / prepare() chose). Collective: every rank passes
+  // the same value. The decision's record (opening_choice()) is unchanged.
+  void force_opening(Opening o);
+  // The same for the later super-steps of a call (SolverConfig::steady).
+  void force_steady(Opening o);
   // Whether the opening super-step of a call at depth S runs interior-first on
   // this rank (the opening is on and the tile has the chunk-list form).
   bool halo_last(int S) const;

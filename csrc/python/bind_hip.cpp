@@ -502,6 +502,28 @@ PYBIND11_MODULE(_mxs_hip, m) {
       .def(
           "halo_last", [](SolverHandle& h, int S) { return h.visit([S](auto& s) { return s.halo_last(S); }); },
           py::arg("S"), "whether a call's opening super-step of depth S runs interior-first on this rank")
+      .def(
+          "force_opening",
+          [](SolverHandle& h, const std::string& o) {
+            const Opening op = o == "serial" ? Opening::Serial
+                               : o == "interior-first" ? Opening::InteriorFirst
+                               : o == "auto" ? Opening::Auto
+                                             : throw std::invalid_argument("opening: auto|serial|interior-first");
+            h.visit([op](auto& s) { s.force_opening(op); });
+          },
+          py::arg("opening"),
+          "paired measurements: the opening of the following calls (serial, interior-first, or auto = the one "
+          "construction / prepare() chose); collective")
+      .def(
+          "force_steady",
+          [](SolverHandle& h, const std::string& o) {
+            const Opening op = o == "serial" ? Opening::Serial
+                               : o == "interior-first" ? Opening::InteriorFirst
+                               : o == "auto" ? Opening::Auto
+                                             : throw std::invalid_argument("steady: auto|serial|interior-first");
+            h.visit([op](auto& s) { s.force_steady(op); });
+          },
+          py::arg("steady"), "paired measurements: the later super-steps' schedule of the following calls")
       .def("multi_rank", [](SolverHandle& h) { return h.visit([](auto& s) { return s.multi_rank(); }); },
            "whether the solver follows the peers' schedule (remote peers or a loopback rehearsal)")
       .def("schedule_times",

@@ -770,6 +770,31 @@ void StencilSolver<T>::prepare(int iters) {
 }
 
 template <typename T>
+void StencilSolver<T>::force_opening(Opening o) {
+  join_side();
+  wait_idle("force_opening");
+  if (o == Opening::Auto) {
+    halo_last_on_ = halo_last_allowed_ &&
+                    (opening_choice_ == "interior-first" || (opening_choice_.empty() && cfg_.opening == Opening::InteriorFirst));
+    return;
+  }
+  MXS_CHECK(o == Opening::Serial || halo_last_allowed_,
+            "force_opening: this solver has no interior-first opening (backend, tile or configuration)");
+  halo_last_on_ = o == Opening::InteriorFirst;
+}
+
+template <typename T>
+void StencilSolver<T>::force_steady(Opening o) {
+  join_side();
+  wait_idle("force_steady");
+  if (o == Opening::Auto) {
+    steady_on_ = steady_choice_ == "interior-first" || (steady_choice_.empty() && cfg_.steady == Opening::InteriorFirst);
+    return;
+  }
+  steady_on_ = o == Opening::InteriorFirst;
+}
+
+template <typename T>
 void StencilSolver<T>::warm(int iters, int passes) {
   MXS_TRACE_RANGE("stencil.warm");
   maybe_stall("warm");
