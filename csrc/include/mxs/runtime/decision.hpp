@@ -20,6 +20,19 @@
 // A candidate wins when the upper end of its median ratio's 95% notch,
 // median + 1.58 IQR / sqrt(n), is below 1 - min_gain (min_gain 0: the notch
 // alone guards against noise). Among candidates the lowest notch is taken.
+//
+// WinRule::Median (the opening decision, since round 6): the lowest-notch
+// candidate wins when its median ratio is at most 1 - min_gain, i.e. also on a
+// tie. The serial opening's window starts its pass only after the host has
+// enqueued pack, the RCCL group and unpack, with the GPU idle in between; the
+// paired samples, taken back to back on a busy host, see less of that host
+// latency than the window does. On the 8-GPU tile the processes whose notch
+// rule kept serial (paired ratios 0.986-1.000) ran their windows at 0.308-0.356
+// ms, those that took interior-first at 0.276-0.294 (30 single shots,
+// profiles/r06_tiles), and a serial window's run() host time varied 17-82 us
+// from process to process (profiles/r06_serial_host). Interior-first launches
+// the inner chunks first and hides that latency.
+enum class WinRule : int { Notch = 0, Median = 1 };
 #pragma once
 
 #include <algorithm>
@@ -76,7 +89,7 @@ struct RoundDecision {
 // The decision on per-round maxima over ranks: base[r], cand[c][r] (ms; a
 // kMissingSample anywhere in a candidate's rounds drops it).
 inline RoundDecision decide_on_maxima(const std::vector<double>& base, const std::vector<std::vector<double>>& cand,
-                                      double min_gain) {
+                                      double min_gain, WinRule rule = WinRule::Notch) {
   RoundDecision d;
   d.rounds = int(base.size());
   std::vector<double> b = base;
@@ -104,7 +117,10 @@ inline RoundDecision decide_on_maxima(const std::vector<double>& base, const std
       d.candidate_ms = median_iqr(cv).first;
     }
   }
-  d.win = d.best >= 0 && paired_win(d.ratio, d.ratio_iqr, d.rounds, min_gain);
+  if (rule == WinRule::Median)
+    d.win = d.best >= 0 && d.rounds > 0 && d.ratio > 0 && d.ratio <= 1.0 - min_gain;
+  else
+    d.win = d.best >= 0 && paired_win(d.ratio, d.ratio_iqr, d.rounds, min_gain);
   return d;
 }
 

@@ -473,7 +473,8 @@ class StencilSolver {
   void choose_opening(int S);                // Opening::Auto: time both, agree, keep the faster
   void choose_steady(int S);                 // SolverConfig::steady Auto: the same for two super-steps
   RoundDecision paired_rounds(int rounds, const std::vector<std::function<double()>>& kinds,
-                              const std::vector<bool>& have, const char* phase, std::vector<double>* local = nullptr);
+                              const std::vector<bool>& have, const char* phase, std::vector<double>* local = nullptr,
+                              WinRule rule = WinRule::Notch);
   bool steady_on_ = false;                   // every super-step interior-first (with the opening)
   std::string steady_choice_, steady_reason_;
   bool side_pending_ = false;                // side-stream work not yet joined to main

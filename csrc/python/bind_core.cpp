@@ -173,7 +173,7 @@ PYBIND11_MODULE(_mxs_core, m) {
   m.def(
       "opening_decision",
       [](const std::vector<std::vector<double>>& serial, const std::vector<std::vector<std::vector<double>>>& cands,
-         double min_gain) {
+         double min_gain, const std::string& rule) {
         // serial[rank][round], cands[rank][candidate][round]: what every rank timed.
         // The solver agrees the element-wise max (one vector per rank), then decides.
         MXS_CHECK(!serial.empty() && serial.size() == cands.size(), "one serial and one candidate set per rank");
@@ -190,7 +190,9 @@ PYBIND11_MODULE(_mxs_core, m) {
         const std::vector<double> v = elementwise_max(flat);
         std::vector<std::vector<double>> cm(nc);
         for (size_t c = 0; c < nc; ++c) cm[c].assign(v.begin() + (1 + c) * nr, v.begin() + (2 + c) * nr);
-        const RoundDecision d = decide_on_maxima(std::vector<double>(v.begin(), v.begin() + nr), cm, min_gain);
+        MXS_CHECK(rule == "median" || rule == "notch", "rule: median (the opening) or notch");
+        const RoundDecision d = decide_on_maxima(std::vector<double>(v.begin(), v.begin() + nr), cm, min_gain,
+                                                 rule == "median" ? WinRule::Median : WinRule::Notch);
         py::dict out;
         out["best"] = d.best;
         out["win"] = d.win;
@@ -202,9 +204,11 @@ PYBIND11_MODULE(_mxs_core, m) {
         out["ratios"] = d.ratios;
         return out;
       },
-      py::arg("serial"), py::arg("candidates"), py::arg("min_gain") = 0.0,
+      py::arg("serial"), py::arg("candidates"), py::arg("min_gain") = 0.0, py::arg("rule") = "median",
       "StencilSolver::choose_opening's collective rule: per-round maxima over ranks, paired ratios of the maxima, "
-      "the lowest notch among candidates (runtime/decision.hpp); missing slots: kMissingSample");
+      "the lowest notch among candidates, which wins when its median ratio is <= 1 - min_gain (rule 'median', the "
+      "opening) or its notch is below it (rule 'notch', the steady and direct-halo decisions) "
+      "(runtime/decision.hpp); missing slots: kMissingSample");
   m.attr("MISSING_SAMPLE") = kMissingSample;
   m.def("balanced_starts", &kernels::balanced_starts, py::arg("groups"), py::arg("rows"), py::arg("blocks"),
         py::arg("fill"), "fill-aware linear starts of the pipeline workgroups' shares (blocks + 1 entries)");

@@ -270,8 +270,10 @@ void StencilSolver<T>::choose_opening(int S) {
       });
     });
   std::vector<double> local;
+  // Median rule: a tie goes to interior-first (decision.hpp: the window sees the
+  // host's enqueue latency in front of the serial opening's pass).
   const RoundDecision d = paired_rounds(nr, kinds, {true, !!cands[0], !!cands[1], !!cands[2]},
-                                        "prepare: opening agreement", &local);
+                                        "prepare: opening agreement", &local, WinRule::Median);
   opening_local_ratio_samples_.clear();  // this rank's own paired ratios (diagnostics)
   for (int c = 0; c < kCands; ++c) {
     if (!cands[c]) continue;
@@ -301,8 +303,8 @@ void StencilSolver<T>::choose_opening(int S) {
   } else {
     std::snprintf(buf, sizeof(buf),
                   "paired ratio of the per-round maxima over %d rank(s), interior-first / serial, %d rounds (host "
-                  "clock, enqueue to drained): median %.3f, IQR %.3f, notch %.3f (switch at notch < %.3f); medians %.4f / %.4f "
-                  "ms: %s; outer set %d workgroups from the measured exchange lead %.1f us of a %.1f us pass",
+                  "clock, enqueue to drained): median %.3f, IQR %.3f, notch %.3f (switch at median <= %.3f); medians "
+                  "%.4f / %.4f ms: %s; outer set %d workgroups from the measured exchange lead %.1f us of a %.1f us pass",
                   world_, nr, d.ratio, d.ratio_iqr, d.notch, 1.0 - cfg_.min_gain, d.candidate_ms, d.baseline_ms,
                   d.win ? "interior-first" : "serial kept", halo_last_outer_wgs(S), lead_us_, lead_pass_us_);
   }
@@ -415,7 +417,7 @@ void StencilSolver<T>::choose_steady(int S) {
 template <typename T>
 RoundDecision StencilSolver<T>::paired_rounds(int rounds, const std::vector<std::function<double()>>& kinds,
                                               const std::vector<bool>& have, const char* phase,
-                                              std::vector<double>* local) {
+                                              std::vector<double>* local, WinRule rule) {
   MXS_CHECK(!kinds.empty() && have.size() == kinds.size() && rounds > 0, "paired_rounds: one have-flag per kind");
   const size_t nk = kinds.size(), nr = size_t(rounds);
   std::vector<double> v(nk * nr, kMissingSample);  // [kind 0 x rounds, kind 1 x rounds, ...]
@@ -428,7 +430,7 @@ RoundDecision StencilSolver<T>::paired_rounds(int rounds, const std::vector<std:
   agree_max(v, phase);
   std::vector<std::vector<double>> cand(nk - 1);
   for (size_t k = 1; k < nk; ++k) cand[k - 1].assign(v.begin() + long(k * nr), v.begin() + long((k + 1) * nr));
-  return decide_on_maxima(std::vector<double>(v.begin(), v.begin() + long(nr)), cand, cfg_.min_gain);
+  return decide_on_maxima(std::vector<double>(v.begin(), v.begin() + long(nr)), cand, cfg_.min_gain, rule);
 }
 
 template <typename T>
@@ -689,7 +691,7 @@ WindowPhases StencilSolver<T>::profile_window(int iters) {
   template T* StencilSolver<T>::scratch_tiles(int);                                                          \
   template RoundDecision StencilSolver<T>::paired_rounds(int, const std::vector<std::function<double()>>&,   \
                                                          const std::vector<bool>&, const char*,              \
-                                                         std::vector<double>*);                              \
+                                                         std::vector<double>*, WinRule);                     \
   template void StencilSolver<T>::poison_ghost(T*);                                                          \
   template void StencilSolver<T>::validate_direct(int);                                                      \
   template WindowPhases StencilSolver<T>::profile_window(int);

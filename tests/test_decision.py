@@ -138,3 +138,33 @@ def test_lowest_notch_wins_among_candidates():
         serial.append(s)
         cands.append([c0, c1])
     assert C.opening_decision(serial, cands, 0.0)["best"] == 1
+
+
+def test_opening_rule_takes_interior_first_on_a_tie():
+    """The opening's rule (round 6): the lowest-notch candidate wins when its
+    median ratio is <= 1, a tie included, where the notch rule (steady, direct
+    halo) keeps the baseline. A serial window pays the host's enqueue of the
+    RCCL group in front of its pass, which the back-to-back paired samples see
+    less of (runtime/decision.hpp, profiles/r06_tiles)."""
+    rng = random.Random(13)
+    serial, cands = [], []
+    for r in range(8):
+        s, c = _rank(0.290, 0.2885, 0.01, 20, rng)  # a 0.5% gain: inside the noise
+        serial.append(s)
+        cands.append([c])
+    med = C.opening_decision(serial, cands, 0.0)
+    notch = C.opening_decision(serial, cands, 0.0, "notch")
+    assert med["ratio"] <= 1.0 and med["notch"] >= 1.0, med
+    assert med["win"] is True and notch["win"] is False, (med, notch)
+
+
+def test_opening_rule_keeps_serial_when_interior_first_is_slower():
+    rng = random.Random(17)
+    serial, cands = [], []
+    for r in range(8):
+        s, c = _rank(0.290, 0.300, 0.01, 20, rng)  # 3.4% slower
+        serial.append(s)
+        cands.append([c])
+    for rule in ("median", "notch"):
+        d = C.opening_decision(serial, cands, 0.0, rule)
+        assert d["win"] is False and d["ratio"] > 1.0, (rule, d)
