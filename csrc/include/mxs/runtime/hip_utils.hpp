@@ -37,6 +37,18 @@ class DeviceBuffer {
     if (n > 0) MXS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&p_), size_t(n) * sizeof(T)));
     n_ = n;
   }
+  // reset() without the error policy: false (and empty) when the device has no room.
+  bool try_reset(index_t n) {
+    release();
+    if (n <= 0) return true;
+    if (hipMalloc(reinterpret_cast<void**>(&p_), size_t(n) * sizeof(T)) != hipSuccess) {
+      (void)hipGetLastError();
+      p_ = nullptr;
+      return false;
+    }
+    n_ = n;
+    return true;
+  }
   void release() {
     if (p_) (void)hipFree(p_);
     p_ = nullptr;

@@ -320,13 +320,10 @@ T* StencilSolver<T>::scratch_tiles(int n) {
   const index_t elems = tile_.alloc_elems();
   const int want = std::max(n, direct_ && direct_state_ == "pending validation" ? 2 : 1);
   if (ref_.size() >= index_t(n) * elems) return ref_.get();
-  try {
-    ref_.reset(index_t(want) * elems);
-  } catch (const std::exception&) {
-    (void)hipGetLastError();  // clear the failed allocation's sticky error
-    return nullptr;
-  }
-  return ref_.get();
+  // try_reset: no error policy on a full device (an Abort policy would end the job).
+  if (ref_.try_reset(index_t(want) * elems)) return ref_.get();
+  if (want > n && ref_.try_reset(index_t(n) * elems)) return ref_.get();
+  return nullptr;
 }
 
 // SolverConfig::steady Auto, once (the first prepare() of a call with two or
