@@ -204,11 +204,14 @@ PYBIND11_MODULE(_mxs_hip, m) {
   m.def(
       "stencil5_chunk_pass",
       [](std::uintptr_t in, std::uintptr_t out, const TileGeom& g, int steps, double c0, double c1,
-         const std::string& dt, int outer_wgs, std::uintptr_t s, bool sum_form, double range) -> py::object {
+         const std::string& dt, int outer_wgs, std::uintptr_t s, bool sum_form, double range, double lead_frac,
+         const std::string& part) -> py::object {
         // One interior-first pass (tests / tuning): the inner and the outer
         // chunk lists of kernels::make_halo_last_schedule as two launches of the
         // chunk-list kernel on one stream. The tables live for the call, so the
-        // launches are synchronised before return.
+        // launches are synchronised before return. part: "both", or "inner" /
+        // "outer" alone (timing one set against the one-launch pass).
+        MXS_CHECK(part == "both" || part == "inner" || part == "outer", "stencil5_chunk_pass: part both|inner|outer");
         kernels::Stencil5Coeffs c{c0, c1, sum_form, range};
         auto run = [&](auto tag) -> py::object {
           using T = decltype(tag);
@@ -220,7 +223,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
             ghost[size_t(k)] = (x0 < 0 || x0 + sh.read_span > g.width) ? 1 : 0;
           }
           const auto hl = kernels::make_halo_last_schedule(sh.groups, g.height, sh.blocks, sh.fill, steps, ghost,
-                                                           outer_wgs, 0.12, 0, sh.blocks % kNumXCDs == 0 ? kNumXCDs : 1,
+                                                           outer_wgs, lead_frac, 0, sh.blocks % kNumXCDs == 0 ? kNumXCDs : 1,
                                                            32);
           DeviceBuffer<kernels::PassChunk> ti(index_t(hl.inner.table.size())), to(index_t(hl.outer.table.size()));
           MXS_HIP_CHECK(hipMemcpy(ti.get(), hl.inner.table.data(), ti.bytes(), hipMemcpyHostToDevice));
@@ -230,8 +233,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
           so.blocks = hl.outer.blocks;
           Event e0(true), e1(true);
           e0.record(strm(s));
-          kernels::stencil5_chunk_pass<T>(ptr<T>(in), ptr<T>(out), g, c, si, ti.get(), hl.inner.entries, strm(s));
-          kernels::stencil5_chunk_pass<T>(ptr<T>(in), ptr<T>(out), g, c, so, to.get(), hl.outer.entries, strm(s));
+          if (part != "outer")
+            kernels::stencil5_chunk_pass<T>(ptr<T>(in), ptr<T>(out), g, c, si, ti.get(), hl.inner.entries, strm(s));
+          if (part != "inner")
+            kernels::stencil5_chunk_pass<T>(ptr<T>(in), ptr<T>(out), g, c, so, to.get(), hl.outer.entries, strm(s));
           e1.record(strm(s));
           MXS_HIP_CHECK(hipStreamSynchronize(strm(s)));
           py::dict d;
@@ -241,6 +246,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
           d["js0"] = sh.js0;
           d["lag1"] = sh.lag1;
           d["fill"] = sh.fill;
+          d["band"] = hl.band;
+          d["inner_cost"] = hl.inner_cost;
+          d["outer_cost"] = hl.outer_cost;
+          d["serial_cost"] = hl.serial_cost;
           d["kernel_us"] = double(e1.since(e0)) * 1000.0;
           return d;
         };
@@ -248,9 +257,10 @@ PYBIND11_MODULE(_mxs_hip, m) {
       },
       py::arg("src"), py::arg("dst"), py::arg("geom"), py::arg("steps"), py::arg("c_center") = 0.2,
       py::arg("c_neighbor") = 0.2, py::arg("dtype") = "f32", py::arg("outer_wgs") = 0, py::arg("stream") = 0,
-      py::arg("sum_form") = true, py::arg("range") = -1.0,
+      py::arg("sum_form") = true, py::arg("range") = -1.0, py::arg("lead_frac") = 0.12, py::arg("part") = "both",
       "one interior-first pass (inner + outer chunk lists) over the core of a ghost-ring tile (None: no "
-      "chunk-list form for this depth); sum_form / range as for stencil5_tb");
+      "chunk-list form for this depth); sum_form / range as for stencil5_tb; lead_frac: the exchange's share "
+      "of the pass the schedule assumes; part: both, inner or outer alone");
   m.def("last_pipe_lag1", &kernels::last_pipe_lag1,
         "whether the most recent stencil launch was a pipeline pass in ascending level order");
   m.def(
