@@ -85,10 +85,6 @@ class HaloExchanger {
   void set_copy_block(int threads) { copy_block_ = threads; }
   // Workgroups per copy segment (0 = sized from the segments, or MXS_HALO_GRID).
   void set_copy_grid(int wgs) { copy_grid_ = wgs; }
-  // Dynamic LDS per pack / unpack workgroup (0 = none; kernels::copy2d_batch).
-  void set_copy_lds(int bytes) { copy_lds_ = bytes; }
-  // Copies per pack launch (the grid's second dimension).
-  int pack_segments() const { return progs_.pack.n; }
   // Rehearsal of wire time on one GPU (RCCL loopback): every transfer() is
   // followed by a one-workgroup kernel that holds the stream for `us`
   // microseconds, so the exchange takes as long as an xGMI transfer would.
@@ -104,7 +100,6 @@ class HaloExchanger {
   std::unique_ptr<IpcHaloTransport<T>> ipc_;
   int copy_block_ = 0;
   int copy_grid_ = 0;
-  int copy_lds_ = 0;
   double wire_delay_us_ = 0;
 };
 

@@ -197,7 +197,6 @@ struct ChunkPassShape {
   // read_span) for a group whose first output column is x (its chunks read the
   // ghost columns when that range leaves [0, width)).
   index_t read_lead = 0, read_span = 0;
-  int lds_bytes = 0;   // LDS per workgroup of the chunk-list kernel (static)
 };
 // False when `steps` has no chunk-list form here (fp32 S = 20 / 24, fp64
 // S = 16 on whole lane vectors; other depths keep the one-launch pass). The
@@ -308,13 +307,10 @@ struct Copy2DBatch {
 // kind: which kernel symbol the launch uses (same body): halo_pack_kernel,
 // halo_unpack_kernel or copy2d_batch_kernel, so kernel traces separate the
 // exchange's two sides.
-// lds_bytes: dynamic LDS each workgroup reserves (unused by the body). A
-// reservation larger than what a CU running a pipeline workgroup has left keeps
-// the copies off those CUs: they run only on CUs no pass workgroup holds.
 enum class CopyKind : int { Copy = 0, Pack = 1, Unpack = 2 };
 template <typename T>
 void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x = 0, int block = 0,
-                  CopyKind kind = CopyKind::Copy, int lds_bytes = 0);
+                  CopyKind kind = CopyKind::Copy);
 
 // ---------------------------------------------------------------- dot (K2-K8)
 enum class DotReduce : int {

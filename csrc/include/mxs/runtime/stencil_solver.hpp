@@ -290,12 +290,6 @@ class StencilSolver {
   void force_opening(Opening o);
   // The same for the later super-steps of a call (SolverConfig::steady).
   void force_steady(Opening o);
-  // Where the interior-first super-step's pack / unpack run: true = only on
-  // the CUs the inner launch leaves free (each copy workgroup reserves more LDS
-  // than a CU holding a pipeline workgroup has left), false = beside the inner
-  // launch's workgroups (one-wave workgroups; rounds 3-5).
-  void set_copies_on_free_cus(bool on) { copies_free_cus_ = on; }
-  bool copies_on_free_cus() const { return copies_free_cus_; }
   // Whether the opening super-step of a call at depth S runs interior-first on
   // this rank (the opening is on and the tile has the chunk-list form).
   bool halo_last(int S) const;
@@ -451,7 +445,6 @@ class StencilSolver {
   bool halo_last_allowed_ = false;           // RCCL with remote peers, tuned pipeline forms, no thin strips
   bool halo_last_on_ = false;                // a call's opening super-step runs interior-first
   std::vector<std::unique_ptr<HaloLastPass>> halo_lasts_;
-  bool copies_free_cus_ = false;
   std::vector<int> no_halo_last_;
   // Super-steps exchange AFTER their pass (the ghost ring of the next pass's
   // input): every schedule but the fused periodic, the direct IPC halo and the

@@ -127,7 +127,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_vgpr(32))) void c
 
 template <typename T>
 void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_t s, int grid_x, int block_req,
-                  CopyKind kind, int lds_bytes) {
+                  CopyKind kind) {
   if (b.n <= 0) return;
   MXS_CHECK(b.n <= kMaxCopies, "copy2d_batch: too many copies " << b.n);
   index_t biggest = 0;
@@ -149,33 +149,19 @@ void copy2d_batch(T* slot0, T* slot1, T* slot2, const Copy2DBatch& b, hipStream_
   const index_t want = (biggest + block * kVec - 1) / (block * kVec);
   const index_t cap = std::max<index_t>(64, index_t(4 * kBlock / block) * device_cu_count() / b.n);
   const int gx = grid_x > 0 ? grid_x : int(std::min<index_t>(want, cap));
-  const unsigned lds = unsigned(std::max(0, lds_bytes));
-  auto allow = [lds](const void* fn) {  // dynamic LDS above the default cap needs the attribute
-    if (lds > 65536) MXS_HIP_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, int(lds)));
-  };
   switch (kind) {
-    case CopyKind::Pack:
-      allow(reinterpret_cast<const void*>(halo_pack_kernel<T>));
-      halo_pack_kernel<T><<<dim3(gx, b.n), block, lds, s>>>(slot0, slot1, slot2, b);
-      break;
-    case CopyKind::Unpack:
-      allow(reinterpret_cast<const void*>(halo_unpack_kernel<T>));
-      halo_unpack_kernel<T><<<dim3(gx, b.n), block, lds, s>>>(slot0, slot1, slot2, b);
-      break;
-    default:
-      allow(reinterpret_cast<const void*>(copy2d_batch_kernel<T>));
-      copy2d_batch_kernel<T><<<dim3(gx, b.n), block, lds, s>>>(slot0, slot1, slot2, b);
-      break;
+    case CopyKind::Pack: halo_pack_kernel<T><<<dim3(gx, b.n), block, 0, s>>>(slot0, slot1, slot2, b); break;
+    case CopyKind::Unpack: halo_unpack_kernel<T><<<dim3(gx, b.n), block, 0, s>>>(slot0, slot1, slot2, b); break;
+    default: copy2d_batch_kernel<T><<<dim3(gx, b.n), block, 0, s>>>(slot0, slot1, slot2, b); break;
   }
   MXS_HIP_CHECK_LAUNCH();
 }
 
-template void copy2d_batch<float>(float*, float*, float*, const Copy2DBatch&, hipStream_t, int, int, CopyKind, int);
-template void copy2d_batch<double>(double*, double*, double*, const Copy2DBatch&, hipStream_t, int, int, CopyKind,
-                                   int);
-template void copy2d_batch<int>(int*, int*, int*, const Copy2DBatch&, hipStream_t, int, int, CopyKind, int);
+template void copy2d_batch<float>(float*, float*, float*, const Copy2DBatch&, hipStream_t, int, int, CopyKind);
+template void copy2d_batch<double>(double*, double*, double*, const Copy2DBatch&, hipStream_t, int, int, CopyKind);
+template void copy2d_batch<int>(int*, int*, int*, const Copy2DBatch&, hipStream_t, int, int, CopyKind);
 template void copy2d_batch<unsigned char>(unsigned char*, unsigned char*, unsigned char*, const Copy2DBatch&,
-                                          hipStream_t, int, int, CopyKind, int);
+                                          hipStream_t, int, int, CopyKind);
 
 }  // namespace kernels
 }  // namespace mxs

@@ -24,17 +24,13 @@ constexpr auto chunks_kernel() {
 template <typename T, int S, bool SUM, int JS0, int LAG1>
 void fill_shape(const TileGeom& g, ChunkPassShape* out) {
   constexpr int OWG = JointShape<JS0, S - JS0, kWavesPerBlock>::OWG;
-  static int blocks = 0, lds = 0;
+  static int blocks = 0;
   if (blocks == 0) {
     int occ = 0;
-    const void* fn = reinterpret_cast<const void*>(chunks_kernel<T, S, SUM, JS0, LAG1>());
-    MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, fn, 2 * kBlock, 0));
-    hipFuncAttributes fa{};
-    MXS_HIP_CHECK(hipFuncGetAttributes(&fa, fn));
-    lds = int(fa.sharedSizeBytes);
+    MXS_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &occ, reinterpret_cast<const void*>(chunks_kernel<T, S, SUM, JS0, LAG1>()), 2 * kBlock, 0));
     blocks = std::max(occ, 1) * device_cu_count();
   }
-  out->lds_bytes = lds;
   out->steps = S;
   out->sum = SUM;
   out->js0 = JS0;

@@ -534,13 +534,6 @@ PYBIND11_MODULE(_mxs_hip, m) {
             h.visit([op](auto& s) { s.force_steady(op); });
           },
           py::arg("steady"), "paired measurements: the later super-steps' schedule of the following calls")
-      .def(
-          "set_copies_on_free_cus",
-          [](SolverHandle& h, bool on) { h.visit([on](auto& s) { s.set_copies_on_free_cus(on); }); }, py::arg("on"),
-          "interior-first super-step: pack / unpack only on the CUs the inner launch leaves free (True) or beside "
-          "its workgroups (False)")
-      .def("copies_on_free_cus",
-           [](SolverHandle& h) { return h.visit([](auto& s) { return s.copies_on_free_cus(); }); })
       .def("multi_rank", [](SolverHandle& h) { return h.visit([](auto& s) { return s.multi_rank(); }); },
            "whether the solver follows the peers' schedule (remote peers or a loopback rehearsal)")
       .def("schedule_times",

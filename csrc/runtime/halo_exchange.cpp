@@ -98,7 +98,7 @@ template <typename T>
 void HaloExchanger<T>::pack(T* tile, hipStream_t stream) {
   MXS_TRACE_RANGE("halo.pack");
   kernels::copy2d_batch<T>(tile, send_.get(), recv_.get(), progs_.pack, stream, copy_grid_ > 0 ? copy_grid_ : halo_grid(), copy_block_,
-                           kernels::CopyKind::Pack, copy_lds_);
+                           kernels::CopyKind::Pack);
 }
 
 template <typename T>
@@ -121,7 +121,7 @@ template <typename T>
 void HaloExchanger<T>::unpack(T* tile, hipStream_t stream) {
   MXS_TRACE_RANGE("halo.unpack");
   kernels::copy2d_batch<T>(tile, send_.get(), recv_.get(), progs_.unpack, stream, copy_grid_ > 0 ? copy_grid_ : halo_grid(),
-                           copy_block_, kernels::CopyKind::Unpack, copy_lds_);
+                           copy_block_, kernels::CopyKind::Unpack);
   if (ipc_) ipc_->release(stream);  // receive buffer consumed: senders may write the next exchange
 }
 

@@ -691,20 +691,8 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
   if (marks) marks->mark("side:inner chunks", side);
   side_pending_ = true;
   const int copy_wgs = halo_last_copy_wgs();
-  if (copies_free_cus_ && copy_wgs == 0) {
-    // Copies on the free CUs only: 256-thread workgroups, one per free CU (a
-    // reservation of more LDS than a pipeline CU has left; the whole CU's is
-    // 160 KiB), as many as the outer launch will take, spread over the segments.
-    constexpr int kLdsPerCu = 160 * 1024;
-    const int lds = std::min(kLdsPerCu, kLdsPerCu - hl->inner_shape.lds_bytes + 1024);
-    const int segs = std::max(1, ex_->pack_segments());
-    ex_->set_copy_block(256);
-    ex_->set_copy_grid(std::max(1, hl->sched.outer.blocks / segs));
-    ex_->set_copy_lds(hl->inner_shape.lds_bytes > 0 ? lds : 0);
-  } else {
-    ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
-    ex_->set_copy_grid(copy_wgs);
-  }
+  ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
+  ex_->set_copy_grid(copy_wgs);
   if (marks) {
     marks->mark("main:start", m);
     ex_->pack(cur, m);
@@ -718,7 +706,6 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
   }
   ex_->set_copy_grid(0);
   ex_->set_copy_block(0);
-  ex_->set_copy_lds(0);
   kernels::stencil5_chunk_pass<T>(cur, nxt, tile_, cfg_.coeffs, hl->outer_shape, hl->outer_table.get(),
                                   hl->sched.outer.entries, m);
   if (marks) marks->mark("main:outer chunks", m);

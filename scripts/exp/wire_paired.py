@@ -84,9 +84,6 @@ def main() -> int:
     p.add_argument("--rounds", type=int, default=16)
     p.add_argument("--steady", action="store_true")
     p.add_argument("--warm-ms", type=float, default=100.0)
-    p.add_argument("--copies-ab", action="store_true",
-                   help="add 'ifree': interior-first with the pack / unpack on the free CUs only, and run 'ifirst' "
-                        "with them beside the inner launch")
     args = p.parse_args()
     ctx = dist_init(backend="nccl")
     hip().set_comm_timeout(120.0)
@@ -107,8 +104,7 @@ def main() -> int:
         choice = st.solver.schedule_times()
         decided = choice["steady"] if args.steady else choice["opening"]
         force = st.solver.force_steady if args.steady else st.solver.force_opening
-        names = ["serial", "ifirst", "fused"] + (["ifree"] if args.copies_ab else [])
-        free0 = st.solver.copies_on_free_cus()
+        names = ["serial", "ifirst", "fused"]
         ms = {k: [] for k in names}
         for r in range(args.rounds):
             fused.warm(steps, args.warm_ms / 1e3)  # the bench's clock warm-up, once per round
@@ -118,11 +114,8 @@ def main() -> int:
                     ms[k].append(window(fused, steps))
                 else:
                     force("serial" if k == "serial" else "interior-first")
-                    if args.copies_ab:
-                        st.solver.set_copies_on_free_cus(k == "ifree")
                     ms[k].append(window(st, steps))
         force("auto")
-        st.solver.set_copies_on_free_cus(free0)
         auto = "ifirst" if decided == "interior-first" else "serial"
 
         def ratio(a, b):
@@ -136,9 +129,7 @@ def main() -> int:
                "side_stream": st.solver.stream_note(),
                "median_ms": {k: round(statistics.median(v), 4) for k, v in ms.items()},
                "ratios": {"ifirst/serial": ratio("ifirst", "serial"), "serial/fused": ratio("serial", "fused"),
-                          "ifirst/fused": ratio("ifirst", "fused"), "auto/fused": ratio(auto, "fused"),
-                          **({"ifree/ifirst": ratio("ifree", "ifirst"), "ifree/fused": ratio("ifree", "fused"),
-                              "ifree/serial": ratio("ifree", "serial")} if args.copies_ab else {})},
+                          "ifirst/fused": ratio("ifirst", "fused"), "auto/fused": ratio(auto, "fused")},
                "ms": {k: [round(x, 4) for x in v] for k, v in ms.items()}}
         print(json.dumps(rec), flush=True)
         st.synchronize()

@@ -444,27 +444,3 @@ def test_streams_concurrent_probe_and_solver_side_stream(gpu):
     note = a.solver.stream_note()
     assert note.startswith("side stream on its own") or note.startswith("side stream replaced"), note
     assert H.streams_concurrent(a.solver.side_stream(), a.solver.main_stream()) is True
-
-
-@pytest.mark.parametrize("w,h,dtype,S,runs", [
-    (16384, 8192, "f32", 20, (20,)),        # the 8-GPU tile
-    (4000, 1536, "f32", 24, (24, 24)),      # ragged last group, S = 24
-    (4096, 2048, "f64", 16, (32,)),         # fp64 wide lanes
-])
-@pytest.mark.parametrize("free", [False, True])
-def test_interior_first_copy_placement_bitwise(gpu, w, h, dtype, S, runs, free):
-    """The interior-first super-step's pack / unpack beside the inner launch's
-    workgroups (one-wave copies) or only on the CUs it leaves free (copies that
-    reserve more LDS than a pipeline CU has left): the same field as the serial
-    schedule, bit for bit, either way."""
-    a = _loopback(w, h, dtype, seed=w + 7, opening="interior-first", rehearse_peers=True, time_block=S)
-    b = _loopback(w, h, dtype, seed=w + 7, opening="serial", time_block=S)
-    a.solver.set_copies_on_free_cus(free)
-    assert a.solver.copies_on_free_cus() == free
-    for n in runs:
-        a.run(n)
-        assert a.solver.last_run_opening() == "interior-first"
-        b.run(n)
-    a.synchronize()
-    b.synchronize()
-    assert torch.equal(a.core_view(), b.core_view())
