@@ -21,18 +21,6 @@
 // median + 1.58 IQR / sqrt(n), is below 1 - min_gain (min_gain 0: the notch
 // alone guards against noise). Among candidates the lowest notch is taken.
 //
-// WinRule::Median (the opening decision, since round 6): the lowest-notch
-// candidate wins when its median ratio is at most 1 - min_gain, i.e. also on a
-// tie. The serial opening's window starts its pass only after the host has
-// enqueued pack, the RCCL group and unpack, with the GPU idle in between; the
-// paired samples, taken back to back on a busy host, see less of that host
-// latency than the window does. On the 8-GPU tile the processes whose notch
-// rule kept serial (paired ratios 0.986-1.000) ran their windows at 0.308-0.356
-// ms, those that took interior-first at 0.276-0.294 (30 single shots,
-// profiles/r06_tiles), and a serial window's run() host time varied 17-82 us
-// from process to process (profiles/r06_serial_host). Interior-first launches
-// the inner chunks first and hides that latency.
-enum class WinRule : int { Notch = 0, Median = 1 };
 #pragma once
 
 #include <algorithm>
@@ -46,6 +34,29 @@ namespace mxs {
 // A sample a rank could not take (a candidate it lacks): the element-wise max
 // over ranks carries it, so the candidate drops out for every rank.
 constexpr double kMissingSample = 1e30;
+
+// WinRule::Median (the opening decision on tiles whose exchange is a large
+// share of the pass, kTieLeadFrac; since round 6): the lowest-notch
+// candidate wins when its median ratio is at most 1 - min_gain, i.e. also on a
+// tie. The serial opening's window starts its pass only after the host has
+// enqueued pack, the RCCL group and unpack, with the GPU idle in between; the
+// paired samples, taken back to back on a busy host, see less of that host
+// latency than the window does. On the 8-GPU tile the processes whose notch
+// rule kept serial (paired ratios 0.986-1.000) ran their windows at 0.308-0.356
+// ms, those that took interior-first at 0.276-0.294 (30 single shots,
+// profiles/r06_tiles), and a serial window's run() host time varied 17-82 us
+// from process to process (profiles/r06_serial_host). Interior-first launches
+// the inner chunks first and hides that latency.
+// Only there: on the 2-GPU tile (32768 x 16384, exchange lead ~9% of the pass)
+// the decision's ratios sit at 0.99-1.00 on every box while the windows'
+// interior-first / serial was 1.047 / 1.051 on two boxes and 0.985 on a third
+// (profiles/r06_tie): the interior-first pass runs 5-7% longer than the fused
+// pass in the window, which a short exchange does not repay. The 8-GPU tile's
+// lead is 21% of its pass, the 4-GPU tile's 13%.
+enum class WinRule : int { Notch = 0, Median = 1 };
+constexpr double kTieLeadFrac = 0.11;
+// The opening's rule for a measured exchange lead / pass (0: not measured).
+inline WinRule opening_rule(double lead_frac) { return lead_frac >= kTieLeadFrac ? WinRule::Median : WinRule::Notch; }
 
 // Median and interquartile range of a small sample (sorted in place; 0 / 0 when empty).
 inline std::pair<double, double> median_iqr(std::vector<double>& v) {

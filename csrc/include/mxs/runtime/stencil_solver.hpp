@@ -297,6 +297,9 @@ class StencilSolver {
   // and the statistics of the per-round maxima over ranks it was taken from.
   const std::string& opening_choice() const { return opening_choice_; }
   const std::string& opening_reason() const { return opening_reason_; }
+  // The decision's rule: "median" (a tie goes to interior-first) or "notch"
+  // (decision.hpp: opening_rule); "" before prepare() decided.
+  const std::string& opening_rule() const { return opening_rule_; }
   // prepare()'s steady decision ("" before it decided, "serial" or
   // "interior-first") and why.
   const std::string& steady_choice() const { return steady_choice_; }
@@ -470,6 +473,7 @@ class StencilSolver {
   }
   std::string opening_choice_;               // "" before prepare() decided, "serial" or "interior-first"
   std::string opening_reason_;
+  std::string opening_rule_;
   void choose_opening(int S);                // Opening::Auto: time both, agree, keep the faster
   void choose_steady(int S);                 // SolverConfig::steady Auto: the same for two super-steps
   RoundDecision paired_rounds(int rounds, const std::vector<std::function<double()>>& kinds,

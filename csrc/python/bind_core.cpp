@@ -171,6 +171,12 @@ PYBIND11_MODULE(_mxs_core, m) {
       py::arg("ratios"), py::arg("min_gain") = 0.0,
       "the solver's opening / direct-halo rule on per-round ratios candidate / baseline (runtime/decision.hpp)");
   m.def(
+      "opening_rule",
+      [](double lead_frac) { return opening_rule(lead_frac) == WinRule::Median ? "median" : "notch"; },
+      py::arg("lead_frac"),
+      "the opening decision's rule for a measured exchange lead / pass: median (a tie goes to interior-first) "
+      "or notch");
+  m.def(
       "opening_decision",
       [](const std::vector<std::vector<double>>& serial, const std::vector<std::vector<std::vector<double>>>& cands,
          double min_gain, const std::string& rule) {

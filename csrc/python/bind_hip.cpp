@@ -542,6 +542,7 @@ PYBIND11_MODULE(_mxs_hip, m) {
                py::dict d;
                d["opening"] = s.opening_choice();
                d["reason"] = s.opening_reason();
+               d["rule"] = s.opening_rule();
                d["serial_ms"] = s.opening_serial_ms();
                d["interior_first_ms"] = s.opening_halo_last_ms();
                d["serial_iqr_ms"] = s.opening_serial_spread_ms();

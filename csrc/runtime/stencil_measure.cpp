@@ -270,10 +270,14 @@ void StencilSolver<T>::choose_opening(int S) {
       });
     });
   std::vector<double> local;
-  // Median rule: a tie goes to interior-first (decision.hpp: the window sees the
-  // host's enqueue latency in front of the serial opening's pass).
+  // A tie goes to interior-first where the exchange is a large share of the
+  // pass (decision.hpp: opening_rule; the window sees the host's enqueue
+  // latency in front of the serial opening's pass). lead_frac_ derives from
+  // the agreed lead and pass, so every rank takes the same rule.
+  const WinRule rule = mxs::opening_rule(hl && lead_us_ > 0 && lead_pass_us_ > 0 ? lead_us_ / lead_pass_us_ : 0.0);
+  opening_rule_ = rule == WinRule::Median ? "median" : "notch";
   const RoundDecision d = paired_rounds(nr, kinds, {true, !!cands[0], !!cands[1], !!cands[2]},
-                                        "prepare: opening agreement", &local, WinRule::Median);
+                                        "prepare: opening agreement", &local, rule);
   opening_local_ratio_samples_.clear();  // this rank's own paired ratios (diagnostics)
   for (int c = 0; c < kCands; ++c) {
     if (!cands[c]) continue;
@@ -303,9 +307,10 @@ void StencilSolver<T>::choose_opening(int S) {
   } else {
     std::snprintf(buf, sizeof(buf),
                   "paired ratio of the per-round maxima over %d rank(s), interior-first / serial, %d rounds (host "
-                  "clock, enqueue to drained): median %.3f, IQR %.3f, notch %.3f (switch at median <= %.3f); medians "
+                  "clock, enqueue to drained): median %.3f, IQR %.3f, notch %.3f (switch at %s %s %.3f); medians "
                   "%.4f / %.4f ms: %s; outer set %d workgroups from the measured exchange lead %.1f us of a %.1f us pass",
-                  world_, nr, d.ratio, d.ratio_iqr, d.notch, 1.0 - cfg_.min_gain, d.candidate_ms, d.baseline_ms,
+                  world_, nr, d.ratio, d.ratio_iqr, d.notch, rule == WinRule::Median ? "median" : "notch",
+                  rule == WinRule::Median ? "<=" : "<", 1.0 - cfg_.min_gain, d.candidate_ms, d.baseline_ms,
                   d.win ? "interior-first" : "serial kept", halo_last_outer_wgs(S), lead_us_, lead_pass_us_);
   }
   opening_reason_ = buf;

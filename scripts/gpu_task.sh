@@ -130,7 +130,7 @@ print(json.dumps({"mode": sys.argv[2], "tile": e["tile"], "window_ms": round(d["
                   "choice": {k: (e.get("schedule_choice") or {}).get(k) for k in ("opening", "ratio", "ratio_iqr",
                                                                                    "outer_wgs", "serial_ms",
                                                                                    "interior_first_ms", "lead_us",
-                                                                                   "lead_pass_us", "steady")},
+                                                                                   "lead_pass_us", "steady", "rule")},
                   "phases": e.get("window_phases")}))
 PY
     done

@@ -158,6 +158,16 @@ def test_opening_rule_takes_interior_first_on_a_tie():
     assert med["win"] is True and notch["win"] is False, (med, notch)
 
 
+def test_opening_rule_follows_the_exchange_share():
+    """The tie goes to interior-first only where the measured exchange lead is
+    at least 11% of the pass: the 8-GPU tile (21%) and the 4-GPU tile (13%),
+    not the 2-GPU tile (8-9.5%), whose windows ran interior-first 5% slower on
+    two of three boxes while the decision's ratio said 0.99-1.00
+    (profiles/r06_tie); unmeasured (0) keeps the notch."""
+    assert [C.opening_rule(f) for f in (0.21, 0.127, 0.11, 0.095, 0.079, 0.0)] == \
+        ["median", "median", "median", "notch", "notch", "notch"]
+
+
 def test_opening_rule_keeps_serial_when_interior_first_is_slower():
     rng = random.Random(17)
     serial, cands = [], []
