@@ -290,13 +290,6 @@ class StencilSolver {
   void force_opening(Opening o);
   // The same for the later super-steps of a call (SolverConfig::steady).
   void force_steady(Opening o);
-  // Paired measurements: the interior-first super-step's pack / unpack launch
-  // shape, `block` threads per workgroup (64, 128 or 256) and `grid`
-  // workgroups per copy segment (0: sized from the segments). Default 64 / 0.
-  void set_halo_last_copies(int block, int grid) {
-    hl_copy_block_ = block;
-    hl_copy_grid_ = grid;
-  }
   // Whether the opening super-step of a call at depth S runs interior-first on
   // this rank (the opening is on and the tile has the chunk-list form).
   bool halo_last(int S) const;
@@ -455,7 +448,6 @@ class StencilSolver {
   bool halo_last_allowed_ = false;           // RCCL with remote peers, tuned pipeline forms, no thin strips
   bool halo_last_on_ = false;                // a call's opening super-step runs interior-first
   std::vector<std::unique_ptr<HaloLastPass>> halo_lasts_;
-  int hl_copy_block_ = 64, hl_copy_grid_ = 0;
   std::vector<int> no_halo_last_;
   // Super-steps exchange AFTER their pass (the ghost ring of the next pass's
   // input): every schedule but the fused periodic, the direct IPC halo and the

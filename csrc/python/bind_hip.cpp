@@ -534,16 +534,6 @@ PYBIND11_MODULE(_mxs_hip, m) {
             h.visit([op](auto& s) { s.force_steady(op); });
           },
           py::arg("steady"), "paired measurements: the later super-steps' schedule of the following calls")
-      .def(
-          "set_halo_last_copies",
-          [](SolverHandle& h, int block, int grid) {
-            MXS_CHECK(block == 64 || block == 128 || block == 256, "set_halo_last_copies: block 64|128|256");
-            MXS_CHECK(grid >= 0, "set_halo_last_copies: grid >= 0");
-            h.visit([=](auto& s) { s.set_halo_last_copies(block, grid); });
-          },
-          py::arg("block") = 64, py::arg("grid") = 0,
-          "paired measurements: the interior-first super-step's pack / unpack threads per workgroup and "
-          "workgroups per segment (0: sized from the segments)")
       .def("multi_rank", [](SolverHandle& h) { return h.visit([](auto& s) { return s.multi_rank(); }); },
            "whether the solver follows the peers' schedule (remote peers or a loopback rehearsal)")
       .def("schedule_times",

@@ -691,8 +691,8 @@ void StencilSolver<T>::enqueue_halo_last(T* cur, T* nxt, HaloLastPass* hl, Marks
   if (marks) marks->mark("side:inner chunks", side);
   side_pending_ = true;
   const int copy_wgs = halo_last_copy_wgs();
-  ex_->set_copy_block(copy_wgs > 0 ? 256 : hl_copy_block_);
-  ex_->set_copy_grid(copy_wgs > 0 ? copy_wgs : hl_copy_grid_);
+  ex_->set_copy_block(copy_wgs > 0 ? 256 : 64);
+  ex_->set_copy_grid(copy_wgs);
   if (marks) {
     marks->mark("main:start", m);
     ex_->pack(cur, m);
