@@ -61,7 +61,8 @@ def stamped_passes(launch: Callable[[], None], stream: int, passes: int, warm: i
         clock = statistics.median([m for v in per_xcd.values() for m in v]) if per_xcd else 0.0
         slow = xcd_mhz[0] if xcd_mhz else 0.0
         out.append({"cycles": span_us * slow, "cycles_median_clock": span_us * clock, "us": span_us, "mhz": clock,
-                    "mhz_slowest_xcd": slow, "xcd_spread": (xcd_mhz[-1] / slow - 1.0) if slow else 0.0})
+                    "mhz_slowest_xcd": slow, "xcd_spread": (xcd_mhz[-1] / slow - 1.0) if slow else 0.0,
+                    "xcd_mhz": {k: statistics.median(v) for k, v in sorted(per_xcd.items())}})
     return out
 
 
