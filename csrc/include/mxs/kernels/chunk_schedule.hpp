@@ -94,12 +94,11 @@ std::int64_t min_budget(const std::vector<Run>& runs, int blocks, std::int64_t f
 // empty range.
 //
 // speed (optional, k entries): workgroup w runs at relative speed
-// speed[w % k] and gets a budget of T x speed[w % k] row iterations. With
-// k = 8, w % 8 is the XCD: the pipeline kernel takes slot 8 (b / 8) + XCD for
-// its workgroup b (PipeShares::xcd), and the XCDs run at clocks 2-8% apart
-// within one pass (profiles/r06_fill, r06_xcd): shares in proportion to each
-// XCD's measured clock end every XCD together instead of waiting for the
-// slowest.
+// speed[w % k] and gets a budget of T x speed[w % k] row iterations. The
+// hardware deals a launch's workgroups round-robin over the 8 XCDs (workgroup
+// w on XCD w % 8), and the XCDs run at clocks 2-8% apart within one pass
+// (profiles/r06_fill, r06_xcd): shares in proportion to each XCD's measured
+// clock end every XCD together instead of waiting for the slowest.
 inline std::vector<std::int64_t> balanced_starts(std::int64_t groups, std::int64_t rows, int blocks,
                                                  std::int64_t fill, const std::vector<double>& speed = {}) {
   std::vector<detail::Run> runs;

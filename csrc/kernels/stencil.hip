@@ -419,7 +419,6 @@ void pipe_starts(index_t groups, index_t rows, int blocks, index_t fill, PipeSha
     index_t groups, rows, fill;
     int blocks, gen;
     std::vector<std::int64_t> start;
-    bool xcd;
   };
   thread_local std::vector<Entry> cache;
   const int gen = g_xcd_gen.load(std::memory_order_relaxed);
@@ -430,11 +429,10 @@ void pipe_starts(index_t groups, index_t rows, int blocks, index_t fill, PipeSha
     if (cache.size() >= 16) cache.erase(cache.begin());
     // XCD weights only where every XCD holds the same number of workgroups.
     std::vector<double> w = blocks % kNumXCDs == 0 ? xcd_weights() : std::vector<double>{};
-    cache.push_back(Entry{groups, rows, fill, blocks, gen, balanced_starts(groups, rows, blocks, fill, w), !w.empty()});
+    cache.push_back(Entry{groups, rows, fill, blocks, gen, balanced_starts(groups, rows, blocks, fill, w)});
     hit = &cache.back();
   }
   out->n = blocks;
-  out->xcd = hit->xcd ? 1 : 0;
   for (int w = 0; w <= blocks; ++w) out->start[w] = int(hit->start[size_t(w)]);
 }
 void note_dispatch(const char* k) { note(k); }

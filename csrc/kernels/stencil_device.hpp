@@ -1474,16 +1474,9 @@ __device__ __forceinline__ void pipe_chunk(const typename B::T* __restrict__ in,
 // in the kernel arguments (2 KB), so a launch needs no device table and stays
 // graph-capturable.
 constexpr int kMaxShareBlocks = 512;
-// xcd = 1 (per-XCD weighted starts, kernels::set_xcd_weights): start[] is
-// indexed by (XCD, position on it), slot 8 * (w / 8) + XCD for workgroup w. The
-// hardware deals a launch's workgroups round-robin over the 8 XCDs from an
-// offset that depends on the queue's earlier dispatches (workgroup w on XCD
-// (w + offset) % 8), so the workgroups with one w / 8 sit on 8 distinct XCDs
-// and the slot map is a bijection whatever the offset (grid a multiple of 8).
 struct PipeShares {
   index_t share = 0;
   int n = 0;
-  int xcd = 0;
   int start[kMaxShareBlocks + 1];
   static PipeShares equal(index_t share) {
     PipeShares p;
@@ -1516,10 +1509,6 @@ __global__ __launch_bounds__(2 * G * kWaveSize) void stencil5_stream_pipe_kernel
   index_t slot = blockIdx.x;
   if constexpr (XM) {
     if (gridDim.x % kNumXcds == 0) slot = (blockIdx.x % kNumXcds) * (gridDim.x / kNumXcds) + blockIdx.x / kNumXcds;
-  }
-  if (shares.xcd) {  // workgroup-uniform; HW_REG_XCC_ID[3:0]
-    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & unsigned(kNumXcds - 1);
-    slot = (index_t(blockIdx.x) & ~index_t(kNumXcds - 1)) | index_t(xcc);
   }
   index_t a, b;
   if (shares.n > 0) {

@@ -858,22 +858,14 @@ void StencilSolver<T>::update_xcd_weights() {
     return;
   }
   std::map<unsigned long long, std::pair<unsigned long long, unsigned long long>> before;
-  // Round-robin from some offset: workgroup b on XCD (b + offset) % 8 (the
-  // offset follows the queue's earlier dispatches; the pipeline kernel reads its
-  // XCD itself, stencil_device.hpp PipeShares::xcd).
   bool round_robin = true;
-  const int off0 = (int(h[0] >> 16) % kXcds + kXcds) % kXcds, off1 = int(h[size_t(rec)] >> 16) % kXcds;
   for (int b = 0; b < kernels::kClockStampWgs; ++b) {
     const unsigned long long* r = h.data() + 3 * b;
-    round_robin = round_robin && int(r[0] >> 16) == (b + off0) % kXcds && int(r[rec] >> 16) == (b + off1) % kXcds;
+    round_robin = round_robin && int(r[0] >> 16) == b % kXcds && int(r[rec] >> 16) == b % kXcds;
     before[r[0]] = {r[1], r[2]};
   }
   if (!round_robin) {
-    std::string seen;
-    for (int b = 0; b < 16; ++b) seen += std::to_string(int(h[size_t(3 * b)] >> 16)) + "/" +
-                                        std::to_string(int(h[size_t(rec + 3 * b)] >> 16)) + " ";
-    xcd_note_ = "workgroups not dealt round-robin over the XCDs (XCD of stamp workgroups 0-15, before/after: " +
-                seen + "): equal shares";
+    xcd_note_ = "workgroups not dealt round-robin over the XCDs: equal shares";
     kernels::set_xcd_weights({});
     return;
   }
