@@ -525,11 +525,7 @@ def main(argv=None) -> int:
         # Level order of the last pipeline pass (bottom-up on short chunks).
         extras["pipe_level_order"] = "bottom-up" if H.last_pipe_lag1() else "top-down"
         extras["pipe_balanced_shares"] = bool(H.pipe_balanced())
-        # Per-XCD weights of those shares, from the XCDs' clocks over the last warm pass.
-        extras["xcd_weights"] = [round(w, 4) for w in H.xcd_weights()]
         if st.solver is not None:
-            extras["xcd_clocks_mhz"] = [round(c) for c in st.solver.xcd_clocks()]
-            extras["xcd_note"] = st.solver.xcd_note()
             extras["opening"] = st.solver.last_run_opening()
             # How the ranks agreed on the time block, the opening and the sum-form range.
             extras["agreement"] = st.solver.agreement_path()

@@ -92,24 +92,14 @@ std::int64_t min_budget(const std::vector<Run>& runs, int blocks, std::int64_t f
 // Linear start index (group * rows + row) of each workgroup's range, blocks + 1
 // entries (the last = groups * rows); a workgroup with nothing to do has an
 // empty range.
-//
-// speed (optional, k entries): workgroup w runs at relative speed
-// speed[w % k] and gets a budget of T x speed[w % k] row iterations. The
-// hardware deals a launch's workgroups round-robin over the 8 XCDs (workgroup
-// w on XCD w % 8), and the XCDs run at clocks 2-8% apart within one pass
-// (profiles/r06_fill, r06_xcd): shares in proportion to each XCD's measured
-// clock end every XCD together instead of waiting for the slowest.
 inline std::vector<std::int64_t> balanced_starts(std::int64_t groups, std::int64_t rows, int blocks,
-                                                 std::int64_t fill, const std::vector<double>& speed = {}) {
+                                                 std::int64_t fill) {
   std::vector<detail::Run> runs;
   for (std::int64_t g = 0; g < groups; ++g) runs.push_back(detail::Run{std::int32_t(g), 0, rows});
-  auto budget_t = [&speed](int w, std::int64_t t) {
-    return speed.empty() ? t : std::int64_t(double(t) * speed[size_t(w) % speed.size()]);
-  };
-  const std::int64_t T = detail::min_budget(runs, blocks, fill, budget_t);
+  const std::int64_t T = detail::min_budget(runs, blocks, fill, [](int, std::int64_t t) { return t; });
   std::vector<std::int64_t> start(size_t(blocks) + 1, groups * rows);
   std::vector<std::uint8_t> seen(size_t(blocks), 0);
-  detail::greedy_walk(runs, blocks, fill, [&](int w) { return budget_t(w, T); },
+  detail::greedy_walk(runs, blocks, fill, [&](int) { return T; },
                       [&](int w, std::int32_t g, std::int64_t r0, std::int64_t) {
                         if (!seen[size_t(w)]) {
                           seen[size_t(w)] = 1;

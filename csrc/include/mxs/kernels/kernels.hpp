@@ -264,12 +264,6 @@ bool last_pipe_lag1();
 // the pass time. MXS_PIPE_BALANCED=0 restores equal shares. Bitwise equal output.
 void set_pipe_balanced(bool on);
 bool pipe_balanced_on();
-// Per-XCD speed weights of those shares (chunk_schedule.hpp: balanced_starts'
-// speed; 8 entries, normalised to mean 1; empty = equal). Set from the XCDs'
-// measured clocks (StencilSolver::warm, xcd_balance); process-wide, as the
-// GPU is. Bitwise equal output: only which workgroup computes a row changes.
-void set_xcd_weights(const std::vector<double>& w);
-std::vector<double> xcd_weights();
 
 // Kernel form chosen by the most recent stencil launcher on this host process:
 // "stream_pipe" (the two-stage pipeline: fp32 blocks > 16 steps, the one the

@@ -233,16 +233,7 @@ class StencilSolver {
   // brings the device to its sustained clocks before a short timed window
   // (a cold 20-step window at 32768^2 runs ~20% slower than a warm one,
   // profiles/r02_deep/clock_ramp.txt). Collective: same passes on all ranks.
-  // With xcd_balance on (default), the last warm pass is bracketed by clock
-  // stamps and the XCDs' measured clocks become the pipeline shares' per-XCD
-  // weights (kernels::set_xcd_weights) for the passes that follow.
   void warm(int iters, int passes);
-  void set_xcd_balance(bool on) { xcd_balance_ = on; }
-  bool xcd_balance() const { return xcd_balance_; }
-  // Median shader clock (MHz) per XCD over the last stamped warm pass (empty:
-  // not measured) and why weights were or were not set.
-  const std::vector<double>& xcd_clocks() const { return xcd_clocks_; }
-  const std::string& xcd_note() const { return xcd_note_; }
   // Collective, state-preserving: one untimed replica of run(iters)'s opening
   // super-step (priming exchange + pass, or the interior-first opening) with a
   // GPU event between its phases, from drained streams after a device barrier
@@ -518,11 +509,6 @@ class StencilSolver {
   std::string sum_note_;
   DeviceBuffer<T> absmax_;
   DeviceBuffer<double> agree_buf_;
-  bool xcd_balance_ = true;
-  DeviceBuffer<unsigned long long> stamps_;  // two clock_stamp records
-  std::vector<double> xcd_clocks_;
-  std::string xcd_note_;
-  void update_xcd_weights();
   std::vector<std::pair<int, int>> last_blocks_;
   std::string stall_phase_;
   double stall_s_ = 0;

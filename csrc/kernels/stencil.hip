@@ -38,7 +38,6 @@
 #include <atomic>
 #include <cmath>
 #include <limits>
-#include <mutex>
 #include <cstdlib>
 #include <string>
 #include <vector>
@@ -391,45 +390,21 @@ bool pipe_lag1() { return g_pipe_lag1.load(std::memory_order_relaxed); }
 bool last_pipe_lag1() { return g_last_lag1.load(std::memory_order_relaxed); }
 void set_pipe_balanced(bool on) { g_pipe_balanced.store(on, std::memory_order_relaxed); }
 bool pipe_balanced_on() { return g_pipe_balanced.load(std::memory_order_relaxed); }
-namespace {
-std::mutex g_xcd_mutex;
-std::vector<double> g_xcd_weights;   // guarded by g_xcd_mutex
-std::atomic<int> g_xcd_gen{0};       // bumped on every change (pipe_starts' memo key)
-}  // namespace
-void set_xcd_weights(const std::vector<double>& w) {
-  std::vector<double> n;
-  double sum = 0;
-  for (double v : w) sum += v;
-  const bool ok = w.size() == size_t(kNumXCDs) && sum > 0 &&
-                  std::all_of(w.begin(), w.end(), [](double v) { return std::isfinite(v) && v > 0; });
-  if (ok)
-    for (double v : w) n.push_back(v * double(w.size()) / sum);
-  std::lock_guard<std::mutex> lk(g_xcd_mutex);
-  g_xcd_weights = n;
-  g_xcd_gen.fetch_add(1, std::memory_order_relaxed);
-}
-std::vector<double> xcd_weights() {
-  std::lock_guard<std::mutex> lk(g_xcd_mutex);
-  return g_xcd_weights;
-}
 namespace detail {
 bool pipe_balanced() { return g_pipe_balanced.load(std::memory_order_relaxed); }
 void pipe_starts(index_t groups, index_t rows, int blocks, index_t fill, PipeShares* out) {
   struct Entry {
     index_t groups, rows, fill;
-    int blocks, gen;
+    int blocks;
     std::vector<std::int64_t> start;
   };
   thread_local std::vector<Entry> cache;
-  const int gen = g_xcd_gen.load(std::memory_order_relaxed);
   const Entry* hit = nullptr;
   for (const auto& e : cache)
-    if (e.groups == groups && e.rows == rows && e.fill == fill && e.blocks == blocks && e.gen == gen) hit = &e;
+    if (e.groups == groups && e.rows == rows && e.fill == fill && e.blocks == blocks) hit = &e;
   if (!hit) {
     if (cache.size() >= 16) cache.erase(cache.begin());
-    // XCD weights only where every XCD holds the same number of workgroups.
-    std::vector<double> w = blocks % kNumXCDs == 0 ? xcd_weights() : std::vector<double>{};
-    cache.push_back(Entry{groups, rows, fill, blocks, gen, balanced_starts(groups, rows, blocks, fill, w)});
+    cache.push_back(Entry{groups, rows, fill, blocks, balanced_starts(groups, rows, blocks, fill)});
     hit = &cache.back();
   }
   out->n = blocks;

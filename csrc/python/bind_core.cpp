@@ -217,9 +217,7 @@ PYBIND11_MODULE(_mxs_core, m) {
       "(runtime/decision.hpp); missing slots: kMissingSample");
   m.attr("MISSING_SAMPLE") = kMissingSample;
   m.def("balanced_starts", &kernels::balanced_starts, py::arg("groups"), py::arg("rows"), py::arg("blocks"),
-        py::arg("fill"), py::arg("speed") = std::vector<double>{},
-        "fill-aware linear starts of the pipeline workgroups' shares (blocks + 1 entries); speed: per-XCD "
-        "relative speeds (workgroup w runs at speed[w % len(speed)])");
+        py::arg("fill"), "fill-aware linear starts of the pipeline workgroups' shares (blocks + 1 entries)");
   // Interior-first (halo-last) schedule of the multi-GPU opening super-step.
   m.def(
       "halo_last_schedule",

@@ -183,9 +183,6 @@ PYBIND11_MODULE(_mxs_hip, m) {
   m.def("set_pipe_balanced", &kernels::set_pipe_balanced, py::arg("on"),
         "fill-aware workgroup shares in the pipeline passes (default on; bitwise equal output)");
   m.def("pipe_balanced", &kernels::pipe_balanced_on);
-  m.def("set_xcd_weights", &kernels::set_xcd_weights, py::arg("weights"),
-        "per-XCD speed weights of the pipeline shares (8 entries, normalised; [] = equal shares; bitwise equal output)");
-  m.def("xcd_weights", &kernels::xcd_weights, "the pipeline shares' per-XCD weights in use ([] = equal)");
   m.def(
       "absmax",
       [](std::uintptr_t x, index_t n, const std::string& dt) {
@@ -537,13 +534,6 @@ PYBIND11_MODULE(_mxs_hip, m) {
             h.visit([op](auto& s) { s.force_steady(op); });
           },
           py::arg("steady"), "paired measurements: the later super-steps' schedule of the following calls")
-      .def(
-          "set_xcd_balance", [](SolverHandle& h, bool on) { h.visit([on](auto& s) { s.set_xcd_balance(on); }); },
-          py::arg("on"), "weight the pipeline shares by the XCDs' clocks measured over the last warm pass (default on)")
-      .def("xcd_balance", [](SolverHandle& h) { return h.visit([](auto& s) { return s.xcd_balance(); }); })
-      .def("xcd_clocks", [](SolverHandle& h) { return h.visit([](auto& s) { return s.xcd_clocks(); }); },
-           "median shader clock (MHz) per XCD over the last stamped warm pass ([]: not measured)")
-      .def("xcd_note", [](SolverHandle& h) { return h.visit([](auto& s) { return s.xcd_note(); }); })
       .def("multi_rank", [](SolverHandle& h) { return h.visit([](auto& s) { return s.multi_rank(); }); },
            "whether the solver follows the peers' schedule (remote peers or a loopback rehearsal)")
       .def("schedule_times",

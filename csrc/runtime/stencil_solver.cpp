@@ -1,7 +1,6 @@
 #include "mxs/runtime/stencil_solver.hpp"
 
 #include <algorithm>
-#include <map>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -806,22 +805,9 @@ void StencilSolver<T>::warm(int iters, int passes) {
     prime_exchange();
     ghost_fresh_ = true;
   }
-  const index_t rec = 3 * kernels::kClockStampWgs;
-  const bool stamp = xcd_balance_ && passes > 0;
-  if (stamp && stamps_.size() < 2 * rec) stamps_.reset(2 * rec);
-  for (int p = 0; p < passes; ++p) {
-    const bool last = stamp && p == passes - 1;
-    if (last) {
-      join_side();
-      kernels::clock_stamp(stamps_.get(), main_.get());
-    }
+  for (int p = 0; p < passes; ++p)
     for (const Group& g : gr)
       if (g.count > 0) enqueue_block(cur_, nxt_, g.S);  // cur -> nxt, no swap: state unchanged
-    if (last) {
-      join_side();
-      kernels::clock_stamp(stamps_.get() + rec, main_.get());
-    }
-  }
   // End on the opening's own shape (cur -> nxt, one exchange on every rank):
   // a short window is that super-step, so its launches (both chunk-list
   // passes, the copies beside them) and both streams are the last thing warmed.
@@ -832,63 +818,6 @@ void StencilSolver<T>::warm(int iters, int passes) {
   }
   join_side();
   wait_idle("warm");
-  if (stamp) update_xcd_weights();
-}
-
-// Per-XCD clocks of the last stamped warm pass -> the pipeline shares' XCD
-// weights. Each CU's clock is its shader-clock delta over the wall-clock delta
-// between the two stamps; an XCD's clock is the median over its CUs. The
-// weights assume the hardware's round-robin deal (workgroup b on XCD b % 8):
-// the stamp launch itself is checked for it, and nothing is set when it does
-// not hold. Host-only arithmetic after the warm-up's own synchronisation.
-template <typename T>
-void StencilSolver<T>::update_xcd_weights() {
-  const index_t rec = 3 * kernels::kClockStampWgs;
-  std::vector<unsigned long long> h(size_t(2 * rec));
-  MXS_HIP_CHECK(hipMemcpy(h.data(), stamps_.get(), h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-  static const double khz = [] {
-    int dev = 0, v = 0;
-    MXS_HIP_CHECK(hipGetDevice(&dev));
-    MXS_HIP_CHECK(hipDeviceGetAttribute(&v, hipDeviceAttributeWallClockRate, dev));
-    return double(v);
-  }();
-  xcd_clocks_.clear();
-  if (khz <= 0) {
-    xcd_note_ = "no wall clock rate";
-    return;
-  }
-  std::map<unsigned long long, std::pair<unsigned long long, unsigned long long>> before;
-  bool round_robin = true;
-  for (int b = 0; b < kernels::kClockStampWgs; ++b) {
-    const unsigned long long* r = h.data() + 3 * b;
-    round_robin = round_robin && int(r[0] >> 16) == b % kXcds && int(r[rec] >> 16) == b % kXcds;
-    before[r[0]] = {r[1], r[2]};
-  }
-  if (!round_robin) {
-    xcd_note_ = "workgroups not dealt round-robin over the XCDs: equal shares";
-    kernels::set_xcd_weights({});
-    return;
-  }
-  std::vector<std::vector<double>> per(kXcds);
-  for (int b = 0; b < kernels::kClockStampWgs; ++b) {
-    const unsigned long long* r = h.data() + rec + 3 * b;
-    const auto it = before.find(r[0]);
-    if (it == before.end() || r[2] <= it->second.second || r[1] <= it->second.first) continue;
-    const double us = double(r[2] - it->second.second) / (khz / 1e3);
-    per[size_t(r[0] >> 16)].push_back(double(r[1] - it->second.first) / us);
-  }
-  for (auto& v : per) {
-    if (v.empty()) {
-      xcd_clocks_.clear();
-      xcd_note_ = "an XCD without a stamped CU: equal shares";
-      kernels::set_xcd_weights({});
-      return;
-    }
-    std::sort(v.begin(), v.end());
-    xcd_clocks_.push_back(v[v.size() / 2]);
-  }
-  kernels::set_xcd_weights(xcd_clocks_);
-  xcd_note_ = "shares weighted by the XCDs' clocks of the last warm pass";
 }
 
 template <typename T>

@@ -94,11 +94,6 @@ class StencilConfig:
     # opening), or "auto" (prepare() of a call with >= 2 super-steps times both
     # and all ranks adopt the faster).
     steady: str = "auto"
-    # warm() measures the XCDs' clocks over its last pass and weights the
-    # pipeline shares by them, so the XCDs end a pass together instead of the
-    # fast ones waiting for the slowest (kernels::set_xcd_weights; bitwise
-    # equal output).
-    xcd_balance: bool = True
     # Single GPU with loopback: follow the peers' schedule (every call primes,
     # the last pass of a call is bare, the opening is chosen as with peers), so
     # one GPU rehearses the window an N-GPU run executes.
@@ -242,7 +237,6 @@ class Stencil2D:
                                           cfg.graph_max_superstep_us, cfg.opening, cfg.rehearse_peers, cfg.min_gain,
                                           cfg.halo_max_ctas, cfg.main_priority, cfg.side_priority,
                                           cfg.wire_delay_us, cfg.direct_engine, cfg.steady)
-            self.solver.set_xcd_balance(bool(cfg.xcd_balance))
             # The solver may cap the request (blocks > 16 need the fp32 pipeline's
             # preconditions); the ghost ring was sized for the request.
             self.time_block = self.solver.time_block()

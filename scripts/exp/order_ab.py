@@ -10,11 +10,7 @@ the median clock. The order alternates first/second from round to round.
 Prints per tile the paired ratios asc / desc (median, notch) of wall time and
 of cycles.
 
---ab xcd: the same paired windows with the shares weighted by the XCDs'
-clocks over the last warm pass (A: xcd_balance on, the default) against equal
-shares (B: off), the ratio reported as asc / desc = weighted / equal.
-
-usage: python scripts/exp/order_ab.py [--tiles 32768x32768,16384x16384] [--rounds 12] [--steps 20] [--ab order|xcd]
+usage: python scripts/exp/order_ab.py [--tiles 32768x32768,16384x16384] [--rounds 12] [--steps 20]
 """
 import argparse
 import json
@@ -46,7 +42,6 @@ def main() -> int:
     p.add_argument("--tiles", default="32768x32768,16384x16384")
     p.add_argument("--rounds", type=int, default=12)
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--ab", default="order", choices=["order", "xcd"])
     args = p.parse_args()
     H = hip()
     K = H.clock_stamp_slots()
@@ -61,11 +56,7 @@ def main() -> int:
         res = {True: [], False: []}
         for r in range(args.rounds):
             for lag in ((True, False) if r % 2 == 0 else (False, True)):
-                if args.ab == "order":
-                    H.set_pipe_lag1(lag)
-                else:
-                    st.solver.set_xcd_balance(lag)
-                    H.set_xcd_weights([])
+                H.set_pipe_lag1(lag)
                 st.warm(args.steps, 0.2, 1)
                 st.synchronize()
                 torch.cuda.synchronize()
@@ -76,7 +67,7 @@ def main() -> int:
                 st.synchronize()
                 torch.cuda.synchronize()
                 wall = (time.perf_counter() - t0) * 1e3
-                used = bool(H.last_pipe_lag1()) if args.ab == "order" else bool(H.xcd_weights())
+                used = bool(H.last_pipe_lag1())
                 H.clock_stamp(stamps.data_ptr() + 3 * K * 8, s)
                 torch.cuda.synchronize()
                 v = stamps.cpu().view(2, K, 3).tolist()
@@ -91,9 +82,8 @@ def main() -> int:
                 res[lag].append({"wall_ms": wall, "kcycles_slowest": wall * 1e3 * slow / 1e3, "mhz": med,
                                  "mhz_slowest": slow, "lag1_used": used})
         H.set_pipe_lag1(True)
-        st.solver.set_xcd_balance(True)
         a, d = res[True], res[False]
-        rec = {"tile": tile, "ab": args.ab, "steps": args.steps, "rounds": args.rounds,
+        rec = {"tile": tile, "steps": args.steps, "rounds": args.rounds,
                "asc_wall_ms": round(statistics.median(x["wall_ms"] for x in a), 4),
                "desc_wall_ms": round(statistics.median(x["wall_ms"] for x in d), 4),
                "asc_mhz": round(statistics.median(x["mhz"] for x in a)),

@@ -31,9 +31,6 @@ def main() -> int:
     p = argparse.ArgumentParser()
     p.add_argument("--passes", type=int, default=24)
     p.add_argument("--size", type=int, default=32768)
-    p.add_argument("--bench-flow", type=int, default=0,
-                   help="instead: N times the bench's shape (200 ms burst, sync, one stamped tail pass, sync, one "
-                        "stamped 'timed' pass) and the gain of shares from the tail pass's clocks")
     args = p.parse_args()
     n, S = args.size, 20
     g = core().TileGeom.aligned(n, n, S, S, 4)
@@ -44,35 +41,6 @@ def main() -> int:
     def launch():
         hip().stencil5_tb(a.data_ptr(), b.data_ptr(), g, S, 0, n, 0, n, 0.2, 0.2, True, "f32", s, "auto", True)
 
-    if args.bench_flow:
-        got = []
-        for rep in range(args.bench_flow):
-            t0 = time.perf_counter()
-            k = 0
-            while time.perf_counter() - t0 < 0.2:
-                launch()
-                k += 1
-                if k % 16 == 0:
-                    torch.cuda.synchronize()
-            torch.cuda.synchronize()
-            tail = stamped_passes(launch, s, 1, warm=0)[0]["xcd_mhz"]
-            torch.cuda.synchronize()
-            timed = stamped_passes(launch, s, 1, warm=0)[0]
-            mhz = timed["xcd_mhz"]
-            if set(tail) != set(mhz):
-                continue
-            slow = min(mhz.values())
-            st = sum(tail.values())
-            t = max((tail[k] / st) / mhz[k] for k in mhz) * len(mhz) * slow
-            now = slow * len(mhz) / sum(mhz.values())
-            got.append(t)
-            print(json.dumps({"rep": rep, "timed_us": round(timed["us"], 1), "tail_mhz": {k: round(v) for k, v in tail.items()},
-                              "timed_mhz": {k: round(v) for k, v in mhz.items()}, "proportional_now": round(now, 4),
-                              "proportional_tail": round(t, 4)}), flush=True)
-        print(json.dumps({"summary": True, "bench_flow": len(got),
-                          "proportional_tail_median": round(statistics.median(got), 4) if got else None,
-                          "proportional_tail_max": round(max(got), 4) if got else None}))
-        return 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.2:
         launch()

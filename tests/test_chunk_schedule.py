@@ -55,31 +55,6 @@ def test_balanced_starts_8192_gain():
     assert max(old) == 382 and max(costs) <= 340
 
 
-SPEEDS = [  # per-XCD clocks of one bench-flow pass (MHz, profiles/r06_xcd), and a flat set
-    [1993, 1906, 2038, 1956, 1987, 1955, 1962, 1909], [1.0] * 8,
-]
-
-
-@pytest.mark.parametrize("groups,rows,blocks,fill", [s for s in SHAPES if s[2] % 8 == 0])
-@pytest.mark.parametrize("speed", SPEEDS)
-def test_xcd_weighted_starts_cover_and_end_together(groups, rows, blocks, fill, speed):
-    """Shares weighted by per-XCD speed (workgroup w on XCD w % 8) still cover
-    every row once in order, and each workgroup's time (cost / speed) stays
-    within one fill + a row of the weighted optimum, below the equal-cost
-    split's slowest XCD whenever the clocks differ."""
-    mean = sum(speed) / len(speed)
-    sp = [v / mean for v in speed]
-    st = C.balanced_starts(groups, rows, blocks, fill, sp)
-    assert len(st) == blocks + 1 and st[0] == 0 and st[-1] == groups * rows
-    assert all(a <= b for a, b in zip(st, st[1:]))
-    t_w = max(c / sp[w % 8] for w, c in enumerate(_chunk_costs(st, groups, rows, fill)) if c)
-    t_eq = max(c / sp[w % 8] for w, c in enumerate(_chunk_costs(C.balanced_starts(groups, rows, blocks, fill),
-                                                                groups, rows, fill)) if c)
-    assert t_w <= t_eq + 1e-9
-    if len(set(speed)) > 1 and groups * rows >= 8 * blocks * fill:
-        assert t_w < 0.99 * t_eq
-
-
 def _ghost(groups):
     return [1] + [0] * (groups - 2) + [1] if groups > 1 else [1]
 

@@ -220,62 +220,6 @@ def test_balanced_shares_bitwise(gpu, w, h, steps, wrap, dtype):
     assert torch.equal(outs[0], outs[1])
 
 
-@pytest.mark.parametrize("w,h,steps,wrap,dtype", [
-    (8192, 8192, 20, True, "f32"),
-    (16384, 2048, 20, False, "f32"),
-    (4096, 2048, 16, True, "f64"),
-])
-def test_xcd_weighted_shares_bitwise(gpu, w, h, steps, wrap, dtype):
-    """Shares weighted by per-XCD clocks move chunk boundaries only: bitwise the
-    equal-weight pass (kernels::set_xcd_weights)."""
-    tdt = torch.float32 if dtype == "f32" else torch.float64
-    g = core().TileGeom.aligned(w, h, 1 if wrap else steps, 1 if wrap else steps, tdt.itemsize)
-    gen = torch.Generator(device=gpu).manual_seed(w + steps + 5)
-    src = torch.rand(g.alloc_elems(), generator=gen, device=gpu, dtype=torch.float64).to(tdt)
-    outs = []
-    old = hip().xcd_weights()
-    try:
-        for wts in ([1.06, 0.95, 1.08, 0.97, 1.0, 0.96, 1.01, 0.97], []):
-            hip().set_xcd_weights(wts)
-            assert bool(hip().xcd_weights()) == bool(wts)
-            dst = torch.full_like(src, -3.0)
-            hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, steps, 0, w, 0, h, 0.2, 0.2, wrap, dtype,
-                              torch.cuda.current_stream().cuda_stream, "auto", True)
-            torch.cuda.synchronize()
-            outs.append(dst)
-    finally:
-        hip().set_xcd_weights(old)
-    assert torch.equal(outs[0], outs[1])
-
-
-def test_warm_measures_xcd_clocks_and_sets_weights(gpu):
-    """warm() stamps its last pass: eight XCD clocks, the stamp launch dealt
-    round-robin over the XCDs, and the weights (normalised clocks) in use; with
-    xcd_balance off it measures nothing. The field is unchanged either way."""
-    st = Stencil2D(StencilConfig(global_width=4096, global_height=4096, dims="1x1", dtype="f32", seed=5))
-    ref = Stencil2D(StencilConfig(global_width=4096, global_height=4096, dims="1x1", dtype="f32", seed=5,
-                                  xcd_balance=False))
-    old = hip().xcd_weights()
-    try:
-        hip().set_xcd_weights([])
-        ref.warm(20, 0.01, 1)
-        assert ref.solver.xcd_clocks() == [] and hip().xcd_weights() == []
-        st.warm(20, 0.01, 1)
-        clocks = st.solver.xcd_clocks()
-        assert len(clocks) == 8 and all(500 < c < 4000 for c in clocks), (clocks, st.solver.xcd_note())
-        wts = hip().xcd_weights()
-        assert len(wts) == 8 and abs(sum(wts) - 8.0) < 1e-9
-        mean = sum(clocks) / 8
-        assert all(abs(wv - c / mean) < 1e-9 for wv, c in zip(wts, clocks))
-        st.run(40)
-        ref.run(40)
-        st.synchronize()
-        ref.synchronize()
-        assert torch.equal(st.core_view(), ref.core_view())
-    finally:
-        hip().set_xcd_weights(old)
-
-
 def test_auto_opening_is_recorded_thresholded_and_exact(gpu):
     """Default (opening auto): prepare() times the serial and interior-first
     openings on the real path (here RCCL loopback in the peers' schedule), in
