@@ -272,9 +272,9 @@ void StencilSolver<T>::choose_opening(int S) {
   std::vector<double> local;
   // A tie goes to interior-first where the exchange is a large share of the
   // pass (decision.hpp: opening_rule; the window sees the host's enqueue
-  // latency in front of the serial opening's pass). lead_frac_ derives from
-  // the agreed lead and pass, so every rank takes the same rule.
-  const WinRule rule = mxs::opening_rule(hl && lead_us_ > 0 && lead_pass_us_ > 0 ? lead_us_ / lead_pass_us_ : 0.0);
+  // latency in front of the serial opening's pass). The lead and the pass are
+  // agreed values (max over ranks), so every rank takes the same rule.
+  const WinRule rule = mxs::opening_rule(lead_us_ > 0 && lead_pass_us_ > 0 ? lead_us_ / lead_pass_us_ : 0.0);
   opening_rule_ = rule == WinRule::Median ? "median" : "notch";
   const RoundDecision d = paired_rounds(nr, kinds, {true, !!cands[0], !!cands[1], !!cands[2]},
                                         "prepare: opening agreement", &local, rule);
