@@ -61,6 +61,29 @@ def test_chunk_pass_bitwise_vs_one_launch(gpu, w, h, S, dtype, sum_form):
     assert torch.equal(got, ref)
 
 
+def test_chunk_pass_parts_compose(gpu):
+    """The interior-first pass's two launches one at a time (part="inner", then
+    "outer", as scripts/exp/inner_alone.py times them) write what both together
+    write, for the schedule of any lead share."""
+    w, h, S = 16384, 2048, 20
+    g = core().TileGeom.aligned(w, h, S, S, 4)
+    src = torch.rand(g.alloc_elems(), generator=torch.Generator(device=gpu).manual_seed(9), device=gpu)
+    s = torch.cuda.current_stream().cuda_stream
+    for lf in (0.05, 0.21):
+        both = torch.full_like(src, -3.0)
+        parts = torch.full_like(src, -3.0)
+        d = hip().stencil5_chunk_pass(src.data_ptr(), both.data_ptr(), g, S, 0.2, 0.2, "f32", 0, s, True,
+                                      lead_frac=lf, part="both")
+        assert d["check"] == "" and d["inner_cost"] > 0 and d["outer_cost"] > 0 and d["band"] >= S
+        for part in ("inner", "outer"):
+            hip().stencil5_chunk_pass(src.data_ptr(), parts.data_ptr(), g, S, 0.2, 0.2, "f32", 0, s, True,
+                                      lead_frac=lf, part=part)
+        torch.cuda.synchronize()
+        assert torch.equal(both, parts)
+    with pytest.raises(Exception):
+        hip().stencil5_chunk_pass(src.data_ptr(), parts.data_ptr(), g, S, 0.2, 0.2, "f32", 0, s, True, part="all")
+
+
 @pytest.mark.parametrize("w,h,S", [(4096, 2048, 24), (8192, 1024, 20), (5000, 1200, 24)])
 @pytest.mark.parametrize("opening", ["serial", "interior-first"])
 def test_rccl_solver_production_depth_per_step_bitwise(gpu, w, h, S, opening):
