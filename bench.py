@@ -369,16 +369,12 @@ def main(argv=None) -> int:
     p.add_argument("--dims", default=None,
                    help="process grid as ROWSxCOLS of ranks (default: MPI_Dims_create order 1x1, 2x1, 2x2, 4x2)")
     p.add_argument("--dtype", default="f32", choices=["f32", "f64"])
-    p.add_argument("--variant", default="auto", choices=["auto", "roll", "lds"])
     p.add_argument("--time-block", type=int, default=0,
                    help="Jacobi steps per halo exchange / kernel pass (0 = measured default per tile, kernels::auto_time_block: 20 or 24 for fp32)")
     p.add_argument("--no-sum-form", action="store_true",
                    help="per-step evaluation in the time-blocked kernels (bitwise equal to S single steps; "
                         "default: the sum form, c^S applied once per pass, for the equal default coefficients)")
     p.add_argument("--no-overlap", action="store_true")
-    p.add_argument("--no-fuse-periodic", action="store_true",
-                   help="N = 1: explicit self-exchange (copies into the ghost ring) + the ghost-ring pass instead "
-                        "of the wrap-around addressing")
     p.add_argument("--opening", default="auto", choices=["auto", "serial", "interior-first"],
                    help="multi-GPU: a call's opening super-step (its priming exchange) serial, or interior-first "
                         "(under the chunks that read only core cells); auto: prepare() times both on every rank "
@@ -470,12 +466,11 @@ def main(argv=None) -> int:
                         kind="jacobi5", backend=args.backend,
                         overlap=False if args.no_overlap else (True if args.overlap else None),
                         graph=not args.no_graph,
-                        variant=args.variant, time_block=args.time_block, loopback=args.loopback,
+                        time_block=args.time_block, loopback=args.loopback,
                         sum_form=not args.no_sum_form, opening=args.opening, rehearse_peers=args.rehearse_peers,
                         direct_halo=("validate" if args.direct_halo == "validate" else None),
                         halo_max_ctas=args.halo_max_ctas, wire_delay_us=args.wire_delay_us,
-                        direct_engine=args.direct_engine, steady=args.steady,
-                        fuse_periodic=not args.no_fuse_periodic)
+                        direct_engine=args.direct_engine, steady=args.steady)
     st = Stencil2D(cfg, ctx)
     window_sync = args.window_sync
     if window_sync == "auto":
