@@ -21,7 +21,7 @@
 #                          -st / -ss --steady interior-first / serial (default auto) (in that order,
 #                          e.g. ifirst-c16-w40-st); a final -aw runs it with ROC_ACTIVE_WAIT_TIMEOUT=2000
 #                          (the HIP runtime spins up to 2 ms on a wait before sleeping on an interrupt);
-#                          -cwNN --clock-warmup-ms NN, -t0 / -t1 --warm-tail 0 / 1 (checked first)
+#                          -cwNN --clock-warmup-ms NN, -tNN --warm-tail NN (checked first)
 #                          -> OUT/window_TILE.jsonl + medians
 #   py SCRIPT [ARGS]       python SCRIPT ARGS (experiment scripts under scripts/exp/) -> OUT/py.txt
 #   tune BIN FOCUS [ARGS]  an in-process tuner (build/bin/BIN with TUNE_FOCUS=FOCUS) -> OUT/tune_FOCUS.txt
@@ -99,8 +99,7 @@ task_window() {
       local base=$mode envs=()
       case $base in *-aw) envs+=(ROC_ACTIVE_WAIT_TIMEOUT=2000); base=${base%-aw} ;; esac
       if [[ $base =~ ^(.*)-cw([0-9]+)$ ]]; then args+=(--clock-warmup-ms "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi
-      case $base in *-t1) args+=(--warm-tail 1); base=${base%-t1} ;; esac
-      case $base in *-t0) args+=(--warm-tail 0); base=${base%-t0} ;; esac
+      if [[ $base =~ ^(.*)-t([0-9]+)$ ]]; then args+=(--warm-tail "${BASH_REMATCH[2]}"); base=${BASH_REMATCH[1]}; fi
       case $base in *-tsync) args+=(--window-sync torch); base=${base%-tsync} ;; esac
       case $base in *-ssync) args+=(--window-sync solver); base=${base%-ssync} ;; esac
       case $base in *-st) args+=(--steady interior-first); base=${base%-st} ;; esac
