@@ -378,7 +378,7 @@ std::atomic<bool> g_pipe_lag1{[] {
 }()};
 std::atomic<bool> g_pipe_deep{[] {
   const char* e = experiment_env("MXS_PIPE_DEEP");  // experiments build only
-  return e && std::string(e) == "1";
+  return !(e && std::string(e) == "0");
 }()};
 std::atomic<int> g_last_s0{0};
 std::atomic<bool> g_pipe_balanced{[] {
