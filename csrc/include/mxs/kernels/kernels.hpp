@@ -258,13 +258,6 @@ void set_pipe_lag1(bool on);
 bool pipe_lag1();
 // Whether the most recent stencil launch was a pipeline pass in that order.
 bool last_pipe_lag1();
-// Deeper stage 0 on long shares of wide tiles: fp32 S = 20 as 16 + 4 instead
-// of 12 + 8 in the sum and scaled forms (stencil_pipe.hpp kDeepMinShare).
-// Bitwise equal output. MXS_PIPE_DEEP=0 turns it off at start-up.
-void set_pipe_deep(bool on);
-bool pipe_deep();
-// Stage-0 levels of the most recent pipeline pass (0: not a joint pipeline pass).
-int last_pipe_s0();
 // Fill-aware workgroup shares of the pipeline passes (chunk_schedule.hpp:
 // balanced_starts; default on): a share that crosses a column-group boundary
 // pays a second pipeline fill, and with equal row shares those workgroups set

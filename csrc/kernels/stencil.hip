@@ -376,11 +376,6 @@ std::atomic<bool> g_pipe_lag1{[] {
   const char* e = experiment_env("MXS_PIPE_LAG1");  // experiments build only
   return !(e && std::string(e) == "0");
 }()};
-std::atomic<bool> g_pipe_deep{[] {
-  const char* e = experiment_env("MXS_PIPE_DEEP");  // experiments build only
-  return !(e && std::string(e) == "0");
-}()};
-std::atomic<int> g_last_s0{0};
 std::atomic<bool> g_pipe_balanced{[] {
   const char* e = experiment_env("MXS_PIPE_BALANCED");  // experiments build only
   return !(e && std::string(e) == "0");
@@ -393,9 +388,6 @@ bool pipe_joint() { return g_pipe_joint.load(std::memory_order_relaxed); }
 void set_pipe_lag1(bool on) { g_pipe_lag1.store(on, std::memory_order_relaxed); }
 bool pipe_lag1() { return g_pipe_lag1.load(std::memory_order_relaxed); }
 bool last_pipe_lag1() { return g_last_lag1.load(std::memory_order_relaxed); }
-void set_pipe_deep(bool on) { g_pipe_deep.store(on, std::memory_order_relaxed); }
-bool pipe_deep() { return g_pipe_deep.load(std::memory_order_relaxed); }
-int last_pipe_s0() { return g_last_s0.load(std::memory_order_relaxed); }
 void set_pipe_balanced(bool on) { g_pipe_balanced.store(on, std::memory_order_relaxed); }
 bool pipe_balanced_on() { return g_pipe_balanced.load(std::memory_order_relaxed); }
 namespace detail {
@@ -420,7 +412,6 @@ void pipe_starts(index_t groups, index_t rows, int blocks, index_t fill, PipeSha
 }
 void note_dispatch(const char* k) { note(k); }
 void note_pipe_lag1(bool lag1) { g_last_lag1.store(lag1, std::memory_order_relaxed); }
-void note_pipe_s0(int s0) { g_last_s0.store(s0, std::memory_order_relaxed); }
 }  // namespace detail
 
 #define MXS_INST_STENCIL(T)                                                                                    \

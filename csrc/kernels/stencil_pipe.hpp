@@ -17,7 +17,6 @@ namespace detail {
 
 void note_dispatch(const char* kernel);  // stencil.hip: last_stencil_dispatch() record
 void note_pipe_lag1(bool lag1);          // stencil.hip: last_pipe_lag1() record
-void note_pipe_s0(int s0);               // stencil.hip: last_pipe_s0() record
 
 // fp64 depths the wide-lane pipeline takes (S0 = S/2, S1 = S - S0 <= 8 levels
 // per stage: the windows fit 2 waves/SIMD without spilling).
@@ -82,14 +81,6 @@ constexpr index_t kLag1MaxChunkF64 = index_t(1) << 62;
 // With LAG1 (short chunks) S = 20 runs 8 + 12 below 12288 columns (8192^2:
 // 9.49 vs 9.36 for 12 + 8), else 12 + 8.
 constexpr index_t kJointWide = 12288;
-// From that width, shares of at least kDeepMinShare rows run S = 20 as 16 + 4
-// (888-column groups) in the sum and scaled forms: in shader cycles per
-// workgroup (tuner focus fillfit, TUNE_FILL_SET=deep0, 32768-wide tiles,
-// profiles/r06_deep) 16 + 4 costs 2.6% less than 12 + 8 on 4608-row shares
-// (the headline), 2.3% on 2304, 1.9% on 1184, 0.3% on 592, and 0.6% MORE on
-// 296. The per-step form keeps 12 + 8 (its 12-level stage is already at 244
-// VGPRs).
-constexpr index_t kDeepMinShare = 1024;
 
 // JS0: 0 = per-strip layout (pipe_s0 split), else joint windows with S0 = JS0.
 // XB = kScaledBody (with SUM): the scaled form's body (stencil_device.hpp).
@@ -170,7 +161,6 @@ void launch_pipe_form(const T* in, T* out, const TileGeom& g, index_t x0, index_
       in, out, g.pitch, g.core_offset(), g.width, g.height, x0, x1, y0, y1, shares, SUM ? sc : c0, kc);
   note_dispatch(XB == kScaledBody ? "stream_pipe_scaled" : SUM ? "stream_pipe_sum" : "stream_pipe");
   note_pipe_lag1(LAG1 != 0);
-  note_pipe_s0(JS0);
 }
 
 template <typename T, int S, bool WRAP, bool SUM, int XB = 0>
@@ -182,13 +172,6 @@ void launch_pipe_impl(const T* in, T* out, const TileGeom& g, index_t x0, index_
         if (pipe_lag1() && pipe_share<T, S, WRAP, SUM, 12>(x0, x1, y0, y1) <= kLag1MaxChunk) {
           if (x1 - x0 < kJointWide)
             return launch_pipe_form<T, S, WRAP, SUM, 8, kLagBoth, XB>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
-          if constexpr (SUM) {
-            // Periodic (WRAP): descending levels; the ascending 16-level stage
-            // with the wrap-around addressing spills (72 B at 256 VGPRs).
-            constexpr int kDeepLag = WRAP ? 0 : kLagBoth;
-            if (pipe_deep() && pipe_share<T, S, WRAP, SUM, 16>(x0, x1, y0, y1) >= kDeepMinShare)
-              return launch_pipe_form<T, S, WRAP, SUM, 16, kDeepLag, XB>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
-          }
           return launch_pipe_form<T, S, WRAP, SUM, 12, kLagBoth, XB>(in, out, g, x0, x1, y0, y1, c0, c1, sc, s);
         }
       } else if constexpr (sizeof(T) == 4 && S == 24) {

@@ -78,7 +78,6 @@ void launch_chunks(const T* in, T* out, const TileGeom& g, T c0, T c1, const Chu
       in, out, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, table, entries, c0, c1);
   note_dispatch(XB == kScaledBody ? "stream_pipe_scaled_chunks" : SUM ? "stream_pipe_sum_chunks" : "stream_pipe_chunks");
   note_pipe_lag1(LAG1 != 0);
-  note_pipe_s0(JS0);
 }
 
 template <typename T, int S, bool SUM, int XB = 0>

@@ -180,10 +180,6 @@ PYBIND11_MODULE(_mxs_hip, m) {
   m.def("set_pipe_lag1", &kernels::set_pipe_lag1, py::arg("on"),
         "ascending level order in the joint fp32 pipeline where it pays (default on; bitwise equal output)");
   m.def("pipe_lag1", &kernels::pipe_lag1);
-  m.def("set_pipe_deep", &kernels::set_pipe_deep, py::arg("on"),
-        "fp32 S = 20 as 16 + 4 on long shares of wide tiles (sum and scaled forms; default on; bitwise equal output)");
-  m.def("pipe_deep", &kernels::pipe_deep);
-  m.def("last_pipe_s0", &kernels::last_pipe_s0, "stage-0 levels of the most recent joint pipeline pass (0: other)");
   m.def("set_pipe_balanced", &kernels::set_pipe_balanced, py::arg("on"),
         "fill-aware workgroup shares in the pipeline passes (default on; bitwise equal output)");
   m.def("pipe_balanced", &kernels::pipe_balanced_on);

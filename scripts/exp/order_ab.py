@@ -10,11 +10,7 @@ the median clock. The order alternates first/second from round to round.
 Prints per tile the paired ratios asc / desc (median, notch) of wall time and
 of cycles.
 
---ab deep: the same paired windows with fp32 S = 20 as 16 + 4 on long shares of
-wide tiles (hip().set_pipe_deep(True), A) against 12 + 8 (B); "asc / desc" then
-reads 16 + 4 / 12 + 8.
-
-usage: python scripts/exp/order_ab.py [--tiles 32768x32768,16384x16384] [--rounds 12] [--steps 20] [--ab order|deep]
+usage: python scripts/exp/order_ab.py [--tiles 32768x32768,16384x16384] [--rounds 12] [--steps 20]
 """
 import argparse
 import json
@@ -46,7 +42,6 @@ def main() -> int:
     p.add_argument("--tiles", default="32768x32768,16384x16384")
     p.add_argument("--rounds", type=int, default=12)
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--ab", default="order", choices=["order", "deep"])
     args = p.parse_args()
     H = hip()
     K = H.clock_stamp_slots()
@@ -61,10 +56,7 @@ def main() -> int:
         res = {True: [], False: []}
         for r in range(args.rounds):
             for lag in ((True, False) if r % 2 == 0 else (False, True)):
-                if args.ab == "order":
-                    H.set_pipe_lag1(lag)
-                else:
-                    H.set_pipe_deep(lag)
+                H.set_pipe_lag1(lag)
                 st.warm(args.steps, 0.2, 1)
                 st.synchronize()
                 torch.cuda.synchronize()
@@ -75,7 +67,7 @@ def main() -> int:
                 st.synchronize()
                 torch.cuda.synchronize()
                 wall = (time.perf_counter() - t0) * 1e3
-                used = bool(H.last_pipe_lag1()) if args.ab == "order" else H.last_pipe_s0() == 16
+                used = bool(H.last_pipe_lag1())
                 H.clock_stamp(stamps.data_ptr() + 3 * K * 8, s)
                 torch.cuda.synchronize()
                 v = stamps.cpu().view(2, K, 3).tolist()
@@ -90,9 +82,8 @@ def main() -> int:
                 res[lag].append({"wall_ms": wall, "kcycles_slowest": wall * 1e3 * slow / 1e3, "mhz": med,
                                  "mhz_slowest": slow, "lag1_used": used})
         H.set_pipe_lag1(True)
-        H.set_pipe_deep(True)
         a, d = res[True], res[False]
-        rec = {"tile": tile, "ab": args.ab, "steps": args.steps, "rounds": args.rounds,
+        rec = {"tile": tile, "steps": args.steps, "rounds": args.rounds,
                "asc_wall_ms": round(statistics.median(x["wall_ms"] for x in a), 4),
                "desc_wall_ms": round(statistics.median(x["wall_ms"] for x in d), 4),
                "asc_mhz": round(statistics.median(x["mhz"] for x in a)),

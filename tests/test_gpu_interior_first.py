@@ -61,35 +61,6 @@ def test_chunk_pass_bitwise_vs_one_launch(gpu, w, h, S, dtype, sum_form):
     assert torch.equal(got, ref)
 
 
-@pytest.mark.parametrize("w,h,wrap,c0,c1", [
-    (32768, 8192, True, 0.2, 0.2),      # periodic: 16 + 4 descending, sum form (1184-row shares)
-    (32768, 8192, False, 0.2, 0.2),     # ghost ring: 16 + 4 ascending, sum form
-    (32768, 8192, True, 0.5, 0.125),    # periodic, scaled form
-    (24576, 10240, False, 0.5, 0.125),  # ghost ring, scaled form, 28 groups
-])
-def test_deep_stage0_bitwise(gpu, w, h, wrap, c0, c1):
-    """S = 20 as 16 + 4 (long shares of wide tiles) moves levels between the
-    stages only: bitwise the 12 + 8 pass."""
-    S = 20
-    g = core().TileGeom.aligned(w, h, 1 if wrap else S, 1 if wrap else S, 4)
-    src = torch.rand(g.alloc_elems(), generator=torch.Generator(device=gpu).manual_seed(w + h), device=gpu)
-    outs, s0 = [], []
-    old = hip().pipe_deep()
-    try:
-        for on in (True, False):
-            hip().set_pipe_deep(on)
-            dst = torch.full_like(src, -3.0)
-            hip().stencil5_tb(src.data_ptr(), dst.data_ptr(), g, S, 0, w, 0, h, c0, c1, wrap, "f32",
-                              torch.cuda.current_stream().cuda_stream, "auto", True, range=1.0)
-            s0.append(hip().last_pipe_s0())
-            torch.cuda.synchronize()
-            outs.append(dst)
-    finally:
-        hip().set_pipe_deep(old)
-    assert s0 == [16, 12]
-    assert torch.equal(outs[0], outs[1])
-
-
 def test_chunk_pass_parts_compose(gpu):
     """The interior-first pass's two launches one at a time (part="inner", then
     "outer", as scripts/exp/inner_alone.py times them) write what both together
