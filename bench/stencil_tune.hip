@@ -450,6 +450,13 @@ int main(int argc, char** argv) {
       fillfit<13, 7, 6, 3>("13+7_pf6_asc", in, out, g, hs, reps);
       return 0;
     }
+    if (set && std::string(set) == "deep0") {  // deeper stage 0: 16 + 4 (888-column groups) against 12 + 8
+      fillfit<12, 8, 6, 3>("12+8_pf6_asc", in, out, g, hs, reps);
+      fillfit<16, 4, 6, 3>("16+4_pf6_asc", in, out, g, hs, reps);
+      fillfit<12, 8, 6, 3>("12+8_pf6_asc_b", in, out, g, hs, reps);
+      fillfit<16, 4, 6, 3>("16+4_pf6_asc_b", in, out, g, hs, reps);
+      return 0;
+    }
     if (set && std::string(set) == "prod") {  // the forms the launcher picks: ascending <= 768-row shares, else descending
       fillfit<12, 8, 6, 3>("12+8_pf6_asc", in, out, g, hs, reps);
       fillfit<12, 8, 6, 0>("12+8_pf6_desc", in, out, g, hs, reps);
