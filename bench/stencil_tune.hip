@@ -345,7 +345,7 @@ Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullpt
   std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_b%d%s%s%s%s%s%s%s%s", S0, S1, PF, per_cu, WRAP ? "_wrap" : "",
                 PRIO == 1 ? "_prio0" : (PRIO == 2 ? "_prio1" : ""), SUM ? "_sum" : "",
                 G == 4 ? "" : (G == 2 ? "_g2" : "_g1"), XM ? "_xcd" : "", JOINT ? "_joint" : "", LAG1 == 3 ? "_lag1" : (LAG1 == 2 ? "_lag1s1" : (LAG1 == 1 ? "_lag1s0" : "")),
-                XB == 1 ? "_perm" : "");
+                XB == 1 ? "_perm" : (XB == 7 ? "_ntload" : ""));
   const float c0 = SUM ? float(std::pow(0.2, S0 + S1)) : 0.2f;  // sum form: c0 carries c^S
   auto mk = [=](const float* I, float* O) {
     return [=](hipStream_t s) {
@@ -715,6 +715,13 @@ int main(int argc, char** argv) {
       v.tol = 0.f;
       vs.push_back(v);
     }
+  } else if (focus && std::string(focus) == "ntload") {  // the headline pass with non-temporal input loads (r06)
+    const Variant a = pipe<12, 8, 6, true, 0, true, 4, false, true, 3>(in, out, g);
+    Variant b = pipe<12, 8, 6, true, 0, true, 4, false, true, 3, 7>(in, out, g);
+    b.ref = a.launch;
+    b.tol = 0.f;
+    vs.push_back(a);
+    vs.push_back(b);
   } else if (focus && std::string(focus) == "lag2head") {  // long-chunk tiles: the S = 20 / 24 candidates
     const Variant a = pipe<12, 8, 6, true, 0, true, 4, false, true>(in, out, g);
     Variant b = pipe<8, 12, 6, true, 0, true, 4, false, true, 2>(in, out, g);

@@ -453,6 +453,17 @@ template <>
 struct FastBody<float, true, 1> {
   using type = BodySumF32Perm;
 };
+// Non-temporal 16-byte loads of the fetching stage (TUNE_FOCUS=ntload): the
+// input rows are read once per pass.
+struct BodySumF32NT : BodySumF32 {
+  static __device__ __forceinline__ V load(const float* p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  }
+};
+template <>
+struct FastBody<float, true, 7> {
+  using type = BodySumF32NT;
+};
 template <>
 struct FastBody<double, true, 1> {
   using type = BodySumF64Perm;
