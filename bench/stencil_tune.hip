@@ -370,6 +370,40 @@ Variant pipe(const float* in, float* out, const TileGeom& g, float* tmp = nullpt
   return v;
 }
 
+// Row-band shares (TUNE_FOCUS=bands): every column group split into `per_group`
+// equal row bands, one per workgroup (groups x per_group workgroups, so some CUs
+// idle), so the workgroups of neighbouring groups stream the same rows at the
+// same time and the columns their joint windows both read (20 on each side)
+// can hit the memory-side cache for the second reader.
+template <int S0, int S1, int PF, int LAG1>
+Variant pipe_bands(const float* in, float* out, const TileGeom& g, int per_group, float* tmp = nullptr) {
+  constexpr int G = kWavesPerBlock, threads = 2 * G * kWaveSize;
+  constexpr int OWG = JointShape<S0, S1, G>::OWG;
+  const index_t groups = (g.width + OWG - 1) / OWG;
+  const int blocks = int(groups) * per_group;
+  MXS_CHECK(blocks <= kMaxShareBlocks, "pipe_bands: too many workgroups");
+  char buf[128];
+  std::snprintf(buf, sizeof(buf), "pipe_s%d+%d_pf%d_wrap_sum_joint_lag1_bands%d_b%d", S0, S1, PF, per_group, blocks);
+  const float c0 = float(std::pow(0.2, S0 + S1));
+  auto mk = [=](const float* I, float* O) {
+    return [=](hipStream_t s) {
+      PipeShares shares = PipeShares::equal(0);
+      shares.n = blocks;
+      for (int w = 0; w < blocks; ++w)
+        shares.start[w] = int(index_t(w / per_group) * g.height + (index_t(w % per_group) * g.height) / per_group);
+      shares.start[blocks] = int(groups * g.height);
+      stencil5_stream_pipe_kernel<S0, S1, PF, true, 0, float, true, G, false, true, LAG1, 0><<<blocks, threads, 0, s>>>(
+          I, O, g.pitch, g.core_offset(), g.width, g.height, 0, g.width, 0, g.height, shares, c0, 0.2f);
+    };
+  };
+  Variant v{buf, mk(in, out)};
+  v.launch2 = mk(out, const_cast<float*>(in));
+  v.steps = S0 + S1;
+  v.ref = ref_for<S0 + S1, true>(in, out, g, tmp);
+  v.tol = 2e-6f;
+  return v;
+}
+
 // Three-stage wave pipeline (S = S0 + S1 + S2 levels; 768-thread workgroups).
 template <int S0, int S1, int S2, int PF, bool WRAP = true, bool SUM = true>
 Variant pipe3(const float* in, float* out, const TileGeom& g, float* tmp = nullptr) {
@@ -714,6 +748,15 @@ int main(int argc, char** argv) {
       v.ref = a.launch;
       v.tol = 0.f;
       vs.push_back(v);
+    }
+  } else if (focus && std::string(focus) == "bands") {  // row-band shares (memory-side cache reuse), r06
+    const Variant a = pipe<12, 8, 6, true, 0, true, 4, false, true, 3>(in, out, g);
+    vs.push_back(a);
+    for (int pg : {7}) {
+      Variant b = pipe_bands<12, 8, 6, 3>(in, out, g, pg);
+      b.ref = a.launch;
+      b.tol = 0.f;
+      vs.push_back(b);
     }
   } else if (focus && std::string(focus) == "ntload") {  // the headline pass with non-temporal input loads (r06)
     const Variant a = pipe<12, 8, 6, true, 0, true, 4, false, true, 3>(in, out, g);
